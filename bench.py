@@ -1,0 +1,194 @@
+"""Benchmark: device-resident block checksums on MI355X (BASELINE.json metric).
+
+One step = checksum every block of the per-GPU workload (XXH64 seed 0 =
+storm's blocks.Checksum, /root/reference/blocks/checksum.go:15-17), build the
+shard's Merkle pointer tree over the checksums, and (N > 1) all-gather the shard
+roots over RCCL and hash the combining pointer block.
+
+Workload (N = 1): BASELINE.json configs[2] — 16M x 32 KiB blocks (512 GiB) per
+GPU. 512 GiB exceeds one MI355X's 288 GB of HBM, so the blocks stream through a
+resident 4M-block (128 GiB) arena, 4 passes per step; the arena
+holds synthetic blocks written by the on-device generator before timing. XXH64
+cost is data-independent; full-size parity of the 16M logical set is tested by
+tests/test_gpu_parity.py::test_c3_16m_blocks_digest (arena regenerated per pass).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU, RCCL)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "GiB/s device-resident block checksum; % of MI355X HBM roofline"
+HBM_PEAK_GBS = 8000.0  # MI355X spec, /opt/skills/guides/MI355X_MICROARCH.md (chip-level parameters)
+BLOCK = 32768          # blocks.BlockSize, /root/reference/blocks/types.go:4
+FANOUT = 1200          # pointer.PointersPerBlock, /root/reference/blocks/pointer/params.go:6
+REV = 1
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=5)
+    p.add_argument("--warmup", type=int, default=2)
+    p.add_argument("--blocks", type=int, default=16 << 20, help="blocks per GPU per step")
+    p.add_argument("--arena", type=int, default=4 << 20, help="resident arena (blocks)")
+    p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget (rank 0, N=1)")
+    p.add_argument("--no-cpu", action="store_true")
+    return p.parse_args()
+
+
+def cpu_baseline(seconds: float):
+    """Oracle C restatement (port of XXH64 = xxhash.Sum64) on the host, 1 thread,
+    over a bounded sample of the same synthetic 32 KiB blocks. Also timed on all
+    threads of this process's CPU share (reported as an extra field)."""
+    import numpy as np
+    from oracle import oracle as o
+
+    n = 2048  # 64 MiB sample, regenerated identically to the GPU arena's first blocks
+    buf = o.fill_synthetic(n, BLOCK, 0)
+    out = o.checksum_batch(buf, n, BLOCK, BLOCK)  # warm
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        out = o.checksum_batch(buf, n, BLOCK, BLOCK)
+        reps += 1
+        el = time.perf_counter() - t0
+        if el >= seconds * 0.75:
+            break
+    one = reps * n * BLOCK / el / 2**30
+    threads = min(16, len(os.sched_getaffinity(0)))
+    reps_mt, t0 = 0, time.perf_counter()
+    while True:
+        o.checksum_batch(buf, n, BLOCK, BLOCK, threads=threads)
+        reps_mt += 1
+        el_mt = time.perf_counter() - t0
+        if el_mt >= seconds * 0.25:
+            break
+    multi = reps_mt * n * BLOCK / el_mt / 2**30
+    assert int(out[0]) == int(o.checksum_batch(buf[:BLOCK], 1, BLOCK, BLOCK)[0])
+    return {"value": round(one, 3), "unit": "GiB/s", "cores": 1, "kind": "port",
+            "sample": f"{n} x 32 KiB synthetic blocks (64 MiB) hashed {reps}x in {el:.1f} s by oracle/xxh64_oracle.c "
+                      f"(-O3, 1 thread); Go reference unbuildable here (no Go toolchain)",
+            "all_threads": {"value": round(multi, 3), "threads": threads}}
+
+
+def main():
+    a = parse()
+    import numpy as np
+    import torch
+
+    from storm_amd import dist as sdist
+    from storm_amd import engine
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+    engine.init(local)
+
+    n_gpu = a.blocks                      # weak scaling: fixed blocks per GPU
+    n_total = n_gpu * world
+    lo = rank * n_gpu
+    arena_n = min(a.arena, n_gpu)
+    passes = (n_gpu + arena_n - 1) // arena_n
+    stream = torch.cuda.current_stream(dev)
+    st = stream.cuda_stream
+
+    arena = torch.empty((arena_n, BLOCK), dtype=torch.uint8, device=dev)
+    engine.fill_synthetic_device(arena.data_ptr(), BLOCK, arena_n, lo, 0x53544F524D, st)
+    cs = torch.empty(n_gpu, dtype=torch.int64, device=dev)
+    ws = torch.empty(max(engine.merkle_workspace_bytes(n_gpu, FANOUT) // 8, 1), dtype=torch.int64, device=dev)
+    torch.cuda.synchronize()
+
+    ev = []  # (start, end) events around every hash-kernel launch of the timed steps
+
+    def step(record: bool):
+        for p in range(passes):
+            cnt = min(arena_n, n_gpu - p * arena_n)
+            if record:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+            engine.checksum_device(arena.data_ptr(), BLOCK, cnt, cs[p * arena_n:].data_ptr(), BLOCK, 0, st)
+            if record:
+                e1.record(stream)
+                ev.append((e0, e1, cnt))
+        root = engine.merkle_root_tensor(cs, lo, sdist.shard_node_addr_base(n_total, lo), REV, FANOUT, ws)
+        if world > 1:
+            root, _ = sdist.global_root(root, REV, n_total, lambda t, r, ad: engine.combine_roots_tensor(t, r, ad, FANOUT))
+        return root
+
+    for _ in range(a.warmup):
+        step(False)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        root = step(True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # dominant kernel: average launch duration from HIP events on its stream
+    kms = [e0.elapsed_time(e1) for (e0, e1, _) in ev]
+    kblocks = [c for (_, _, c) in ev]
+    avg_ms = sum(kms) / len(kms)
+    avg_blocks = sum(kblocks) / len(kblocks)
+    alg_bytes = avg_blocks * (BLOCK + 8)          # L bytes read + 8 bytes written per block
+    achieved = alg_bytes / (avg_ms * 1e-3) / 1e9  # GB/s (decimal, like the spec peak)
+
+    total_bytes = n_total * BLOCK * a.steps
+    value = total_bytes / elapsed / 2**30
+    traffic = None
+    tpath = os.path.join(ROOT, "profiles", "traffic.json")
+    if os.path.exists(tpath):
+        with open(tpath) as f:
+            tj = json.load(f)
+        if tj.get("arena_blocks") == arena_n:
+            traffic = tj.get("hbm_bytes_per_launch")
+
+    if rank == 0:
+        root_t = engine.as_tuple(root)
+        res = {
+            "metric": METRIC, "value": round(value, 2), "unit": "GiB/s", "n_gpus": world, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u64", "data": "synthetic",
+            "config": {"workload": "c3: 16M x 32 KiB blocks per GPU, XXH64 seed 0 (blocks.Checksum) "
+                                   "+ shard Merkle pointer tree" + (" + RCCL all-gather of shard roots" if world > 1 else ""),
+                       "blocks_per_gpu": n_gpu, "block_bytes": BLOCK, "arena_blocks": arena_n,
+                       "passes_per_step": passes, "parallelism": f"dp{world} (contiguous block ranges)"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "kernel": "k_xxh64_quad<16>", "avg_launch_ms": round(avg_ms, 4),
+                         "algorithmic_bytes_per_launch": int(alg_bytes)},
+            "root": "0x%016x" % root_t[0],
+        }
+        if world == 1 and not a.no_cpu:
+            res["cpu_baseline"] = cpu_baseline(a.cpu_seconds)
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

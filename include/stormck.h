@@ -1,0 +1,146 @@
+/*
+ * stormck — MI355X-native block-checksum engine for storm (C ABI).
+ *
+ * Drop-in boundary for storm's per-block content hash (Go package `blocks`):
+ *
+ *   func Checksum(b []byte) Hash                         /root/reference/blocks/checksum.go:15-17
+ *   func BlockChecksum[T Block](b *T) Hash               /root/reference/blocks/checksum.go:10-12
+ *   func VerifyChecksum(address, p, expected) error      /root/reference/blocks/checksum.go:20-27
+ *   type Pointer struct{Checksum, Address, BirthRevision} /root/reference/blocks/types.go:35-39
+ *
+ * The hash is XXH64 with seed 0 (github.com/cespare/xxhash/v2 v2.2.0 Sum64,
+ * /root/reference/go.mod:6), bit-exact. All entry points are plain C: pointers and
+ * sizes only. Every function returns 0 on success or a negative STORMCK_E* code;
+ * stormck_last_error() then holds a thread-local message.
+ *
+ * "_device" entry points take device pointers (HBM) and a hipStream_t passed as
+ * void* (NULL = the null stream of the calling thread's current device); they are
+ * asynchronous with respect to the host, like any kernel launch on that stream.
+ * "_host" entry points take host memory and return when the results are in host
+ * memory (H2D -> kernel -> D2H, pipelined).
+ *
+ * There is no CPU fallback: without a usable gfx950 device every compute entry
+ * point returns STORMCK_ENODEV.
+ */
+#ifndef STORMCK_H
+#define STORMCK_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define STORMCK_ABI_VERSION 1
+
+#define STORMCK_OK 0
+#define STORMCK_EINVAL (-1)  /* bad argument (null pointer, n/len/stride out of range, ...) */
+#define STORMCK_EHIP (-2)    /* HIP runtime error */
+#define STORMCK_ENODEV (-3)  /* no usable gfx950 device */
+#define STORMCK_ENOMEM (-4)  /* device / pinned allocation failed */
+#define STORMCK_EMISMATCH (-5) /* verify: at least one checksum differs (see first_bad) */
+
+/* storm block types, blocks/types.go:7-15 */
+#define STORMCK_FREE_BLOCK 0
+#define STORMCK_POINTER_BLOCK 1
+#define STORMCK_LEAF_BLOCK 2
+
+/* storm's PointersPerBlock (blocks/pointer/params.go:6; 10 under the `test` build tag,
+ * blocks/pointer/params_testing.go:6). */
+#define STORMCK_POINTERS_PER_BLOCK 1200
+
+/* blocks.Pointer, 24 bytes, Go amd64 layout (blocks/types.go:35-39). */
+typedef struct stormck_pointer {
+    uint64_t checksum;
+    uint64_t address;
+    uint64_t birth_revision;
+} stormck_pointer;
+
+/* ---- library / device ---------------------------------------------------- */
+
+int stormck_abi_version(void);
+const char* stormck_last_error(void);
+/* Number of visible gfx950 devices (0 on a machine without one). */
+int stormck_device_count(int* count);
+/* Select `device` for the calling thread and create its context (lazy otherwise). */
+int stormck_init(int device);
+/* Free pinned staging / device buffers of every context. */
+void stormck_shutdown(void);
+
+/* ---- hot path: batch checksums of device-resident blocks -------------------
+ * Block i starts at d_base + i*stride and is (d_lens ? d_lens[i] : len) bytes
+ * long. out[i] = XXH64(block i) = blocks.Checksum(block bytes). Any alignment is
+ * accepted; 8-byte-aligned blocks take the fast path. n == 0 is a no-op. */
+int stormck_checksum_device(const void* d_base, uint64_t stride, const uint32_t* d_lens, uint32_t len,
+                            uint64_t n, uint64_t* d_out, void* stream);
+
+/* Same, block i at d_base + d_offsets[i] (e.g. the dirty slots of storm's cache.data,
+ * /root/reference/cache/cache.go:36-40). */
+int stormck_checksum_gather_device(const void* d_base, const uint64_t* d_offsets, const uint32_t* d_lens,
+                                   uint32_t len, uint64_t n, uint64_t* d_out, void* stream);
+
+/* Batched blocks.VerifyChecksum. d_result[0] = index of the first block whose checksum
+ * differs from d_expected (n if none), d_result[1] = number of mismatches. The result
+ * is written on `stream` (no host sync); check it after synchronising. */
+int stormck_verify_device(const void* d_base, uint64_t stride, const uint32_t* d_lens, uint32_t len,
+                          uint64_t n, const uint64_t* d_expected, uint64_t* d_result, void* stream);
+
+/* ---- host-memory batch (starts and ends in host memory) -------------------- */
+
+/* out[i] = XXH64 of host block i (base + i*stride, lens ? lens[i] : len). Pipelined
+ * H2D / kernel / D2H through library-owned pinned staging on the calling thread's
+ * current device; memory registered with stormck_host_register is DMA'd directly. */
+int stormck_checksum_host(const void* base, uint64_t stride, const uint32_t* lens, uint32_t len, uint64_t n,
+                          uint64_t* out);
+/* Batched verify of host blocks: *first_bad = first mismatching index (n if none),
+ * *n_bad = mismatch count. Returns STORMCK_EMISMATCH if n_bad > 0. */
+int stormck_verify_host(const void* base, uint64_t stride, const uint32_t* lens, uint32_t len, uint64_t n,
+                        const uint64_t* expected, uint64_t* first_bad, uint64_t* n_bad);
+/* Single-buffer blocks.Checksum through the device (batch of one). */
+int stormck_checksum(const void* p, uint64_t n_bytes, uint64_t* out);
+/* Page-lock a host range so the host path can DMA from it without staging copies. */
+int stormck_host_register(void* p, uint64_t bytes);
+int stormck_host_unregister(void* p);
+
+/* ---- Merkle pointer tree (storm pointer.Block nodes) -----------------------
+ * One level: children are entries {cs[i], child_addr_base + i, rev}, all of type
+ * child_type. Parent j packs children [j*fanout, min((j+1)*fanout, m)) into a storm
+ * pointer.Block (blocks/pointer/block.go:10-13; size = 25*fanout rounded up to 8
+ * bytes, unused slots zero) and d_parent_cs[j] = XXH64(that block). The node bytes
+ * are never materialised: each word is synthesised from the child arrays. */
+int stormck_pointer_level_device(const uint64_t* d_child_cs, uint64_t m, uint64_t child_addr_base,
+                                 uint64_t rev, uint8_t child_type, uint32_t fanout, uint64_t* d_parent_cs,
+                                 void* stream);
+/* One node from explicit entries (d_entries[0..count), d_types[0..count)), count <=
+ * fanout. Writes *d_out_cs. Used to combine per-shard roots. */
+int stormck_pointer_node_device(const stormck_pointer* d_entries, const uint8_t* d_types, uint32_t count,
+                                uint32_t fanout, uint64_t* d_out_cs, void* stream);
+/* Materialise pointer blocks of one level (same rule as pointer_level) into
+ * d_blocks (pm blocks at dst_stride bytes), e.g. to be written to storage. */
+int stormck_pack_pointer_blocks_device(const uint64_t* d_child_cs, uint64_t m, uint64_t child_addr_base,
+                                       uint64_t rev, uint8_t child_type, uint32_t fanout, void* d_blocks,
+                                       uint64_t dst_stride, void* stream);
+/* Workspace bytes stormck_merkle_root_device needs for n leaves. */
+uint64_t stormck_merkle_workspace_bytes(uint64_t n, uint32_t fanout);
+/* Whole shard tree (DESIGN.md "Shard Merkle tree"): leaves {d_leaf_cs[i],
+ * leaf_addr_base + i, rev} of type Leaf; interior nodes get addresses
+ * node_addr_base, node_addr_base+1, ... level by level, bottom-up. Writes the root
+ * Pointer to *d_root and its type to *d_root_type (device memory). n == 0 -> zero root,
+ * type Free; n == 1 -> the leaf's own pointer, type Leaf. */
+int stormck_merkle_root_device(const uint64_t* d_leaf_cs, uint64_t n, uint64_t leaf_addr_base,
+                               uint64_t node_addr_base, uint64_t rev, uint32_t fanout, void* d_workspace,
+                               uint64_t workspace_bytes, stormck_pointer* d_root, uint8_t* d_root_type,
+                               void* stream);
+
+/* ---- synthetic data (benchmarks / tests) -----------------------------------
+ * Word w of block i = splitmix64(seed ^ (((first + i) << 20) + w)), w < stride/8,
+ * little-endian. stride % 16 == 0, d_dst 16-byte aligned. */
+int stormck_fill_synthetic_device(void* d_dst, uint64_t stride, uint64_t n, uint64_t first, uint64_t seed,
+                                  void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* STORMCK_H */

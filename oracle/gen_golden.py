@@ -1,0 +1,252 @@
+"""Generate the golden fixtures under tests/golden/ (run in the build container only).
+
+ORACLE / TEST INFRASTRUCTURE. The checksum values come from python-xxhash 3.8.1
+(bundled libxxhash 0.8.2) — the canonical XXH64 implementation, independent of
+both the C restatement (oracle/xxh64_oracle.c) and the HIP kernels. storm's own
+hash is github.com/cespare/xxhash/v2 v2.2.0 Sum64 (/root/reference/go.mod:6),
+which is XXH64 seed 0; the Go reference cannot run here (no Go toolchain, SURVEY
+§8c), and no reference test asserts an absolute checksum value, so
+these fixtures plus the public XXH64 known answers are what pins parity.
+
+Block contents, layouts and trees are rebuilt here with numpy/struct code of
+this file alone (independent of oracle/oracle.py and storm_amd/).
+
+    python oracle/gen_golden.py          # small fixtures (seconds)
+    python oracle/gen_golden.py --big    # + 1M / 16M synthetic-block digests (minutes)
+"""
+from __future__ import annotations
+
+import ctypes
+import json
+import os
+import struct
+import sys
+import time
+
+import numpy as np
+import xxhash
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+OUT = os.path.join(ROOT, "tests", "golden")
+SEED = 0x53544F524D
+M64 = (1 << 64) - 1
+STORM_LENGTHS = [72, 256, 536, 728, 28808, 30000, 31808, 32768]
+
+
+def h(v: int) -> str:
+    return "0x%016x" % v
+
+
+def xx(b) -> int:
+    return xxhash.xxh64_intdigest(bytes(b), seed=0)
+
+
+def splitmix_np(x: np.ndarray) -> np.ndarray:
+    with np.errstate(over="ignore"):
+        z = x + np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return z ^ (z >> np.uint64(31))
+
+
+def synth_blocks(first: int, n: int, stride: int, seed: int = SEED) -> np.ndarray:
+    """word w of block i = splitmix64(seed ^ ((i << 20) + w))."""
+    words = stride // 8
+    i = np.arange(first, first + n, dtype=np.uint64)[:, None]
+    w = np.arange(words, dtype=np.uint64)[None, :]
+    key = np.uint64(seed) ^ ((i << np.uint64(20)) + w)
+    return splitmix_np(key).astype("<u8").view(np.uint8).reshape(n, stride)
+
+
+def write(name: str, obj) -> None:
+    os.makedirs(OUT, exist_ok=True)
+    path = os.path.join(OUT, name)
+    with open(path, "w") as f:
+        json.dump(obj, f, indent=1, sort_keys=True)
+        f.write("\n")
+    print("wrote", path, os.path.getsize(path), "bytes")
+
+
+# ---------------------------------------------------------------------------
+def gen_kat() -> None:
+    public = {"": 0xEF46DB3751D8E999, "a": 0xD24EC4F1A98C6E5B, "abc": 0x44BC2CF5AD770999}
+    for s, v in public.items():
+        assert xx(s.encode()) == v, s  # published XXH64 answers agree with libxxhash
+    lengths = list(range(0, 129)) + STORM_LENGTHS + [1000, 4096, 32767, 32769, 65536]
+    rows = []
+    for n in lengths:
+        zeros = bytes(n)
+        iota = bytes(i & 0xFF for i in range(n))
+        rows.append({"len": n, "zeros": h(xx(zeros)), "iota": h(xx(iota))})
+    write("kat.json", {
+        "source": "libxxhash 0.8.2 via python-xxhash 3.8.1, XXH64 seed 0",
+        "public": {k: h(v) for k, v in public.items()},
+        "patterns": {"zeros": "n zero bytes", "iota": "byte i = i & 0xff"},
+        "rows": rows,
+    })
+
+
+def gen_synth_c1() -> None:
+    n, stride = 1024, 32768
+    blocks = synth_blocks(0, n, stride)
+    cs = np.array([xx(blocks[i]) for i in range(n)], dtype=np.uint64)
+    samples = []
+    for (i, w) in [(0, 0), (0, 1), (1, 0), (7, 4095), (1023, 17), (1023, 4095)]:
+        samples.append({"block": i, "word": w, "value": h(int(blocks[i].view("<u8")[w]))})
+    write("synth_c1.json", {
+        "config": "c1: 1K x 32 KiB synthetic blocks (BASELINE.json configs[0] restated)",
+        "rule": "word w of block i = splitmix64(seed ^ ((i << 20) + w)), little-endian",
+        "seed": h(SEED), "n": n, "stride": stride, "length": stride,
+        "checksums": [h(int(v)) for v in cs],
+        "digest": h(xx(cs.astype("<u8").tobytes())),
+        "generator_samples": samples,
+    })
+
+
+def mixed_lengths() -> list:
+    # config c5: objectlist / pointer / singularity / blob / spacelist lengths plus the
+    # test-tag sizes and odd lengths that exercise every tail path.
+    mix = [31808] * 24 + [30000, 72, 32768, 28808, 256, 536, 728] + \
+          [0, 1, 3, 4, 7, 8, 15, 16, 31, 32, 33, 63, 64, 100, 1000, 4097, 32767]
+    rng = np.random.default_rng(5)
+    rng.shuffle(mix)
+    return [int(x) for x in mix]
+
+
+def gen_mixed() -> None:
+    lens = mixed_lengths()
+    n, stride = len(lens), 32768
+    blocks = synth_blocks(1 << 30, n, stride)
+    cs = [h(xx(blocks[i][:lens[i]])) for i in range(n)]
+    write("mixed.json", {
+        "config": "c5: mixed storm block lengths (objectlist/pointer/singularity/blob/spacelist + tails)",
+        "seed": h(SEED), "first": 1 << 30, "stride": stride, "lens": lens, "checksums": cs,
+    })
+
+
+# ---- storm layouts (Go amd64) ---------------------------------------------
+def pack_pointer_block(entries, fanout: int) -> bytes:
+    size = (25 * fanout + 7) & ~7
+    buf = bytearray(size)
+    for k, (cs, addr, rev, typ) in enumerate(entries):
+        struct.pack_into("<QQQ", buf, 24 * k, cs, addr, rev)
+        buf[24 * fanout + k] = typ
+    return bytes(buf)
+
+
+def tree_root(leaf_cs, leaf_base: int, node_base: int, rev: int, fanout: int):
+    n = len(leaf_cs)
+    if n == 0:
+        return (0, 0, 0, 0)
+    entries = [(int(leaf_cs[i]), leaf_base + i, rev) for i in range(n)]
+    typ, nxt = 2, node_base
+    while len(entries) > 1:
+        parents = []
+        for j in range(0, len(entries), fanout):
+            chunk = entries[j:j + fanout]
+            node = pack_pointer_block([(c, a, r, typ) for (c, a, r) in chunk], fanout)
+            parents.append((xx(node), nxt + len(parents), rev))
+        nxt += len(parents)
+        entries, typ = parents, 1
+    c, a, r = entries[0]
+    return (c, a, r, typ)
+
+
+def gen_merkle() -> None:
+    cases = []
+    specs = [(0, 1200), (1, 1200), (2, 1200), (1199, 1200), (1200, 1200), (1201, 1200), (5000, 1200),
+             (1, 10), (10, 10), (11, 10), (101, 10), (1000, 10), (12345, 10), (1_000_000, 1200)]
+    for n, f in specs:
+        leaf = splitmix_np(np.arange(n, dtype=np.uint64) ^ np.uint64(SEED))
+        leaf_base, rev = 7 * n + 3, 5
+        node_base = leaf_base + n
+        t = time.time()
+        root = tree_root(leaf, leaf_base, node_base, rev, f)
+        cases.append({"n": n, "fanout": f, "leaf_addr_base": leaf_base, "node_addr_base": node_base, "rev": rev,
+                      "root": [h(v) for v in root[:3]], "root_type": root[3]})
+        print(f"  merkle n={n} F={f} {time.time() - t:.1f}s")
+    # combine: 8 shard roots of the 1M-leaf tree split 8 ways (storm_amd.dist semantics)
+    n_total, world, rev, f = 1_000_000, 8, 5, 1200
+    leaf = splitmix_np(np.arange(n_total, dtype=np.uint64) ^ np.uint64(SEED))
+    table = []
+    for r in range(world):
+        q, rem = divmod(n_total, world)
+        lo = r * q + min(r, rem)
+        hi = lo + q + (1 if r < rem else 0)
+        table.append(tree_root(leaf[lo:hi], lo, n_total + lo, rev, f))
+    groot = (xx(pack_pointer_block(table, f)), 2 * n_total, rev, 1)
+    write("merkle.json", {
+        "leaf_rule": "leaf_cs[i] = splitmix64(i ^ seed)", "seed": h(SEED), "cases": cases,
+        "combine": {"n_total": n_total, "world": world, "rev": rev, "fanout": f,
+                    "shard_roots": [[h(v) for v in t[:3]] + [t[3]] for t in table],
+                    "global_root": [h(v) for v in groot[:3]] + [groot[3]]},
+    })
+
+
+def gen_layouts() -> None:
+    # Sizes from Go's layout rules, computed by hand here (cross-checks storm_amd.layouts).
+    sizes = {"prod": {"singularity": 72, "pointer": 30000, "spacelist": 28808, "objectlist": 31808, "blob": 32768},
+             "test": {"singularity": 72, "pointer": 256, "spacelist": 728, "objectlist": 536, "blob": 32768}}
+    zero = {tag: {k: h(xx(bytes(v))) for k, v in d.items()} for tag, d in sizes.items()}
+    # singularity block after persistence.Initialize-like fill (fields at 0/8/16/24, Pointer 32..55,
+    # type 56, LastAllocatedBlock 64; Checksum hashed as 0: cache/cache.go:71-73)
+    sb = bytearray(72)
+    struct.pack_into("<QQQQ", sb, 0, 0, 0x73746F726D, 3, 1 << 20)
+    struct.pack_into("<QQQ", sb, 32, 0x1122334455667788, 42, 2)
+    sb[56] = 2
+    struct.pack_into("<Q", sb, 64, 777)
+    # pointer-block sequence of /root/reference/blocks/pointer/block_test.go:15-34 (prod fanout)
+    seq = []
+    f = 1200
+    pb = bytearray(30000)
+    seq.append(xx(pb))
+    struct.pack_into("<Q", pb, 0, 2); seq.append(xx(pb))                 # Pointers[0].Checksum = 2
+    pb[24 * f + 0] = 2; seq.append(xx(pb))                               # PointedBlockTypes[0] = Leaf
+    pb[24 * f + 1] = 2; seq.append(xx(pb))                               # PointedBlockTypes[1] = Leaf
+    struct.pack_into("<Q", pb, 24 + 8, 2); seq.append(xx(pb))            # Pointers[1].Address = 2
+    struct.pack_into("<Q", pb, 48, 4); seq.append(xx(pb))                # Pointers[2].Checksum = 4
+    # blob block with the 4 objects of /root/reference/blocks/blob/block_test.go:19-37
+    blob = bytearray(32768)
+    items = [(1, 2, 3, 1), (4, 5, 6, 2), (7, 8, 9, 0), (10, 11, 12, 1)]
+    for k, (tag, f1, f2, st) in enumerate(items):
+        struct.pack_into("<QQBxxxxxxxB", blob, 32 * k, tag, f1, f2, st)
+    write("layouts.json", {
+        "sizes": sizes, "zero_block_checksums": zero,
+        "singularity_example": {"bytes_hex": bytes(sb).hex(), "checksum": h(xx(sb))},
+        "pointer_block_test_sequence": [h(v) for v in seq],
+        "blob_test_block": {"first_128_hex": bytes(blob[:128]).hex(), "checksum": h(xx(blob))},
+    })
+
+
+def gen_big() -> None:
+    """Digests (XXH64 of the little-endian checksum array) of the c2 (1M) and c3 (16M)
+    synthetic 32 KiB block sets. Blocks are generated with the C oracle's generator
+    (pinned against synth_c1.json's numpy words) and hashed with libxxhash."""
+    sys.path.insert(0, ROOT)
+    from oracle import oracle as o  # generator only; hashing stays libxxhash
+    stride = 32768
+    res = {}
+    for n in (1 << 20, 1 << 24):
+        t = time.time()
+        chunk = 1 << 14
+        cs = np.empty(n, dtype=np.uint64)
+        for first in range(0, n, chunk):
+            buf = o.fill_synthetic(chunk, stride, first)
+            mv = memoryview(buf)
+            cs[first:first + chunk] = [xxhash.xxh64_intdigest(mv[i * stride:(i + 1) * stride]) for i in range(chunk)]
+        res[str(n)] = {"digest": h(xx(cs.astype("<u8").tobytes())),
+                       "first8": [h(int(v)) for v in cs[:8]], "last": h(int(cs[-1])),
+                       "every_65536th": [h(int(v)) for v in cs[::65536]]}
+        print(f"  big n={n} {time.time() - t:.0f}s")
+    write("synth_digests.json", {"rule": "synth_c1.json rule, first = 0, stride = length = 32768",
+                                 "seed": h(SEED), "digests": res})
+
+
+if __name__ == "__main__":
+    gen_kat()
+    gen_synth_c1()
+    gen_mixed()
+    gen_layouts()
+    gen_merkle()
+    if "--big" in sys.argv:
+        gen_big()

@@ -1,0 +1,99 @@
+"""ctypes binding of libstormck (include/stormck.h).
+
+Loads the in-tree build ``storm_amd/lib/libstormck.so``. There is no fallback:
+if the library is missing, importing this module raises; if no gfx950 device is
+present, every compute call raises :class:`NoDeviceError`.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, c_char_p, c_int, c_uint8, c_uint32, c_uint64, c_void_p
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libstormck.so")
+
+OK = 0
+EINVAL = -1
+EHIP = -2
+ENODEV = -3
+ENOMEM = -4
+EMISMATCH = -5
+
+
+class StormckError(RuntimeError):
+    """A libstormck call failed (code < 0)."""
+
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"stormck error {code}: {msg}")
+        self.code = code
+
+
+class NoDeviceError(StormckError):
+    pass
+
+
+class PointerStruct(ctypes.Structure):
+    """stormck_pointer == blocks.Pointer (/root/reference/blocks/types.go:35-39)."""
+
+    _fields_ = [("Checksum", c_uint64), ("Address", c_uint64), ("BirthRevision", c_uint64)]
+
+
+# name -> (restype, argtypes); mirrors include/stormck.h one to one.
+SIGNATURES = {
+    "stormck_abi_version": (c_int, []),
+    "stormck_last_error": (c_char_p, []),
+    "stormck_device_count": (c_int, [POINTER(c_int)]),
+    "stormck_init": (c_int, [c_int]),
+    "stormck_shutdown": (None, []),
+    "stormck_checksum_device": (c_int, [c_void_p, c_uint64, c_void_p, c_uint32, c_uint64, c_void_p, c_void_p]),
+    "stormck_checksum_gather_device": (c_int, [c_void_p, c_void_p, c_void_p, c_uint32, c_uint64, c_void_p, c_void_p]),
+    "stormck_verify_device": (c_int, [c_void_p, c_uint64, c_void_p, c_uint32, c_uint64, c_void_p, c_void_p, c_void_p]),
+    "stormck_checksum_host": (c_int, [c_void_p, c_uint64, c_void_p, c_uint32, c_uint64, c_void_p]),
+    "stormck_verify_host": (c_int, [c_void_p, c_uint64, c_void_p, c_uint32, c_uint64, c_void_p, c_void_p, c_void_p]),
+    "stormck_checksum": (c_int, [c_void_p, c_uint64, POINTER(c_uint64)]),
+    "stormck_host_register": (c_int, [c_void_p, c_uint64]),
+    "stormck_host_unregister": (c_int, [c_void_p]),
+    "stormck_pointer_level_device": (c_int, [c_void_p, c_uint64, c_uint64, c_uint64, c_uint8, c_uint32, c_void_p, c_void_p]),
+    "stormck_pointer_node_device": (c_int, [c_void_p, c_void_p, c_uint32, c_uint32, c_void_p, c_void_p]),
+    "stormck_pack_pointer_blocks_device": (
+        c_int, [c_void_p, c_uint64, c_uint64, c_uint64, c_uint8, c_uint32, c_void_p, c_uint64, c_void_p]),
+    "stormck_merkle_workspace_bytes": (c_uint64, [c_uint64, c_uint32]),
+    "stormck_merkle_root_device": (
+        c_int, [c_void_p, c_uint64, c_uint64, c_uint64, c_uint64, c_uint32, c_void_p, c_uint64, c_void_p, c_void_p, c_void_p]),
+    "stormck_fill_synthetic_device": (c_int, [c_void_p, c_uint64, c_uint64, c_uint64, c_uint64, c_void_p]),
+}
+
+
+def _load() -> ctypes.CDLL:
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"libstormck not built ({LIB_PATH} missing): run `python -c 'import __graft_entry__ as g; g.build()'`")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+lib = _load()
+
+
+def last_error() -> str:
+    msg = lib.stormck_last_error()
+    return msg.decode() if msg else ""
+
+
+def check(rc: int) -> None:
+    """Raise on a negative libstormck status."""
+    if rc == OK:
+        return
+    if rc == ENODEV:
+        raise NoDeviceError(rc, last_error())
+    raise StormckError(rc, last_error())
+
+
+def device_count() -> int:
+    c = c_int(0)
+    check(lib.stormck_device_count(ctypes.byref(c)))
+    return c.value

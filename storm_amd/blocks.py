@@ -1,0 +1,137 @@
+"""Host mirror of storm's Go package ``blocks`` over libstormck.
+
+Same names, argument meaning and error behaviour as the reference:
+
+=====================  ===========================================================
+``Checksum(b)``        ``func Checksum(b []byte) Hash``  blocks/checksum.go:15-17
+``BlockChecksum(b)``   ``func BlockChecksum[T Block](b *T) Hash``  checksum.go:10-12
+``VerifyChecksum``     ``func VerifyChecksum(address, p, expected) error``  :20-27
+``Pointer``            ``type Pointer struct{...}``  blocks/types.go:35-39
+``BlockType``          Free / Pointer / Leaf  blocks/types.go:7-15
+``BLOCK_SIZE``         ``const BlockSize = 32 * 1024``  blocks/types.go:4
+=====================  ===========================================================
+
+plus the batch entry points the GPU path exists for (``ChecksumBatch``,
+``VerifyChecksumBatch``). Every hash is computed by the gfx950 kernels in
+libstormck; there is no host-side hash in the product.
+"""
+from __future__ import annotations
+
+import ctypes
+from enum import IntEnum
+from typing import Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import _lib
+from ._lib import PointerStruct as Pointer  # noqa: F401  (re-export: blocks.Pointer)
+
+BLOCK_SIZE = 32 * 1024
+
+Hash = int
+BlockAddress = int
+
+
+class BlockType(IntEnum):
+    """blocks.BlockType (/root/reference/blocks/types.go:7-15)."""
+
+    FREE = 0
+    POINTER = 1
+    LEAF = 2
+
+
+FreeBlockType = BlockType.FREE
+PointerBlockType = BlockType.POINTER
+LeafBlockType = BlockType.LEAF
+
+
+class ChecksumMismatchError(Exception):
+    """The error VerifyChecksum returns (reference: pkg/errors.Errorf, checksum.go:25-26)."""
+
+    def __init__(self, address: int, computed: int, expected: int):
+        super().__init__(
+            f"checksum mismatch for block {address}, computed: {_go_hex(computed)}, expected: {_go_hex(expected)}")
+        self.address = address
+        self.computed = computed
+        self.expected = expected
+
+
+def _go_hex(v: int) -> str:
+    # Go's %#v of an unsigned integer type: 0x-prefixed lowercase hex, no padding.
+    return "0x%x" % v
+
+
+def _as_u8(b) -> np.ndarray:
+    """Zero-copy uint8 view of any buffer-protocol object (bytes, bytearray,
+    memoryview, numpy array, ctypes structure)."""
+    if isinstance(b, np.ndarray):
+        return np.ascontiguousarray(b).view(np.uint8).reshape(-1)
+    return np.frombuffer(b, dtype=np.uint8)
+
+
+def Checksum(b) -> Hash:
+    """XXH64 (seed 0) of the bytes of ``b``."""
+    a = _as_u8(b)
+    out = ctypes.c_uint64(0)
+    _lib.check(_lib.lib.stormck_checksum(a.ctypes.data if a.size else None, a.size, ctypes.byref(out)))
+    return out.value
+
+
+def BlockChecksum(block) -> Hash:
+    """Checksum of the full in-memory image of a block struct (``ctypes.sizeof``
+    bytes, padding included — what photon.NewFromValue(b).B exposes)."""
+    return Checksum(memoryview(block).cast("B"))
+
+
+def VerifyChecksum(address: BlockAddress, p, expected_checksum: Hash) -> Optional[ChecksumMismatchError]:
+    """Returns None when Checksum(p) == expected, else the mismatch error (Go returns
+    an error value; callers raise it when they need to)."""
+    checksum = Checksum(p)
+    if checksum == expected_checksum:
+        return None
+    return ChecksumMismatchError(address, checksum, expected_checksum)
+
+
+def _lens_arg(n: int, length: Optional[int], lens: Optional[Sequence[int]]):
+    if lens is not None:
+        la = np.ascontiguousarray(np.asarray(lens, dtype=np.uint32))
+        if la.size != n:
+            raise ValueError("lens must have one entry per block")
+        return la, 0
+    if length is None:
+        raise ValueError("length or lens required")
+    return None, int(length)
+
+
+def ChecksumBatch(buf, n: int, stride: int, length: Optional[int] = None,
+                  lens: Optional[Sequence[int]] = None) -> np.ndarray:
+    """Checksums of ``n`` host blocks at ``buf + i*stride`` (``length`` bytes each or
+    ``lens[i]``). H2D -> gfx950 kernel -> D2H. Returns uint64[n]."""
+    a = _as_u8(buf)
+    la, ln = _lens_arg(n, length, lens)
+    if n and a.size < (n - 1) * stride + (int(la.max()) if la is not None else ln):
+        raise ValueError("buffer too small for n blocks")
+    out = np.zeros(n, dtype=np.uint64)
+    if n == 0:
+        return out
+    _lib.check(_lib.lib.stormck_checksum_host(a.ctypes.data, stride, la.ctypes.data if la is not None else None, ln, n,
+                                              out.ctypes.data))
+    return out
+
+
+def VerifyChecksumBatch(buf, n: int, stride: int, expected: Sequence[int], length: Optional[int] = None,
+                        lens: Optional[Sequence[int]] = None) -> Tuple[int, int]:
+    """Batched VerifyChecksum. Returns (first_bad, n_bad); first_bad == n when all match."""
+    a = _as_u8(buf)
+    la, ln = _lens_arg(n, length, lens)
+    exp = np.ascontiguousarray(np.asarray(expected, dtype=np.uint64))
+    if exp.size != n:
+        raise ValueError("expected must have one entry per block")
+    if n == 0:
+        return 0, 0
+    fb, nb = ctypes.c_uint64(0), ctypes.c_uint64(0)
+    rc = _lib.lib.stormck_verify_host(a.ctypes.data, stride, la.ctypes.data if la is not None else None, ln, n,
+                                      exp.ctypes.data, ctypes.byref(fb), ctypes.byref(nb))
+    if rc != _lib.EMISMATCH:
+        _lib.check(rc)
+    return fb.value, nb.value

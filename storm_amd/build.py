@@ -1,0 +1,72 @@
+"""Build libstormck.so (gfx950) in-tree, and the test-only oracle library.
+
+    python -m storm_amd.build            # product library
+    python -m storm_amd.build --all      # + oracle/liboracle.so (tests / CPU baseline)
+
+The built .so files are git-ignored and travel to the GPU box with the snapshot.
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "storm_amd")
+CSRC = os.path.join(PKG, "csrc")
+LIB_DIR = os.path.join(PKG, "lib")
+LIB = os.path.join(LIB_DIR, "libstormck.so")
+ARCH = "gfx950"
+
+
+def hipcc() -> str:
+    for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if cand and os.path.exists(cand):
+            return cand
+    raise RuntimeError("hipcc not found")
+
+
+def _newer(target: str, sources) -> bool:
+    if not os.path.exists(target):
+        return False
+    t = os.path.getmtime(target)
+    return all(os.path.getmtime(s) <= t for s in sources)
+
+
+def build_lib(force: bool = False) -> str:
+    srcs = [os.path.join(CSRC, f) for f in ("stormck.hip", "kernels.h", "xxh64_dev.h")]
+    srcs.append(os.path.join(ROOT, "include", "stormck.h"))
+    if not force and _newer(LIB, srcs):
+        return LIB
+    os.makedirs(LIB_DIR, exist_ok=True)
+    tmp = LIB + ".tmp"
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall",
+           "-o", tmp, os.path.join(CSRC, "stormck.hip")]
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, LIB)
+    return LIB
+
+
+def build_oracle(force: bool = False) -> str:
+    out = os.path.join(ROOT, "oracle", "liboracle.so")
+    src = os.path.join(ROOT, "oracle", "xxh64_oracle.c")
+    if force or not _newer(out, [src]):
+        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
+    return out
+
+
+def build_probe(force: bool = False) -> str:
+    out = os.path.join(ROOT, "tools", "probe")
+    srcs = [os.path.join(ROOT, "tools", "probe.hip"), os.path.join(CSRC, "kernels.h"), os.path.join(CSRC, "xxh64_dev.h")]
+    if force or not _newer(out, srcs):
+        subprocess.run([hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-o", out, srcs[0]], check=True)
+    return out
+
+
+if __name__ == "__main__":
+    force = "--force" in sys.argv
+    print(build_lib(force))
+    if "--all" in sys.argv:
+        print(build_oracle(force))
+        print(build_probe(force))

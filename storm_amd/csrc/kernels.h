@@ -1,0 +1,376 @@
+// gfx950 kernels of the storm block-checksum engine.
+//
+// Hot path: XXH64(seed 0) of every block of a batch = storm's blocks.Checksum /
+// blocks.BlockChecksum (/root/reference/blocks/checksum.go:10-17) applied to many
+// independent blocks at once.
+//
+// Why not "one wavefront per block": XXH64 carries four serial accumulator
+// recurrences over a block's stripes (acc = rotl(acc + w*P2, 31) * P1 per 8-byte word),
+// and the recurrence is not associative, so at most FOUR lanes can work on one block.
+// Mappings implemented here:
+//   * quad  : 4 lanes per block (lane j owns accumulator j and loads word j of each
+//             32-byte stripe), 16 blocks per wave64; the 4 accumulators meet through
+//             DPP quad permutes for the merge; lane 0 of the quad does tail+avalanche.
+//   * lane  : 1 lane per block (all four accumulators in one lane), 64 blocks per wave,
+//             dwordx4 loads of whole stripes.
+// The per-block sizes (stride / explicit offsets) and lengths (uniform / per-block)
+// cover storm's block types: 72, 28808, 30000, 31808, 32768 bytes.
+#pragma once
+#include "xxh64_dev.h"
+
+namespace stormck {
+
+typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+
+// Broadcast lane k of each quad (DPP quad_perm) for a 64-bit value.
+template <int K>
+__device__ __forceinline__ uint64_t quad_bcast(uint64_t v) {
+    constexpr int ctrl = K | (K << 2) | (K << 4) | (K << 6);
+    const int lo = __builtin_amdgcn_update_dpp(0, static_cast<int>(static_cast<uint32_t>(v)), ctrl, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, static_cast<int>(static_cast<uint32_t>(v >> 32)), ctrl, 0xF, 0xF, false);
+    return (static_cast<uint64_t>(static_cast<uint32_t>(hi)) << 32) | static_cast<uint32_t>(lo);
+}
+
+__device__ __forceinline__ uint64_t acc_seed(uint32_t j) {
+    return j == 0 ? kV1 : (j == 1 ? kV2 : (j == 2 ? kV3 : kV4));
+}
+
+// Streaming load; NT selects the non-temporal cache policy (data is read once).
+template <bool NT, typename T>
+__device__ __forceinline__ T ldg(const T* p) {
+    if constexpr (NT) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+
+// Stripe loop of one accumulator over nst stripes, 8-byte-aligned source.
+// p points at word j of stripe 0; word j of stripe s is p[4*s].
+// Software-pipelined in groups of U loads: group g+1 is in flight while group g hashes.
+template <int U, bool NT = false>
+__device__ __forceinline__ uint64_t quad_stripes_aligned(const uint64_t* __restrict__ p, uint32_t nst, uint64_t acc) {
+    const uint32_t ngroups = nst / U;
+    uint32_t s = 0;
+    if (ngroups > 0) {
+        uint64_t wa[U], wb[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) wa[u] = ldg<NT>(p + 4 * u);
+        uint32_t g = 1;
+        for (; g + 1 < ngroups; g += 2) {
+            const uint64_t* q = p + 4 * U * g;
+#pragma unroll
+            for (int u = 0; u < U; ++u) wb[u] = ldg<NT>(q + 4 * u);
+#pragma unroll
+            for (int u = 0; u < U; ++u) acc = round(acc, wa[u]);
+            q += 4 * U;
+#pragma unroll
+            for (int u = 0; u < U; ++u) wa[u] = ldg<NT>(q + 4 * u);
+#pragma unroll
+            for (int u = 0; u < U; ++u) acc = round(acc, wb[u]);
+        }
+        if (g < ngroups) {
+            const uint64_t* q = p + 4 * U * g;
+#pragma unroll
+            for (int u = 0; u < U; ++u) wb[u] = ldg<NT>(q + 4 * u);
+#pragma unroll
+            for (int u = 0; u < U; ++u) acc = round(acc, wa[u]);
+#pragma unroll
+            for (int u = 0; u < U; ++u) acc = round(acc, wb[u]);
+        } else {
+#pragma unroll
+            for (int u = 0; u < U; ++u) acc = round(acc, wa[u]);
+        }
+        s = ngroups * U;
+    }
+    for (; s < nst; ++s) acc = round(acc, p[4 * s]);
+    return acc;
+}
+
+// Byte-granular stripe loop for blocks whose start is not 8-byte aligned.
+__device__ __forceinline__ uint64_t quad_stripes_unaligned(const uint8_t* p, uint32_t nst, uint64_t acc) {
+    for (uint32_t s = 0; s < nst; ++s) acc = round(acc, ld64_unaligned(p + 32 * s));
+    return acc;
+}
+
+// Tail + avalanche with word loads when the tail start is 8-byte aligned.
+__device__ __forceinline__ uint64_t finish_fast(uint64_t h, uint64_t n, const uint8_t* p, uint32_t rem) {
+    if ((reinterpret_cast<uintptr_t>(p) & 7) != 0) return finish(h, n, p, rem);
+    h += n;
+    const uint64_t* w = reinterpret_cast<const uint64_t*>(p);
+    while (rem >= 8) {
+        h ^= round(0, *w++);
+        h = rotl<27>(h) * kP1 + kP4;
+        rem -= 8;
+    }
+    const uint8_t* b = reinterpret_cast<const uint8_t*>(w);
+    if (rem >= 4) {
+        h ^= static_cast<uint64_t>(*reinterpret_cast<const uint32_t*>(b)) * kP1;
+        h = rotl<23>(h) * kP2 + kP3;
+        b += 4;
+        rem -= 4;
+    }
+    while (rem > 0) {
+        h ^= static_cast<uint64_t>(*b) * kP5;
+        h = rotl<11>(h) * kP1;
+        ++b;
+        --rem;
+    }
+    return avalanche(h);
+}
+
+// ---------------------------------------------------------------------------
+// Quad kernel: 4 lanes per block. Block i starts at base + (OFFS ? offs[i] : i*stride)
+// and is LENS ? lens[i] : len bytes long. 256-thread workgroups = 64 blocks.
+// VERIFY: instead of writing the checksum, compare with expected[i]; on mismatch
+// atomically lower *first_bad to i and count into *n_bad.
+// ---------------------------------------------------------------------------
+template <int U, bool LENS, bool OFFS, bool VERIFY, bool NT = false>
+__global__ __launch_bounds__(256) void k_xxh64_quad(const uint8_t* __restrict__ base, uint64_t stride,
+                                                      const uint32_t* __restrict__ lens, uint32_t len,
+                                                      const uint64_t* __restrict__ offs, uint64_t n,
+                                                      uint64_t* __restrict__ out,
+                                                      const uint64_t* __restrict__ expected,
+                                                      unsigned long long* __restrict__ first_bad,
+                                                      unsigned long long* __restrict__ n_bad) {
+    const uint64_t gtid = static_cast<uint64_t>(blockIdx.x) * 256 + threadIdx.x;
+    const uint64_t blk_raw = gtid >> 2;
+    const uint32_t j = threadIdx.x & 3;
+    const bool live = blk_raw < n;
+    const uint64_t blk = live ? blk_raw : n - 1;  // dead quads shadow the last block; never store
+    const uint8_t* src = base + (OFFS ? offs[blk] : blk * stride);
+    const uint32_t L = LENS ? lens[blk] : len;
+    const uint32_t nst = L >> 5;
+
+    uint64_t acc = acc_seed(j);
+    const bool aligned = (reinterpret_cast<uintptr_t>(src) & 7) == 0;
+    if (aligned) {
+        acc = quad_stripes_aligned<U, NT>(reinterpret_cast<const uint64_t*>(src) + j, nst, acc);
+    } else {
+        acc = quad_stripes_unaligned(src + 8 * j, nst, acc);
+    }
+    const uint64_t v1 = quad_bcast<0>(acc);
+    const uint64_t v2 = quad_bcast<1>(acc);
+    const uint64_t v3 = quad_bcast<2>(acc);
+    const uint64_t v4 = quad_bcast<3>(acc);
+    if (j == 0 && live) {
+        const uint64_t h0 = (L >= 32) ? converge(v1, v2, v3, v4) : kP5;
+        const uint64_t h = finish_fast(h0, L, src + 32 * static_cast<uint64_t>(nst), L & 31);
+        if (VERIFY) {
+            if (h != expected[blk]) {
+                atomicMin(first_bad, static_cast<unsigned long long>(blk));
+                atomicAdd(n_bad, 1ULL);
+            }
+        } else {
+            out[blk] = h;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Lane kernel: 1 lane per block, uniform length, 16-byte aligned blocks
+// (base % 16 == 0, stride % 16 == 0). U stripes (2U dwordx4) per pipelined group.
+// ---------------------------------------------------------------------------
+template <int U, bool NT = false>
+__global__ __launch_bounds__(256) void k_xxh64_lane(const uint8_t* __restrict__ base, uint64_t stride,
+                                                      uint32_t len, uint64_t n, uint64_t* __restrict__ out) {
+    const uint64_t blk = static_cast<uint64_t>(blockIdx.x) * 256 + threadIdx.x;
+    if (blk >= n) return;
+    const uint8_t* src = base + blk * stride;
+    const uint32_t nst = len >> 5;
+    const u64x2* p = reinterpret_cast<const u64x2*>(src);
+    uint64_t v1 = kV1, v2 = kV2, v3 = kV3, v4 = kV4;
+    const uint32_t ngroups = nst / U;
+    uint32_t s = 0;
+    if (ngroups > 0) {
+        u64x2 a[2 * U], b[2 * U];
+#pragma unroll
+        for (int u = 0; u < 2 * U; ++u) a[u] = ldg<NT>(p + u);
+        uint32_t g = 1;
+        for (; g + 1 < ngroups; g += 2) {
+            const u64x2* q = p + 2 * U * g;
+#pragma unroll
+            for (int u = 0; u < 2 * U; ++u) b[u] = ldg<NT>(q + u);
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                v1 = round(v1, a[2 * u].x); v2 = round(v2, a[2 * u].y);
+                v3 = round(v3, a[2 * u + 1].x); v4 = round(v4, a[2 * u + 1].y);
+            }
+            q += 2 * U;
+#pragma unroll
+            for (int u = 0; u < 2 * U; ++u) a[u] = ldg<NT>(q + u);
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                v1 = round(v1, b[2 * u].x); v2 = round(v2, b[2 * u].y);
+                v3 = round(v3, b[2 * u + 1].x); v4 = round(v4, b[2 * u + 1].y);
+            }
+        }
+        if (g < ngroups) {
+            const u64x2* q = p + 2 * U * g;
+#pragma unroll
+            for (int u = 0; u < 2 * U; ++u) b[u] = ldg<NT>(q + u);
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                v1 = round(v1, a[2 * u].x); v2 = round(v2, a[2 * u].y);
+                v3 = round(v3, a[2 * u + 1].x); v4 = round(v4, a[2 * u + 1].y);
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                v1 = round(v1, b[2 * u].x); v2 = round(v2, b[2 * u].y);
+                v3 = round(v3, b[2 * u + 1].x); v4 = round(v4, b[2 * u + 1].y);
+            }
+        } else {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                v1 = round(v1, a[2 * u].x); v2 = round(v2, a[2 * u].y);
+                v3 = round(v3, a[2 * u + 1].x); v4 = round(v4, a[2 * u + 1].y);
+            }
+        }
+        s = ngroups * U;
+    }
+    for (; s < nst; ++s) {
+        const u64x2 x = p[2 * s], y = p[2 * s + 1];
+        v1 = round(v1, x.x); v2 = round(v2, x.y); v3 = round(v3, y.x); v4 = round(v4, y.y);
+    }
+    const uint64_t h0 = (len >= 32) ? converge(v1, v2, v3, v4) : kP5;
+    out[blk] = finish_fast(h0, len, src + 32 * static_cast<uint64_t>(nst), len & 31);
+}
+
+// ---------------------------------------------------------------------------
+// Merkle pointer tree: storm pointer.Block nodes (blocks/pointer/block.go:10-13).
+// Node bytes: fanout x {Checksum, Address, BirthRevision} (24 B each, LE) then fanout
+// BlockType bytes, zero-padded to a multiple of 8 (Go struct size). Words are
+// synthesised on the fly from the children; the node never exists in memory.
+// ---------------------------------------------------------------------------
+__host__ __device__ inline uint32_t pointer_block_size(uint32_t fanout) { return (fanout * 25u + 7u) & ~7u; }
+
+// Children {cs[lo+i], addr_base+lo+i, rev} of one type, i < cnt.
+struct LevelWords {
+    const uint64_t* cs;
+    uint64_t lo, addr_base, rev;
+    uint32_t cnt, fanout;
+    uint8_t type;
+    __device__ __forceinline__ uint64_t operator()(uint32_t k) const {
+        const uint32_t pw = 3 * fanout;
+        if (k < pw) {
+            const uint32_t i = k / 3, f = k - 3 * i;
+            if (i >= cnt) return 0;
+            return f == 0 ? cs[lo + i] : (f == 1 ? addr_base + lo + i : rev);
+        }
+        const uint32_t pos = 8 * (k - pw);
+        if (pos >= cnt) return 0;
+        const uint32_t nb = (cnt - pos) >= 8 ? 8 : (cnt - pos);
+        const uint64_t rep = 0x0101010101010101ULL * type;
+        return nb == 8 ? rep : (rep & ((1ULL << (8 * nb)) - 1));
+    }
+};
+
+// Explicit entries (AoS Pointer + type byte), i < cnt.
+struct EntryWords {
+    const uint64_t* entries;  // 3 u64 per entry
+    const uint8_t* types;
+    uint32_t cnt, fanout;
+    __device__ __forceinline__ uint64_t operator()(uint32_t k) const {
+        const uint32_t pw = 3 * fanout;
+        if (k < pw) {
+            const uint32_t i = k / 3;
+            return i < cnt ? entries[k] : 0;
+        }
+        const uint32_t pos = 8 * (k - pw);
+        uint64_t w = 0;
+        for (uint32_t b = 0; b < 8; ++b)
+            if (pos + b < cnt) w |= static_cast<uint64_t>(types[pos + b]) << (8 * b);
+        return w;
+    }
+};
+
+// XXH64 of a synthesised node by one quad (lane j = accumulator j). Every lane of
+// the quad returns the hash. size is a multiple of 8 (no 4-/1-byte tail).
+template <class W>
+__device__ __forceinline__ uint64_t hash_words_quad(const W& word, uint32_t size, uint32_t j) {
+    const uint32_t nst = size >> 5;
+    uint64_t acc = acc_seed(j);
+    for (uint32_t s = 0; s < nst; ++s) acc = round(acc, word(4 * s + j));
+    const uint64_t v1 = quad_bcast<0>(acc), v2 = quad_bcast<1>(acc), v3 = quad_bcast<2>(acc), v4 = quad_bcast<3>(acc);
+    uint64_t h = (size >= 32) ? converge(v1, v2, v3, v4) : kP5;
+    h += size;
+    for (uint32_t k = 4 * nst; k < size / 8; ++k) {
+        h ^= round(0, word(k));
+        h = rotl<27>(h) * kP1 + kP4;
+    }
+    return avalanche(h);
+}
+
+__global__ __launch_bounds__(256) void k_pointer_level(const uint64_t* __restrict__ cs, uint64_t m,
+                                                        uint64_t addr_base, uint64_t rev, uint8_t type,
+                                                        uint32_t fanout, uint64_t* __restrict__ parent_cs) {
+    const uint64_t gtid = static_cast<uint64_t>(blockIdx.x) * 256 + threadIdx.x;
+    const uint64_t pj = gtid >> 2;
+    const uint64_t pm = (m + fanout - 1) / fanout;
+    const uint32_t j = threadIdx.x & 3;
+    const uint64_t node = pj < pm ? pj : pm - 1;
+    LevelWords w;
+    w.cs = cs; w.lo = node * fanout; w.addr_base = addr_base; w.rev = rev; w.fanout = fanout; w.type = type;
+    w.cnt = static_cast<uint32_t>((m - w.lo) < fanout ? (m - w.lo) : fanout);
+    const uint64_t h = hash_words_quad(w, pointer_block_size(fanout), j);
+    if (j == 0 && pj < pm) parent_cs[pj] = h;
+}
+
+__global__ __launch_bounds__(64) void k_pointer_node(const uint64_t* __restrict__ entries,
+                                                      const uint8_t* __restrict__ types, uint32_t cnt,
+                                                      uint32_t fanout, uint64_t* __restrict__ out_cs) {
+    const uint32_t j = threadIdx.x & 3;
+    EntryWords w{entries, types, cnt, fanout};
+    const uint64_t h = hash_words_quad(w, pointer_block_size(fanout), j);
+    if (threadIdx.x == 0) *out_cs = h;
+}
+
+__global__ __launch_bounds__(256) void k_pack_pointer_blocks(const uint64_t* __restrict__ cs, uint64_t m,
+                                                              uint64_t addr_base, uint64_t rev, uint8_t type,
+                                                              uint32_t fanout, uint8_t* __restrict__ dst,
+                                                              uint64_t dst_stride) {
+    const uint32_t words = pointer_block_size(fanout) / 8;
+    const uint64_t pm = (m + fanout - 1) / fanout;
+    const uint64_t total = pm * words;
+    for (uint64_t t = static_cast<uint64_t>(blockIdx.x) * 256 + threadIdx.x; t < total;
+         t += static_cast<uint64_t>(gridDim.x) * 256) {
+        const uint64_t node = t / words;
+        const uint32_t k = static_cast<uint32_t>(t - node * words);
+        LevelWords w;
+        w.cs = cs; w.lo = node * fanout; w.addr_base = addr_base; w.rev = rev; w.fanout = fanout; w.type = type;
+        w.cnt = static_cast<uint32_t>((m - w.lo) < fanout ? (m - w.lo) : fanout);
+        reinterpret_cast<uint64_t*>(dst + node * dst_stride)[k] = w(k);
+    }
+}
+
+// root = {cs ? cs[0] : 0, addr, rev} of `type` (1-entry level, or the empty tree).
+__global__ void k_set_root(const uint64_t* __restrict__ cs, uint64_t addr, uint64_t rev, uint8_t type,
+                           uint64_t* __restrict__ root, uint8_t* __restrict__ root_type) {
+    if (threadIdx.x == 0) {
+        root[0] = cs ? cs[0] : 0;
+        root[1] = addr;
+        root[2] = rev;
+        *root_type = type;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Synthetic block generator: word w of logical block (first + i)
+// = splitmix64(seed ^ ((first + i) << 20 + w)). One 16-byte store per lane,
+// grid-stride over the whole [n x stride] region (stride % 16 == 0).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_fill_synthetic(uint8_t* __restrict__ dst, uint64_t stride, uint64_t n,
+                                                         uint64_t first, uint64_t seed) {
+    const uint64_t pairs_per_block = stride / 16;
+    const uint64_t total = pairs_per_block * n;
+    for (uint64_t t = static_cast<uint64_t>(blockIdx.x) * 256 + threadIdx.x; t < total;
+         t += static_cast<uint64_t>(gridDim.x) * 256) {
+        const uint64_t i = t / pairs_per_block;
+        const uint64_t w = (t - i * pairs_per_block) * 2;
+        const uint64_t key = seed ^ (((first + i) << 20) + w);
+        const uint64_t key2 = seed ^ (((first + i) << 20) + w + 1);
+        ulonglong2 v;
+        v.x = splitmix64(key);
+        v.y = splitmix64(key2);
+        reinterpret_cast<ulonglong2*>(dst + i * stride)[w / 2] = v;
+    }
+}
+
+}  // namespace stormck

@@ -1,0 +1,551 @@
+// libstormck: C-ABI of the MI355X block-checksum engine (declarations and the
+// reference interface each entry point replaces: include/stormck.h).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/stormck.h"
+#include "kernels.h"
+
+using namespace stormck;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string& msg) {
+    g_last_error = msg;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                              \
+    do {                                                                                           \
+        hipError_t e_ = (expr);                                                                    \
+        if (e_ != hipSuccess)                                                                      \
+            return fail(e_ == hipErrorOutOfMemory ? STORMCK_ENOMEM : STORMCK_EHIP,                 \
+                        std::string(#expr) + ": " + hipGetErrorString(e_));                        \
+    } while (0)
+
+// Stripe-loop unroll of the production quad kernel: 16 x 8-byte loads in flight per
+// lane per pipelined group (design probe, profiles/r01_probe.txt: U=16 with plain
+// loads is the fastest quad variant; non-temporal loads cost 35%).
+constexpr int kU = 16;
+constexpr unsigned kThreads = 256;
+constexpr uint32_t kMaxFanout = 1u << 16;
+
+// Cached answer to "is there a usable gfx950 device?" per process.
+int device_check() {
+    static std::once_flag once;
+    static int status = STORMCK_OK;
+    static std::string why;
+    std::call_once(once, [] {
+        int count = 0;
+        hipError_t e = hipGetDeviceCount(&count);
+        if (e != hipSuccess || count == 0) {
+            status = STORMCK_ENODEV;
+            why = std::string("no HIP device: ") + (e != hipSuccess ? hipGetErrorString(e) : "count == 0");
+            return;
+        }
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, 0) != hipSuccess || std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+            status = STORMCK_ENODEV;
+            why = std::string("device 0 is not gfx950: ") + prop.gcnArchName;
+        }
+    });
+    if (status != STORMCK_OK) g_last_error = why;
+    return status;
+}
+
+bool grid_for(uint64_t threads, dim3* grid) {
+    const uint64_t blocks = (threads + kThreads - 1) / kThreads;
+    if (blocks == 0 || blocks > 0x7fffffffULL) return false;
+    *grid = dim3(static_cast<unsigned>(blocks));
+    return true;
+}
+
+int launch_checksum(const uint8_t* base, uint64_t stride, const uint32_t* lens, uint32_t len, const uint64_t* offs,
+                    uint64_t n, uint64_t* out, const uint64_t* expected, unsigned long long* first_bad,
+                    unsigned long long* n_bad, hipStream_t st) {
+    dim3 grid;
+    if (!grid_for(n * 4, &grid)) return fail(STORMCK_EINVAL, "batch too large for one launch");
+    const bool verify = expected != nullptr;
+    // Dispatch on the compile-time shape (per-block lengths / explicit offsets / verify).
+#define STORMCK_LAUNCH(LENS, OFFS, VER)                                                                         \
+    hipLaunchKernelGGL((k_xxh64_quad<kU, LENS, OFFS, VER>), grid, dim3(kThreads), 0, st, base, stride, lens, len, \
+                       offs, n, out, expected, first_bad, n_bad)
+    if (!verify) {
+        if (lens && offs) STORMCK_LAUNCH(true, true, false);
+        else if (lens) STORMCK_LAUNCH(true, false, false);
+        else if (offs) STORMCK_LAUNCH(false, true, false);
+        else STORMCK_LAUNCH(false, false, false);
+    } else {
+        if (lens && offs) STORMCK_LAUNCH(true, true, true);
+        else if (lens) STORMCK_LAUNCH(true, false, true);
+        else if (offs) STORMCK_LAUNCH(false, true, true);
+        else STORMCK_LAUNCH(false, false, true);
+    }
+#undef STORMCK_LAUNCH
+    HIP_TRY(hipGetLastError());
+    return STORMCK_OK;
+}
+
+__global__ void k_init_result(uint64_t* r, uint64_t n) {
+    if (threadIdx.x == 0) {
+        r[0] = n;
+        r[1] = 0;
+    }
+}
+
+// ---- per-device context for the host-memory path ---------------------------------
+constexpr uint64_t kChunkBytes = 256ULL << 20;  // bytes of block data per pipeline stage
+constexpr int kStages = 2;
+
+struct Stage {
+    hipStream_t stream = nullptr;
+    hipEvent_t done = nullptr;
+    uint8_t* pinned = nullptr;      // staging for pageable sources
+    uint8_t* d_data = nullptr;
+    uint32_t* d_lens = nullptr;
+    uint64_t* d_out = nullptr;
+    uint64_t* h_out = nullptr;      // pinned
+    uint64_t* d_expected = nullptr;
+    uint64_t* d_result = nullptr;   // verify: first_bad, n_bad
+    uint64_t* h_result = nullptr;   // pinned
+    // what the stage holds (to drain its outputs)
+    uint64_t first = 0, count = 0;
+    bool busy = false;
+};
+
+struct DeviceCtx {
+    std::mutex mu;
+    int device = -1;
+    bool ready = false;
+    Stage st[kStages];
+};
+
+std::mutex g_ctx_mu;
+std::vector<std::unique_ptr<DeviceCtx>> g_ctx;
+
+int get_ctx(DeviceCtx** out) {
+    int rc = device_check();
+    if (rc) return rc;
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev));
+    std::lock_guard<std::mutex> g(g_ctx_mu);
+    if (g_ctx.size() <= static_cast<size_t>(dev)) g_ctx.resize(dev + 1);
+    if (!g_ctx[dev]) g_ctx[dev].reset(new DeviceCtx());
+    *out = g_ctx[dev].get();
+    (*out)->device = dev;
+    return STORMCK_OK;
+}
+
+int ensure_ready(DeviceCtx* c) {
+    if (c->ready) return STORMCK_OK;
+    for (Stage& s : c->st) {
+        HIP_TRY(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
+        HIP_TRY(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
+        HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&s.pinned), kChunkBytes, hipHostMallocDefault));
+        HIP_TRY(hipMalloc(&s.d_data, kChunkBytes));
+        const uint64_t maxb = kChunkBytes / 8;  // smallest admissible stride is 8 bytes per block
+        HIP_TRY(hipMalloc(&s.d_lens, maxb * 4));
+        HIP_TRY(hipMalloc(&s.d_out, maxb * 8));
+        HIP_TRY(hipMalloc(&s.d_expected, maxb * 8));
+        HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&s.h_out), maxb * 8, hipHostMallocDefault));
+        HIP_TRY(hipMalloc(&s.d_result, 16));
+        HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&s.h_result), 16, hipHostMallocDefault));
+    }
+    c->ready = true;
+    return STORMCK_OK;
+}
+
+void release_ctx(DeviceCtx* c) {
+    if (!c || !c->ready) return;
+    int prev = 0;
+    (void)hipGetDevice(&prev);
+    (void)hipSetDevice(c->device);
+    for (Stage& s : c->st) {
+        if (s.stream) (void)hipStreamSynchronize(s.stream);
+        (void)hipFree(s.d_data);
+        (void)hipFree(s.d_lens);
+        (void)hipFree(s.d_out);
+        (void)hipFree(s.d_expected);
+        (void)hipFree(s.d_result);
+        (void)hipHostFree(s.pinned);
+        (void)hipHostFree(s.h_out);
+        (void)hipHostFree(s.h_result);
+        if (s.done) (void)hipEventDestroy(s.done);
+        if (s.stream) (void)hipStreamDestroy(s.stream);
+        s = Stage();
+    }
+    c->ready = false;
+    (void)hipSetDevice(prev);
+}
+
+bool is_pinned(const void* p) {
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return a.type == hipMemoryTypeHost || a.type == hipMemoryTypeManaged;
+}
+
+// Parallel memcpy into pinned staging (pageable sources): a single thread cannot
+// feed PCIe Gen5; a few threads can.
+void par_copy(uint8_t* dst, const uint8_t* src, uint64_t bytes) {
+    const uint64_t kMin = 8ULL << 20;
+    unsigned nt = static_cast<unsigned>(std::min<uint64_t>(8, std::max<uint64_t>(1, bytes / kMin)));
+    if (nt <= 1) {
+        std::memcpy(dst, src, bytes);
+        return;
+    }
+    std::vector<std::thread> th;
+    th.reserve(nt);
+    for (unsigned t = 0; t < nt; ++t) {
+        const uint64_t lo = bytes * t / nt, hi = bytes * (t + 1) / nt;
+        th.emplace_back([=] { std::memcpy(dst + lo, src + lo, hi - lo); });
+    }
+    for (auto& x : th) x.join();
+}
+
+// Host pipeline shared by checksum_host / verify_host. Blocks are processed in
+// chunks of whole blocks (<= kChunkBytes of stride); stage k's H2D+kernel+D2H run
+// on its own stream while the host fills the other stage.
+int host_pipeline(const void* base, uint64_t stride, const uint32_t* lens, uint32_t len, uint64_t n,
+                  uint64_t* out, const uint64_t* expected, uint64_t* first_bad, uint64_t* n_bad) {
+    if (n == 0) {
+        if (first_bad) *first_bad = 0;
+        if (n_bad) *n_bad = 0;
+        return STORMCK_OK;
+    }
+    if (!base) return fail(STORMCK_EINVAL, "base is null");
+    if (!expected && !out) return fail(STORMCK_EINVAL, "out is null");
+    // Per-block extent actually read: max length (stride may be 0 only for n == 1).
+    uint64_t maxlen = len;
+    if (lens) {
+        maxlen = 0;
+        for (uint64_t i = 0; i < n; ++i) maxlen = std::max<uint64_t>(maxlen, lens[i]);
+    }
+    if (n > 1 && stride < maxlen) return fail(STORMCK_EINVAL, "stride smaller than a block length (blocks overlap)");
+    const uint64_t step = n == 1 ? std::max<uint64_t>(maxlen, 8) : std::max<uint64_t>(stride, 8);
+    if (step > kChunkBytes) return fail(STORMCK_EINVAL, "block stride exceeds the staging chunk (256 MiB)");
+    const uint64_t per_chunk = std::max<uint64_t>(1, kChunkBytes / step);
+
+    DeviceCtx* c = nullptr;
+    int rc = get_ctx(&c);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> g(c->mu);
+    rc = ensure_ready(c);
+    if (rc) return rc;
+
+    const bool direct = is_pinned(base);
+    const uint8_t* src = static_cast<const uint8_t*>(base);
+    uint64_t fb = n, nb = 0;
+
+    auto drain = [&](Stage& s) -> int {
+        if (!s.busy) return STORMCK_OK;
+        HIP_TRY(hipEventSynchronize(s.done));
+        if (expected) {
+            if (s.h_result[1] > 0) {
+                nb += s.h_result[1];
+                fb = std::min<uint64_t>(fb, s.first + s.h_result[0]);
+            }
+        } else {
+            std::memcpy(out + s.first, s.h_out, s.count * 8);
+        }
+        s.busy = false;
+        return STORMCK_OK;
+    };
+
+    uint64_t chunk_idx = 0;
+    for (uint64_t first = 0; first < n; first += per_chunk, ++chunk_idx) {
+        Stage& s = c->st[chunk_idx % kStages];
+        rc = drain(s);
+        if (rc) return rc;
+        const uint64_t cnt = std::min<uint64_t>(per_chunk, n - first);
+        // bytes to move: up to the end of the last block in the chunk
+        const uint64_t last_len = lens ? lens[first + cnt - 1] : len;
+        const uint64_t bytes = (cnt - 1) * stride + last_len;
+        const uint8_t* chunk_src = src + first * stride;
+        if (direct) {
+            HIP_TRY(hipMemcpyAsync(s.d_data, chunk_src, bytes, hipMemcpyHostToDevice, s.stream));
+        } else {
+            par_copy(s.pinned, chunk_src, bytes);
+            HIP_TRY(hipMemcpyAsync(s.d_data, s.pinned, bytes, hipMemcpyHostToDevice, s.stream));
+        }
+        if (lens) HIP_TRY(hipMemcpyAsync(s.d_lens, lens + first, cnt * 4, hipMemcpyHostToDevice, s.stream));
+        if (expected) {
+            HIP_TRY(hipMemcpyAsync(s.d_expected, expected + first, cnt * 8, hipMemcpyHostToDevice, s.stream));
+            const uint64_t init[2] = {cnt, 0};
+            std::memcpy(s.h_result, init, 16);
+            HIP_TRY(hipMemcpyAsync(s.d_result, s.h_result, 16, hipMemcpyHostToDevice, s.stream));
+            rc = launch_checksum(s.d_data, stride, lens ? s.d_lens : nullptr, len, nullptr, cnt, nullptr,
+                                 s.d_expected, reinterpret_cast<unsigned long long*>(s.d_result),
+                                 reinterpret_cast<unsigned long long*>(s.d_result + 1), s.stream);
+            if (rc) return rc;
+            HIP_TRY(hipMemcpyAsync(s.h_result, s.d_result, 16, hipMemcpyDeviceToHost, s.stream));
+        } else {
+            rc = launch_checksum(s.d_data, stride, lens ? s.d_lens : nullptr, len, nullptr, cnt, s.d_out, nullptr,
+                                 nullptr, nullptr, s.stream);
+            if (rc) return rc;
+            HIP_TRY(hipMemcpyAsync(s.h_out, s.d_out, cnt * 8, hipMemcpyDeviceToHost, s.stream));
+        }
+        HIP_TRY(hipEventRecord(s.done, s.stream));
+        s.first = first;
+        s.count = cnt;
+        s.busy = true;
+        // a pinned staging buffer may be refilled only after its H2D finished; with two
+        // stages the drain at the top of the next-but-one iteration guarantees that.
+    }
+    for (Stage& s : c->st) {
+        rc = drain(s);
+        if (rc) return rc;
+    }
+    if (first_bad) *first_bad = fb;
+    if (n_bad) *n_bad = nb;
+    return STORMCK_OK;
+}
+
+}  // namespace
+
+// ============================================================================
+extern "C" {
+
+int stormck_abi_version(void) { return STORMCK_ABI_VERSION; }
+
+const char* stormck_last_error(void) { return g_last_error.c_str(); }
+
+int stormck_device_count(int* count) {
+    if (!count) return fail(STORMCK_EINVAL, "count is null");
+    *count = 0;
+    int c = 0;
+    if (hipGetDeviceCount(&c) != hipSuccess) {
+        (void)hipGetLastError();
+        return STORMCK_OK;
+    }
+    int n = 0;
+    for (int d = 0; d < c; ++d) {
+        hipDeviceProp_t p;
+        if (hipGetDeviceProperties(&p, d) == hipSuccess && std::strncmp(p.gcnArchName, "gfx950", 6) == 0) ++n;
+    }
+    *count = n;
+    return STORMCK_OK;
+}
+
+int stormck_init(int device) {
+    int rc = device_check();
+    if (rc) return rc;
+    HIP_TRY(hipSetDevice(device));
+    DeviceCtx* c = nullptr;
+    rc = get_ctx(&c);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> g(c->mu);
+    return ensure_ready(c);
+}
+
+void stormck_shutdown(void) {
+    std::lock_guard<std::mutex> g(g_ctx_mu);
+    for (auto& c : g_ctx) {
+        if (c) {
+            std::lock_guard<std::mutex> g2(c->mu);
+            release_ctx(c.get());
+        }
+    }
+}
+
+int stormck_checksum_device(const void* d_base, uint64_t stride, const uint32_t* d_lens, uint32_t len, uint64_t n,
+                            uint64_t* d_out, void* stream) {
+    if (n == 0) return STORMCK_OK;
+    int rc = device_check();
+    if (rc) return rc;
+    if (!d_base || !d_out) return fail(STORMCK_EINVAL, "null device pointer");
+    if (!d_lens && n > 1 && stride < len) return fail(STORMCK_EINVAL, "stride smaller than len (blocks overlap)");
+    return launch_checksum(static_cast<const uint8_t*>(d_base), stride, d_lens, len, nullptr, n, d_out, nullptr,
+                           nullptr, nullptr, static_cast<hipStream_t>(stream));
+}
+
+int stormck_checksum_gather_device(const void* d_base, const uint64_t* d_offsets, const uint32_t* d_lens,
+                                   uint32_t len, uint64_t n, uint64_t* d_out, void* stream) {
+    if (n == 0) return STORMCK_OK;
+    int rc = device_check();
+    if (rc) return rc;
+    if (!d_base || !d_offsets || !d_out) return fail(STORMCK_EINVAL, "null device pointer");
+    return launch_checksum(static_cast<const uint8_t*>(d_base), 0, d_lens, len, d_offsets, n, d_out, nullptr,
+                           nullptr, nullptr, static_cast<hipStream_t>(stream));
+}
+
+int stormck_verify_device(const void* d_base, uint64_t stride, const uint32_t* d_lens, uint32_t len, uint64_t n,
+                          const uint64_t* d_expected, uint64_t* d_result, void* stream) {
+    int rc = device_check();
+    if (rc) return rc;
+    if (!d_result) return fail(STORMCK_EINVAL, "d_result is null");
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    // d_result = {n, 0}: "no mismatch" until a block lowers it.
+    hipLaunchKernelGGL(k_init_result, dim3(1), dim3(64), 0, st, d_result, n);
+    HIP_TRY(hipGetLastError());
+    if (n == 0) return STORMCK_OK;
+    if (!d_base || !d_expected) return fail(STORMCK_EINVAL, "null device pointer");
+    if (!d_lens && n > 1 && stride < len) return fail(STORMCK_EINVAL, "stride smaller than len (blocks overlap)");
+    return launch_checksum(static_cast<const uint8_t*>(d_base), stride, d_lens, len, nullptr, n, nullptr, d_expected,
+                           reinterpret_cast<unsigned long long*>(d_result),
+                           reinterpret_cast<unsigned long long*>(d_result + 1), st);
+}
+
+int stormck_checksum_host(const void* base, uint64_t stride, const uint32_t* lens, uint32_t len, uint64_t n,
+                          uint64_t* out) {
+    return host_pipeline(base, stride, lens, len, n, out, nullptr, nullptr, nullptr);
+}
+
+int stormck_verify_host(const void* base, uint64_t stride, const uint32_t* lens, uint32_t len, uint64_t n,
+                        const uint64_t* expected, uint64_t* first_bad, uint64_t* n_bad) {
+    if (!expected || !first_bad || !n_bad) return fail(STORMCK_EINVAL, "null argument");
+    int rc = host_pipeline(base, stride, lens, len, n, nullptr, expected, first_bad, n_bad);
+    if (rc) return rc;
+    if (*n_bad > 0) {
+        g_last_error = "checksum mismatch";
+        return STORMCK_EMISMATCH;
+    }
+    return STORMCK_OK;
+}
+
+int stormck_checksum(const void* p, uint64_t n_bytes, uint64_t* out) {
+    if (!out) return fail(STORMCK_EINVAL, "out is null");
+    if (n_bytes > 0xffffffffULL) return fail(STORMCK_EINVAL, "block longer than 4 GiB");
+    static const uint8_t empty = 0;
+    if (n_bytes == 0) p = &empty;  // XXH64 of an empty slice: nothing is read
+    if (!p) return fail(STORMCK_EINVAL, "p is null");
+    return host_pipeline(p, 0, nullptr, static_cast<uint32_t>(n_bytes), 1, out, nullptr, nullptr, nullptr);
+}
+
+int stormck_host_register(void* p, uint64_t bytes) {
+    int rc = device_check();
+    if (rc) return rc;
+    if (!p || bytes == 0) return fail(STORMCK_EINVAL, "empty range");
+    HIP_TRY(hipHostRegister(p, bytes, hipHostRegisterDefault));
+    return STORMCK_OK;
+}
+
+int stormck_host_unregister(void* p) {
+    int rc = device_check();
+    if (rc) return rc;
+    HIP_TRY(hipHostUnregister(p));
+    return STORMCK_OK;
+}
+
+int stormck_pointer_level_device(const uint64_t* d_child_cs, uint64_t m, uint64_t child_addr_base, uint64_t rev,
+                                 uint8_t child_type, uint32_t fanout, uint64_t* d_parent_cs, void* stream) {
+    if (m == 0) return STORMCK_OK;
+    int rc = device_check();
+    if (rc) return rc;
+    if (!d_child_cs || !d_parent_cs) return fail(STORMCK_EINVAL, "null device pointer");
+    if (fanout == 0 || fanout > kMaxFanout) return fail(STORMCK_EINVAL, "fanout out of range");
+    const uint64_t pm = (m + fanout - 1) / fanout;
+    dim3 grid;
+    if (!grid_for(pm * 4, &grid)) return fail(STORMCK_EINVAL, "level too large");
+    hipLaunchKernelGGL(k_pointer_level, grid, dim3(kThreads), 0, static_cast<hipStream_t>(stream), d_child_cs, m,
+                       child_addr_base, rev, child_type, fanout, d_parent_cs);
+    HIP_TRY(hipGetLastError());
+    return STORMCK_OK;
+}
+
+int stormck_pointer_node_device(const stormck_pointer* d_entries, const uint8_t* d_types, uint32_t count,
+                                uint32_t fanout, uint64_t* d_out_cs, void* stream) {
+    int rc = device_check();
+    if (rc) return rc;
+    if (!d_out_cs || (count > 0 && (!d_entries || !d_types))) return fail(STORMCK_EINVAL, "null device pointer");
+    if (fanout == 0 || fanout > kMaxFanout || count > fanout) return fail(STORMCK_EINVAL, "count/fanout out of range");
+    static_assert(sizeof(stormck_pointer) == 24, "Pointer is 24 bytes");
+    hipLaunchKernelGGL(k_pointer_node, dim3(1), dim3(64), 0, static_cast<hipStream_t>(stream),
+                       reinterpret_cast<const uint64_t*>(d_entries), d_types, count, fanout, d_out_cs);
+    HIP_TRY(hipGetLastError());
+    return STORMCK_OK;
+}
+
+int stormck_pack_pointer_blocks_device(const uint64_t* d_child_cs, uint64_t m, uint64_t child_addr_base, uint64_t rev,
+                                       uint8_t child_type, uint32_t fanout, void* d_blocks, uint64_t dst_stride,
+                                       void* stream) {
+    if (m == 0) return STORMCK_OK;
+    int rc = device_check();
+    if (rc) return rc;
+    if (!d_child_cs || !d_blocks) return fail(STORMCK_EINVAL, "null device pointer");
+    if (fanout == 0 || fanout > kMaxFanout) return fail(STORMCK_EINVAL, "fanout out of range");
+    if (dst_stride < pointer_block_size(fanout) || (dst_stride & 7) || (reinterpret_cast<uintptr_t>(d_blocks) & 7))
+        return fail(STORMCK_EINVAL, "dst_stride/d_blocks must be 8-byte aligned and hold a pointer block");
+    hipLaunchKernelGGL(k_pack_pointer_blocks, dim3(2048), dim3(kThreads), 0, static_cast<hipStream_t>(stream),
+                       d_child_cs, m, child_addr_base, rev, child_type, fanout, static_cast<uint8_t*>(d_blocks),
+                       dst_stride);
+    HIP_TRY(hipGetLastError());
+    return STORMCK_OK;
+}
+
+uint64_t stormck_merkle_workspace_bytes(uint64_t n, uint32_t fanout) {
+    if (fanout < 2) return 0;
+    uint64_t total = 0;
+    for (uint64_t m = n; m > 1;) {
+        m = (m + fanout - 1) / fanout;
+        total += m;
+    }
+    return total * 8;
+}
+
+int stormck_merkle_root_device(const uint64_t* d_leaf_cs, uint64_t n, uint64_t leaf_addr_base,
+                               uint64_t node_addr_base, uint64_t rev, uint32_t fanout, void* d_workspace,
+                               uint64_t workspace_bytes, stormck_pointer* d_root, uint8_t* d_root_type,
+                               void* stream) {
+    int rc = device_check();
+    if (rc) return rc;
+    if (!d_root || !d_root_type) return fail(STORMCK_EINVAL, "null root pointer");
+    if (fanout < 2 || fanout > kMaxFanout) return fail(STORMCK_EINVAL, "fanout out of range");
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    uint64_t* root = reinterpret_cast<uint64_t*>(d_root);
+    if (n == 0) {
+        hipLaunchKernelGGL(k_set_root, dim3(1), dim3(64), 0, st, nullptr, 0ULL, 0ULL, static_cast<uint8_t>(STORMCK_FREE_BLOCK),
+                           root, d_root_type);
+        HIP_TRY(hipGetLastError());
+        return STORMCK_OK;
+    }
+    if (!d_leaf_cs) return fail(STORMCK_EINVAL, "d_leaf_cs is null");
+    if (workspace_bytes < stormck_merkle_workspace_bytes(n, fanout) || (n > 1 && !d_workspace))
+        return fail(STORMCK_EINVAL, "workspace too small (stormck_merkle_workspace_bytes)");
+    const uint64_t* cur = d_leaf_cs;
+    uint64_t m = n, addr_base = leaf_addr_base, next_addr = node_addr_base;
+    uint8_t type = STORMCK_LEAF_BLOCK;
+    uint64_t* ws = static_cast<uint64_t*>(d_workspace);
+    while (m > 1) {
+        const uint64_t pm = (m + fanout - 1) / fanout;
+        rc = stormck_pointer_level_device(cur, m, addr_base, rev, type, fanout, ws, st);
+        if (rc) return rc;
+        cur = ws;
+        ws += pm;
+        addr_base = next_addr;
+        next_addr += pm;
+        m = pm;
+        type = STORMCK_POINTER_BLOCK;
+    }
+    hipLaunchKernelGGL(k_set_root, dim3(1), dim3(64), 0, st, cur, addr_base, rev, type, root, d_root_type);
+    HIP_TRY(hipGetLastError());
+    return STORMCK_OK;
+}
+
+int stormck_fill_synthetic_device(void* d_dst, uint64_t stride, uint64_t n, uint64_t first, uint64_t seed,
+                                  void* stream) {
+    if (n == 0) return STORMCK_OK;
+    int rc = device_check();
+    if (rc) return rc;
+    if (!d_dst || (stride & 15) || stride == 0 || (reinterpret_cast<uintptr_t>(d_dst) & 15))
+        return fail(STORMCK_EINVAL, "fill_synthetic needs a 16-byte aligned destination and stride");
+    hipLaunchKernelGGL(k_fill_synthetic, dim3(8192), dim3(kThreads), 0, static_cast<hipStream_t>(stream),
+                       static_cast<uint8_t*>(d_dst), stride, n, first, seed);
+    HIP_TRY(hipGetLastError());
+    return STORMCK_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,154 @@
+"""Device-resident entry points (HBM in, HBM out) over libstormck.
+
+Raw-pointer functions mirror include/stormck.h one to one; the ``*_tensor``
+helpers take torch tensors (torch is plumbing here: device memory and streams)
+and launch on torch's current stream of the tensor's device.
+"""
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+from . import _lib
+from ._lib import check, lib
+
+POINTERS_PER_BLOCK = 1200  # blocks/pointer/params.go:6
+
+
+def checksum_device(d_base: int, stride: int, n: int, d_out: int, length: int = 0, d_lens: int = 0,
+                    stream: int = 0) -> None:
+    check(lib.stormck_checksum_device(d_base, stride, d_lens or None, length, n, d_out, stream or None))
+
+
+def checksum_gather_device(d_base: int, d_offsets: int, n: int, d_out: int, length: int = 0, d_lens: int = 0,
+                           stream: int = 0) -> None:
+    check(lib.stormck_checksum_gather_device(d_base, d_offsets, d_lens or None, length, n, d_out, stream or None))
+
+
+def verify_device(d_base: int, stride: int, n: int, d_expected: int, d_result: int, length: int = 0, d_lens: int = 0,
+                  stream: int = 0) -> None:
+    check(lib.stormck_verify_device(d_base, stride, d_lens or None, length, n, d_expected, d_result, stream or None))
+
+
+def fill_synthetic_device(d_dst: int, stride: int, n: int, first: int, seed: int, stream: int = 0) -> None:
+    check(lib.stormck_fill_synthetic_device(d_dst, stride, n, first, seed, stream or None))
+
+
+def pointer_level_device(d_child_cs: int, m: int, child_addr_base: int, rev: int, child_type: int, fanout: int,
+                         d_parent_cs: int, stream: int = 0) -> None:
+    check(lib.stormck_pointer_level_device(d_child_cs, m, child_addr_base, rev, child_type, fanout, d_parent_cs,
+                                           stream or None))
+
+
+def pointer_node_device(d_entries: int, d_types: int, count: int, fanout: int, d_out_cs: int, stream: int = 0) -> None:
+    check(lib.stormck_pointer_node_device(d_entries or None, d_types or None, count, fanout, d_out_cs, stream or None))
+
+
+def pack_pointer_blocks_device(d_child_cs: int, m: int, child_addr_base: int, rev: int, child_type: int, fanout: int,
+                               d_blocks: int, dst_stride: int, stream: int = 0) -> None:
+    check(lib.stormck_pack_pointer_blocks_device(d_child_cs, m, child_addr_base, rev, child_type, fanout, d_blocks,
+                                                 dst_stride, stream or None))
+
+
+def merkle_workspace_bytes(n: int, fanout: int = POINTERS_PER_BLOCK) -> int:
+    return int(lib.stormck_merkle_workspace_bytes(n, fanout))
+
+
+def merkle_root_device(d_leaf_cs: int, n: int, leaf_addr_base: int, node_addr_base: int, rev: int, fanout: int,
+                       d_workspace: int, workspace_bytes: int, d_root: int, d_root_type: int, stream: int = 0) -> None:
+    check(lib.stormck_merkle_root_device(d_leaf_cs or None, n, leaf_addr_base, node_addr_base, rev, fanout,
+                                         d_workspace or None, workspace_bytes, d_root, d_root_type, stream or None))
+
+
+def init(device: int) -> None:
+    check(lib.stormck_init(device))
+
+
+def shutdown() -> None:
+    lib.stormck_shutdown()
+
+
+# ---------------------------------------------------------------------------
+# torch helpers
+# ---------------------------------------------------------------------------
+
+def _torch():
+    import torch  # local: the C-ABI itself does not need torch
+    return torch
+
+
+def _stream_of(t) -> int:
+    torch = _torch()
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def checksum_tensor(blocks, length: Optional[int] = None, lens=None, out=None):
+    """Checksums of a device tensor of blocks, shape [n, stride] uint8 (row i =
+    block i; ``length`` bytes of each row, default the full row, or ``lens[i]``).
+    Returns an int64 tensor [n] (bit pattern of the uint64 checksums)."""
+    torch = _torch()
+    if blocks.dim() != 2 or blocks.dtype != torch.uint8 or not blocks.is_cuda:
+        raise ValueError("blocks must be a 2-D uint8 CUDA tensor [n, stride]")
+    if blocks.stride(1) != 1:
+        raise ValueError("rows must be contiguous")
+    n, width = blocks.shape
+    stride = blocks.stride(0)
+    if out is None:
+        out = torch.empty(n, dtype=torch.int64, device=blocks.device)
+    d_lens = 0
+    if lens is not None:
+        if lens.dtype != torch.int32 or lens.device != blocks.device or lens.numel() != n:
+            raise ValueError("lens must be an int32 tensor [n] on the blocks' device")
+        if int(lens.max()) > width:
+            raise ValueError("a length exceeds the row width")
+        d_lens = lens.data_ptr()
+        length = 0
+    elif length is None:
+        length = width
+    elif length > width:
+        raise ValueError("length exceeds the row width")
+    checksum_device(blocks.data_ptr(), stride, n, out.data_ptr(), length, d_lens, _stream_of(blocks))
+    return out
+
+
+def merkle_root_tensor(leaf_cs, leaf_addr_base: int, node_addr_base: int, rev: int,
+                       fanout: int = POINTERS_PER_BLOCK, workspace=None):
+    """Shard Merkle root of device leaf checksums (int64 [n]) as an int64 tensor
+    [4] = {Checksum, Address, BirthRevision, BlockType} on the same device."""
+    torch = _torch()
+    n = leaf_cs.numel()
+    need = merkle_workspace_bytes(n, fanout)
+    if workspace is None or workspace.numel() * workspace.element_size() < need:
+        workspace = torch.empty(max(need // 8, 1), dtype=torch.int64, device=leaf_cs.device)
+    root = torch.zeros(4, dtype=torch.int64, device=leaf_cs.device)
+    merkle_root_device(leaf_cs.data_ptr() if n else 0, n, leaf_addr_base, node_addr_base, rev, fanout,
+                       workspace.data_ptr(), workspace.numel() * 8, root.data_ptr(), root.data_ptr() + 24,
+                       _stream_of(leaf_cs))
+    return root
+
+
+def combine_roots_tensor(roots, rev: int, root_addr: int, fanout: int = POINTERS_PER_BLOCK):
+    """Global root from a table of shard roots (int64 [k, 4] rows {cs, addr, rev, type},
+    shard order): one pointer block holding the k root Pointers, hashed on device.
+    Returns int64 [4] {cs, root_addr, rev, Pointer}."""
+    torch = _torch()
+    k = roots.shape[0]
+    if k == 0 or k > fanout:
+        raise ValueError("need 1..fanout shard roots")
+    entries = roots[:, :3].contiguous()
+    types = roots[:, 3].to(torch.uint8).contiguous()
+    out = torch.zeros(4, dtype=torch.int64, device=roots.device)
+    pointer_node_device(entries.data_ptr(), types.data_ptr(), k, fanout, out.data_ptr(), _stream_of(roots))
+    out[1] = root_addr
+    out[2] = rev
+    out[3] = 1  # BlockType Pointer
+    return out
+
+
+def u64(t) -> "object":
+    """int64 tensor -> numpy uint64 (host)."""
+    return t.detach().cpu().numpy().view("uint64")
+
+
+def as_tuple(root) -> Tuple[int, int, int, int]:
+    a = u64(root)
+    return int(a[0]), int(a[1]), int(a[2]), int(a[3])

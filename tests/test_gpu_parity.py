@@ -1,0 +1,335 @@
+"""GPU parity: the gfx950 kernels through the C-ABI vs the oracle and the golden
+fixtures. Bit-exact (integer work). Runs on the MI355X box: pytest -m gpu.
+
+Reference behaviour pinned: blocks.Checksum / BlockChecksum / VerifyChecksum
+(/root/reference/blocks/checksum.go:10-27) = XXH64 seed 0 over the block bytes.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from tests.conftest import hx, load_golden
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from storm_amd import _lib
+    assert _lib.device_count() > 0, "GPU visible to torch but libstormck finds no gfx950 device"
+    return torch.device("cuda:0")
+
+
+def _u64(t):
+    return t.cpu().numpy().view(np.uint64)
+
+
+def _to_dev(a: np.ndarray, dev):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+
+
+# ---------------------------------------------------------------------------
+# known answers / lengths / tails
+# ---------------------------------------------------------------------------
+
+def test_kat_lengths_device(dev):
+    from storm_amd import engine
+    rows = load_golden("kat.json")["rows"]
+    stride = max(r["len"] for r in rows) + 8
+    stride = (stride + 15) // 16 * 16
+    for pattern in ("zeros", "iota"):
+        host = np.zeros((len(rows), stride), dtype=np.uint8)
+        if pattern == "iota":
+            host[:] = (np.arange(stride) & 0xFF).astype(np.uint8)
+        lens = torch.tensor([r["len"] for r in rows], dtype=torch.int32, device=dev)
+        out = engine.checksum_tensor(_to_dev(host, dev), lens=lens)
+        torch.cuda.synchronize()
+        assert [int(v) for v in _u64(out)] == [hx(r[pattern]) for r in rows]
+
+
+def test_public_answers_single_call(dev):
+    from storm_amd import blocks
+    for s, v in load_golden("kat.json")["public"].items():
+        assert blocks.Checksum(s.encode()) == hx(v)
+
+
+# ---------------------------------------------------------------------------
+# c1: 1K synthetic 32 KiB blocks; generator parity
+# ---------------------------------------------------------------------------
+
+def test_synth_c1_device(dev):
+    from storm_amd import engine
+    g = load_golden("synth_c1.json")
+    n, stride = g["n"], g["stride"]
+    buf = torch.empty((n, stride), dtype=torch.uint8, device=dev)
+    engine.fill_synthetic_device(buf.data_ptr(), stride, n, 0, hx(g["seed"]))
+    out = engine.checksum_tensor(buf)
+    torch.cuda.synchronize()
+    assert [int(v) for v in _u64(out)] == [hx(v) for v in g["checksums"]]
+    words = buf.cpu().numpy().view("<u8")
+    for s in g["generator_samples"]:
+        assert int(words[s["block"], s["word"]]) == hx(s["value"])
+
+
+def test_synth_vs_oracle_random_lengths(dev):
+    """Random lengths/offsets (ragged, unaligned) vs the C oracle."""
+    from oracle import oracle as o
+    from storm_amd import engine
+    rng = np.random.default_rng(11)
+    n, stride = 3000, 4096 + 64
+    host = rng.integers(0, 256, size=n * stride, dtype=np.uint8)
+    lens = rng.integers(0, 4096, size=n).astype(np.uint32)
+    lens[:40] = np.arange(40)
+    offs = (np.arange(n, dtype=np.uint64) * stride + rng.integers(0, 57, size=n).astype(np.uint64))
+    want = np.array([o.xxh64(host[int(offs[i]):int(offs[i]) + int(lens[i])]) for i in range(n)], dtype=np.uint64)
+    d = _to_dev(host, dev)
+    d_offs = _to_dev(offs.view(np.int64), dev)
+    d_lens = _to_dev(lens.view(np.int32), dev)
+    out = torch.empty(n, dtype=torch.int64, device=dev)
+    engine.checksum_gather_device(d.data_ptr(), d_offs.data_ptr(), n, out.data_ptr(), 0, d_lens.data_ptr())
+    torch.cuda.synchronize()
+    assert np.array_equal(_u64(out), want)
+    # uniform length, odd base alignment through the strided entry point
+    out2 = torch.empty(n - 1, dtype=torch.int64, device=dev)
+    engine.checksum_device(d.data_ptr() + 3, stride, n - 1, out2.data_ptr(), 1000)
+    torch.cuda.synchronize()
+    want2 = o.checksum_batch(host[3:], n - 1, stride, 1000)
+    assert np.array_equal(_u64(out2), want2)
+
+
+def test_mixed_c5(dev):
+    from storm_amd import engine
+    g = load_golden("mixed.json")
+    lens = g["lens"]
+    n, stride = len(lens), g["stride"]
+    buf = torch.empty((n, stride), dtype=torch.uint8, device=dev)
+    engine.fill_synthetic_device(buf.data_ptr(), stride, n, g["first"], hx(g["seed"]))
+    out = engine.checksum_tensor(buf, lens=torch.tensor(lens, dtype=torch.int32, device=dev))
+    torch.cuda.synchronize()
+    assert [int(v) for v in _u64(out)] == [hx(v) for v in g["checksums"]]
+
+
+def test_empty_and_zero(dev):
+    from storm_amd import blocks, engine
+    assert blocks.Checksum(b"") == 0xEF46DB3751D8E999
+    engine.checksum_device(0, 0, 0, 0, 0)  # n == 0 is a no-op
+    buf = torch.zeros((4, 64), dtype=torch.uint8, device=dev)
+    out = engine.checksum_tensor(buf, length=0)
+    torch.cuda.synchronize()
+    assert all(int(v) == 0xEF46DB3751D8E999 for v in _u64(out))
+
+
+# ---------------------------------------------------------------------------
+# full-size configs: c2 (1M blocks, 32 GiB resident) and c3 (16M blocks via a
+# 4M-block arena, 4 passes) against the libxxhash digests + oracle spot checks
+# ---------------------------------------------------------------------------
+
+def _digest_check(dev, n_total, arena_blocks):
+    from oracle import oracle as o
+    from storm_amd import engine
+    digests = load_golden("synth_digests.json")["digests"][str(n_total)]
+    stride = 32768
+    arena = torch.empty((arena_blocks, stride), dtype=torch.uint8, device=dev)
+    cs = torch.empty(n_total, dtype=torch.int64, device=dev)
+    rng = np.random.default_rng(n_total)
+    for first in range(0, n_total, arena_blocks):
+        cnt = min(arena_blocks, n_total - first)
+        engine.fill_synthetic_device(arena.data_ptr(), stride, cnt, first, o.SYNTH_SEED)
+        engine.checksum_device(arena.data_ptr(), stride, cnt, cs[first:].data_ptr(), stride)
+        torch.cuda.synchronize()
+        # spot-check 64 random blocks of this pass with the oracle on the host
+        idx = rng.integers(0, cnt, size=64)
+        sample = arena[torch.from_numpy(idx).to(dev)].cpu().numpy()
+        want = o.checksum_batch(sample, 64, stride, stride)
+        assert np.array_equal(_u64(cs[first + torch.from_numpy(idx).to(dev)]), want)
+    host = _u64(cs)
+    assert [int(v) for v in host[:8]] == [hx(v) for v in digests["first8"]]
+    assert [int(v) for v in host[::65536]] == [hx(v) for v in digests["every_65536th"]]
+    assert o.xxh64(host.astype("<u8").tobytes()) == hx(digests["digest"])
+    del arena
+
+
+@pytest.mark.slow
+def test_c2_1m_blocks_digest(dev):
+    _digest_check(dev, 1 << 20, 1 << 20)
+
+
+@pytest.mark.slow
+def test_c3_16m_blocks_digest(dev):
+    _digest_check(dev, 1 << 24, 1 << 22)
+
+
+# ---------------------------------------------------------------------------
+# verify (blocks.VerifyChecksum batched)
+# ---------------------------------------------------------------------------
+
+def test_verify_device_and_host(dev):
+    from storm_amd import blocks, engine
+    n, stride = 5000, 1024
+    buf = torch.empty((n, stride), dtype=torch.uint8, device=dev)
+    engine.fill_synthetic_device(buf.data_ptr(), stride, n, 77, 0x1234)
+    good = engine.checksum_tensor(buf)
+    res = torch.zeros(2, dtype=torch.int64, device=dev)
+    engine.verify_device(buf.data_ptr(), stride, n, good.data_ptr(), res.data_ptr(), stride)
+    torch.cuda.synchronize()
+    assert _u64(res).tolist() == [n, 0]
+    bad = good.clone()
+    for i in (4321, 17, 4999):
+        bad[i] ^= 1
+    engine.verify_device(buf.data_ptr(), stride, n, bad.data_ptr(), res.data_ptr(), stride)
+    torch.cuda.synchronize()
+    assert _u64(res).tolist() == [17, 3]
+    # host path: corrupt one byte of block 123
+    host = buf.cpu().numpy().copy()
+    exp = _u64(good)
+    assert blocks.VerifyChecksumBatch(host, n, stride, exp, length=stride) == (n, 0)
+    host[123, 5] ^= 0xFF
+    assert blocks.VerifyChecksumBatch(host, n, stride, exp, length=stride) == (123, 1)
+
+
+def test_host_batch_paths(dev):
+    from oracle import oracle as o
+    from storm_amd import _lib, blocks
+    rng = np.random.default_rng(3)
+    n, stride = 20000, 32768  # 625 MiB: several 256 MiB pipeline chunks
+    host = rng.integers(0, 256, size=(n, stride), dtype=np.uint8)
+    want = o.checksum_batch(host, n, stride, stride, threads=8)
+    assert np.array_equal(blocks.ChecksumBatch(host, n, stride, length=stride), want)
+    lens = rng.integers(0, stride + 1, size=n)
+    want_l = o.checksum_batch(host, n, stride, lens=lens, threads=8)
+    assert np.array_equal(blocks.ChecksumBatch(host, n, stride, lens=lens), want_l)
+    # registered (pinned) memory is DMA'd directly
+    _lib.check(_lib.lib.stormck_host_register(host.ctypes.data, host.nbytes))
+    try:
+        assert np.array_equal(blocks.ChecksumBatch(host, n, stride, length=stride), want)
+    finally:
+        _lib.check(_lib.lib.stormck_host_unregister(host.ctypes.data))
+
+
+# ---------------------------------------------------------------------------
+# Go API mirror, with the reference's relational tests
+# ---------------------------------------------------------------------------
+
+def test_pointer_block_checksum_sequence(dev):
+    # /root/reference/blocks/pointer/block_test.go:11-35
+    from storm_amd import blocks, layouts
+    seq = [hx(v) for v in load_golden("layouts.json")["pointer_block_test_sequence"]]
+    b = layouts.PointerBlock()
+    got = [blocks.BlockChecksum(b)]
+    b.Pointers[0].Checksum = 2
+    got.append(blocks.BlockChecksum(b))
+    b.PointedBlockTypes[0] = blocks.LeafBlockType
+    got.append(blocks.BlockChecksum(b))
+    b.PointedBlockTypes[1] = blocks.LeafBlockType
+    got.append(blocks.BlockChecksum(b))
+    b.Pointers[1].Address = 2
+    got.append(blocks.BlockChecksum(b))
+    b.Pointers[2].Checksum = 4
+    got.append(blocks.BlockChecksum(b))
+    assert got == seq
+    assert len(set(got)) == len(got)  # every field change changes the checksum
+
+
+def test_zero_blocks_and_singularity(dev):
+    from storm_amd import blocks, layouts
+    g = load_golden("layouts.json")
+    for tag in ("prod", "test"):
+        test_tag = tag == "test"
+        f = layouts.TEST_FANOUT if test_tag else None
+        types = {
+            "singularity": layouts.SingularityBlock,
+            "pointer": layouts.pointer_block(f or layouts.POINTERS_PER_BLOCK),
+            "spacelist": layouts.spacelist_block(f or layouts.SPACES_PER_BLOCK),
+            "objectlist": layouts.objectlist_block(f or layouts.CHUNKS_PER_BLOCK),
+            "blob": layouts.BlobBlock,
+        }
+        for name, T in types.items():
+            assert blocks.BlockChecksum(T()) == hx(g["zero_block_checksums"][tag][name]), (tag, name)
+    # singularity round trip (cache/cache_test.go:23-42): checksum over the block with Checksum = 0
+    s = layouts.SingularityBlock.from_buffer_copy(bytes.fromhex(g["singularity_example"]["bytes_hex"]))
+    s.Checksum = 0
+    cs = blocks.BlockChecksum(s)
+    assert cs == hx(g["singularity_example"]["checksum"])
+    s.Checksum = cs
+    copy = layouts.SingularityBlock.from_buffer_copy(bytes(s))
+    copy.Checksum = 0
+    assert blocks.VerifyChecksum(0, bytes(copy), cs) is None
+
+
+def test_verify_checksum_error_format(dev):
+    # blocks/checksum.go:25-26: "checksum mismatch for block %d, computed: %#v, expected: %#v"
+    from storm_amd import blocks
+    err = blocks.VerifyChecksum(42, b"abc", 0)
+    assert isinstance(err, blocks.ChecksumMismatchError)
+    assert str(err) == "checksum mismatch for block 42, computed: 0x44bc2cf5ad770999, expected: 0x0"
+    assert blocks.VerifyChecksum(42, b"abc", 0x44BC2CF5AD770999) is None
+
+
+def test_blob_block_change_changes_checksum(dev):
+    # blocks/blob/block_test.go:13-49
+    from storm_amd import blocks, layouts
+    g = load_golden("layouts.json")["blob_test_block"]
+    b = layouts.BlobBlock()
+    before = blocks.BlockChecksum(b)
+    raw = bytes.fromhex(g["first_128_hex"])
+    ctypes_buf = (layouts.ctypes.c_uint8 * 128).from_buffer(b.Data)
+    ctypes_buf[:] = raw
+    after = blocks.BlockChecksum(b)
+    assert after != before
+    assert after == hx(g["checksum"])
+
+
+# ---------------------------------------------------------------------------
+# Merkle pointer tree
+# ---------------------------------------------------------------------------
+
+def test_merkle_roots_device(dev):
+    from oracle import oracle as o
+    from storm_amd import engine
+    g = load_golden("merkle.json")
+    for c in g["cases"]:
+        leaf = o.synth_leaf_checksums(c["n"], hx(g["seed"]))
+        d_leaf = _to_dev(leaf.view(np.int64), dev)
+        root = engine.merkle_root_tensor(d_leaf, c["leaf_addr_base"], c["node_addr_base"], c["rev"], c["fanout"])
+        r = engine.as_tuple(root)
+        assert list(r[:3]) == [hx(v) for v in c["root"]], c
+        assert r[3] == c["root_type"], c
+
+
+def test_pack_pointer_blocks_materialised(dev):
+    """Materialised pointer blocks hash to the fused level kernel's checksums."""
+    from oracle import oracle as o
+    from storm_amd import engine
+    for fanout, m in ((1200, 5000), (10, 95)):
+        leaf = o.synth_leaf_checksums(m)
+        d_leaf = _to_dev(leaf.view(np.int64), dev)
+        pm = (m + fanout - 1) // fanout
+        size = o.pointer_block_size(fanout)
+        stride = (size + 15) // 16 * 16
+        blocks_buf = torch.zeros((pm, stride), dtype=torch.uint8, device=dev)
+        engine.pack_pointer_blocks_device(d_leaf.data_ptr(), m, 900, 3, 2, fanout, blocks_buf.data_ptr(), stride)
+        fused = torch.empty(pm, dtype=torch.int64, device=dev)
+        engine.pointer_level_device(d_leaf.data_ptr(), m, 900, 3, 2, fanout, fused.data_ptr())
+        via_bytes = engine.checksum_tensor(blocks_buf, length=size)
+        torch.cuda.synchronize()
+        assert np.array_equal(_u64(fused), _u64(via_bytes))
+        host = blocks_buf.cpu().numpy()
+        for j in range(pm):
+            ent = [(int(leaf[k]), 900 + k, 3, 2) for k in range(j * fanout, min(m, (j + 1) * fanout))]
+            assert bytes(host[j, :size]) == o.pack_pointer_block_py(ent, fanout)
+
+
+def test_combine_roots_device(dev):
+    from storm_amd import engine
+    g = load_golden("merkle.json")["combine"]
+    rows = [[hx(v) for v in r[:3]] + [r[3]] for r in g["shard_roots"]]
+    table = torch.tensor(np.array(rows, dtype=np.uint64).view(np.int64), device=dev)
+    groot = engine.combine_roots_tensor(table, g["rev"], 2 * g["n_total"], g["fanout"])
+    r = engine.as_tuple(groot)
+    assert list(r[:3]) == [hx(v) for v in g["global_root"][:3]]
+    assert r[3] == g["global_root"][3]

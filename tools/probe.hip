@@ -1,0 +1,176 @@
+// Design probe for the block-checksum kernels on MI355X (gfx950).
+// Measures, in ONE process (guide §5.4 rule 24):
+//   1. stream-read peak (dwordx4 grid-stride sum, plain / non-temporal)
+//   2. hash-kernel mapping variants (quad / lane, unroll U, NT) on synthetic 32 KiB blocks
+//   3. a compute-only hash loop (no loads) = the VALU ceiling in byte-equivalents
+//   4. v_mul_lo_u32 / v_mad_u64_u32 issue rate vs v_add_u32
+// Every hash variant is checked bit-exact against a host XXH64 of the first blocks.
+// Usage: probe [GiB=64] [reps=5]
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <vector>
+#include <algorithm>
+#include <string>
+#include "../storm_amd/csrc/kernels.h"
+
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { fprintf(stderr, "HIP %s at %s:%d\n", hipGetErrorString(e), __FILE__, __LINE__); exit(1);} } while (0)
+
+using namespace stormck;
+
+// ---- host XXH64 (probe self-check only) ----
+static inline uint64_t hrotl(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
+static inline uint64_t hround(uint64_t a, uint64_t w) { a += w * kP2; a = hrotl(a, 31); return a * kP1; }
+static uint64_t host_xxh64(const uint8_t* p, size_t n) {
+    const uint8_t* e = p + n; uint64_t h;
+    if (n >= 32) {
+        uint64_t v1 = kV1, v2 = kV2, v3 = kV3, v4 = kV4;
+        do { uint64_t w[4]; memcpy(w, p, 32); v1 = hround(v1, w[0]); v2 = hround(v2, w[1]); v3 = hround(v3, w[2]); v4 = hround(v4, w[3]); p += 32; } while (p + 32 <= e);
+        h = hrotl(v1, 1) + hrotl(v2, 7) + hrotl(v3, 12) + hrotl(v4, 18);
+        uint64_t vs[4] = {v1, v2, v3, v4};
+        for (int i = 0; i < 4; ++i) { h ^= hround(0, vs[i]); h = h * kP1 + kP4; }
+    } else h = kP5;
+    h += n;
+    while (p + 8 <= e) { uint64_t w; memcpy(&w, p, 8); h ^= hround(0, w); h = hrotl(h, 27) * kP1 + kP4; p += 8; }
+    if (p + 4 <= e) { uint32_t w; memcpy(&w, p, 4); h ^= (uint64_t)w * kP1; h = hrotl(h, 23) * kP2 + kP3; p += 4; }
+    while (p < e) { h ^= (*p) * kP5; h = hrotl(h, 11) * kP1; ++p; }
+    h ^= h >> 33; h *= kP2; h ^= h >> 29; h *= kP3; h ^= h >> 32; return h;
+}
+
+// ---- read-peak kernels ----
+template <bool NT>
+__global__ __launch_bounds__(256) void k_readpeak(const u64x2* __restrict__ p, uint64_t n16, uint64_t* out) {
+    u64x2 acc = {0, 0};
+    const uint64_t stride = (uint64_t)gridDim.x * 256;
+    uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    for (; i + 3 * stride < n16; i += 4 * stride) {
+        u64x2 a = ldg<NT>(p + i), b = ldg<NT>(p + i + stride), c = ldg<NT>(p + i + 2 * stride), d = ldg<NT>(p + i + 3 * stride);
+        acc ^= a ^ b ^ c ^ d;
+    }
+    for (; i < n16; i += stride) acc ^= ldg<NT>(p + i);
+    if ((acc.x ^ acc.y) == 0x1234567) out[0] = acc.x;  // practically never: keeps loads live
+}
+
+// ---- compute-only ceiling: same quad loop with register-synthesised words ----
+__global__ __launch_bounds__(256) void k_compute_only(uint32_t nst, uint64_t* out) {
+    uint64_t acc = acc_seed(threadIdx.x & 3);
+    uint64_t w = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    for (uint32_t s = 0; s < nst; s += 4) {
+        acc = round(acc, w); acc = round(acc, w + 1); acc = round(acc, w + 2); acc = round(acc, w + 3);
+        w += acc >> 60;
+    }
+    if (acc == 0x1234567) out[0] = acc;
+}
+
+// ---- multiply issue rate ----
+template <int MODE>
+__global__ __launch_bounds__(256) void k_mulrate(uint32_t iters, uint32_t* out) {
+    uint32_t a0 = threadIdx.x, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 5, a5 = a0 + 7, a6 = a0 + 11, a7 = a0 + 13;
+    const uint32_t c = 0x9E3779B1u + blockIdx.x;
+    for (uint32_t i = 0; i < iters; ++i) {
+        if (MODE == 0) {  // v_mul_lo_u32
+            a0 *= c; a1 *= c; a2 *= c; a3 *= c; a4 *= c; a5 *= c; a6 *= c; a7 *= c;
+        } else if (MODE == 1) {  // v_add_u32
+            a0 += c; a1 += c; a2 += c; a3 += c; a4 += c; a5 += c; a6 += c; a7 += c;
+        } else {  // v_mad_u64_u32 (64-bit product of 32-bit operands)
+            uint64_t t0 = (uint64_t)a0 * c + a1, t1 = (uint64_t)a2 * c + a3, t2 = (uint64_t)a4 * c + a5, t3 = (uint64_t)a6 * c + a7;
+            a0 = (uint32_t)t0; a1 = (uint32_t)(t0 >> 32); a2 = (uint32_t)t1; a3 = (uint32_t)(t1 >> 32);
+            a4 = (uint32_t)t2; a5 = (uint32_t)(t2 >> 32); a6 = (uint32_t)t3; a7 = (uint32_t)(t3 >> 32);
+        }
+    }
+    uint32_t r = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;
+    if (r == 0x1234567) out[0] = r;
+}
+
+struct Timer {
+    hipEvent_t a, b;
+    Timer() { CK(hipEventCreate(&a)); CK(hipEventCreate(&b)); }
+    void start() { CK(hipEventRecord(a, 0)); }
+    float stop() { CK(hipEventRecord(b, 0)); CK(hipEventSynchronize(b)); float ms; CK(hipEventElapsedTime(&ms, a, b)); return ms; }
+};
+
+static int g_reps = 5;
+
+template <typename F>
+static void bench(const char* name, double bytes, F launch) {
+    Timer t;
+    launch();  // warm
+    CK(hipDeviceSynchronize());
+    std::vector<float> ms;
+    for (int r = 0; r < g_reps; ++r) { t.start(); launch(); ms.push_back(t.stop()); }
+    std::sort(ms.begin(), ms.end());
+    double best = bytes / (ms[0] * 1e-3) / 1e9, med = bytes / (ms[ms.size() / 2] * 1e-3) / 1e9;
+    printf("%-34s best %8.3f ms  %8.1f GB/s (%.3f of 8 TB/s)   median %8.1f GB/s\n", name, ms[0], best, best / 8000.0, med);
+    fflush(stdout);
+}
+
+int main(int argc, char** argv) {
+    double gib = argc > 1 ? atof(argv[1]) : 64.0;
+    g_reps = argc > 2 ? atoi(argv[2]) : 5;
+    const uint64_t L = 32768;
+    const uint64_t n = (uint64_t)(gib * 1073741824.0) / L;
+    const uint64_t bytes = n * L;
+    hipDeviceProp_t prop; CK(hipGetDeviceProperties(&prop, 0));
+    printf("device %s  CUs %d  clock %d kHz  blocks %llu (%.1f GiB)\n", prop.gcnArchName, prop.multiProcessorCount, prop.clockRate, (unsigned long long)n, bytes / 1073741824.0);
+    uint8_t* d; CK(hipMalloc(&d, bytes));
+    uint64_t* out; CK(hipMalloc(&out, n * 8));
+    uint64_t* sink; CK(hipMalloc(&sink, 64));
+    const uint64_t seed = 0x53544f524dULL;
+    hipLaunchKernelGGL(k_fill_synthetic, dim3(8192), dim3(256), 0, 0, d, L, n, 0ULL, seed);
+    CK(hipDeviceSynchronize());
+
+    // host reference for the first K blocks
+    const uint64_t K = std::min<uint64_t>(n, 2048);
+    std::vector<uint8_t> hb(K * L);
+    CK(hipMemcpy(hb.data(), d, K * L, hipMemcpyDeviceToHost));
+    std::vector<uint64_t> ref(K);
+    for (uint64_t i = 0; i < K; ++i) ref[i] = host_xxh64(hb.data() + i * L, L);
+    std::vector<uint64_t> got(K);
+    auto check = [&](const char* name) {
+        CK(hipMemcpy(got.data(), out, K * 8, hipMemcpyDeviceToHost));
+        uint64_t bad = 0; for (uint64_t i = 0; i < K; ++i) bad += got[i] != ref[i];
+        if (bad) printf("  !! %s: %llu / %llu mismatches\n", name, (unsigned long long)bad, (unsigned long long)K);
+        CK(hipMemset(out, 0, K * 8));
+    };
+
+    // 1. read peak
+    for (int grid : {2048, 4096, 16384}) {
+        char nm[64];
+        snprintf(nm, 64, "readpeak plain grid=%d", grid);
+        bench(nm, (double)bytes, [&] { hipLaunchKernelGGL(k_readpeak<false>, dim3(grid), dim3(256), 0, 0, (const u64x2*)d, bytes / 16, sink); });
+        snprintf(nm, 64, "readpeak nt grid=%d", grid);
+        bench(nm, (double)bytes, [&] { hipLaunchKernelGGL(k_readpeak<true>, dim3(grid), dim3(256), 0, 0, (const u64x2*)d, bytes / 16, sink); });
+    }
+
+    // 2. hash variants
+    const dim3 gq((unsigned)((n * 4 + 255) / 256));
+    const dim3 gl((unsigned)((n + 255) / 256));
+#define QUAD(U, NT) do { \
+        bench("quad U=" #U " nt=" #NT, (double)bytes, [&] { hipLaunchKernelGGL((k_xxh64_quad<U, false, false, false, NT>), gq, dim3(256), 0, 0, d, L, nullptr, (uint32_t)L, nullptr, n, out, nullptr, nullptr, nullptr); }); \
+        check("quad U=" #U " nt=" #NT); } while (0)
+    QUAD(4, true); QUAD(8, true); QUAD(16, true); QUAD(8, false); QUAD(16, false); QUAD(32, true);
+#define LANE(U, NT) do { \
+        bench("lane U=" #U " nt=" #NT, (double)bytes, [&] { hipLaunchKernelGGL((k_xxh64_lane<U, NT>), gl, dim3(256), 0, 0, d, L, (uint32_t)L, n, out); }); \
+        check("lane U=" #U " nt=" #NT); } while (0)
+    LANE(1, true); LANE(2, true); LANE(4, true); LANE(2, false); LANE(4, false);
+
+    // 3. compute-only ceiling (byte-equivalent: 8 B per lane per round)
+    {
+        const uint32_t nst = 1024; const unsigned grid = 256 * 32;
+        double eq = (double)grid * 256 * nst * 8.0;
+        bench("compute-only (byte-equivalent)", eq, [&] { hipLaunchKernelGGL(k_compute_only, dim3(grid), dim3(256), 0, 0, nst, sink); });
+    }
+    // 4. multiply rate: report Gop/s per CU-cycle via "bytes" = ops
+    {
+        const uint32_t it = 1 << 16; const unsigned grid = 256 * 16;
+        double ops = (double)grid * 256 * it * 8.0;
+        printf("(rates below: 'GB/s' column = G lane-ops/s; full-rate ceiling = 256 CU x 128 lanes x clk)\n");
+        bench("mul_lo_u32", ops, [&] { hipLaunchKernelGGL(k_mulrate<0>, dim3(grid), dim3(256), 0, 0, it, (uint32_t*)sink); });
+        bench("add_u32", ops, [&] { hipLaunchKernelGGL(k_mulrate<1>, dim3(grid), dim3(256), 0, 0, it, (uint32_t*)sink); });
+        bench("mad_u64_u32 (x4 per 8 ops)", ops, [&] { hipLaunchKernelGGL(k_mulrate<2>, dim3(grid), dim3(256), 0, 0, it, (uint32_t*)sink); });
+    }
+    CK(hipFree(d)); CK(hipFree(out)); CK(hipFree(sink));
+    printf("done\n");
+    return 0;
+}
