@@ -52,7 +52,7 @@ def cpu_baseline(seconds: float):
     import numpy as np
     from oracle import oracle as o
 
-    n = 2048  # 64 MiB sample, regenerated identically to the GPU arena's first blocks
+    n = 32768  # 1 GiB sample (larger than the host LLC), the GPU arena's first blocks
     buf = o.fill_synthetic(n, BLOCK, 0)
     out = o.checksum_batch(buf, n, BLOCK, BLOCK)  # warm
     reps, t0 = 0, time.perf_counter()
@@ -74,7 +74,7 @@ def cpu_baseline(seconds: float):
     multi = reps_mt * n * BLOCK / el_mt / 2**30
     assert int(out[0]) == int(o.checksum_batch(buf[:BLOCK], 1, BLOCK, BLOCK)[0])
     return {"value": round(one, 3), "unit": "GiB/s", "cores": 1, "kind": "port",
-            "sample": f"{n} x 32 KiB synthetic blocks (64 MiB) hashed {reps}x in {el:.1f} s by oracle/xxh64_oracle.c "
+            "sample": f"{n} x 32 KiB synthetic blocks (1 GiB) hashed {reps}x in {el:.1f} s by oracle/xxh64_oracle.c "
                       f"(-O3, 1 thread); Go reference unbuildable here (no Go toolchain)",
             "all_threads": {"value": round(multi, 3), "threads": threads}}
 
