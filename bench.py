@@ -31,6 +31,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X spec, /opt/skills/guides/MI355X_MICROARCH.md (ch
 BLOCK = 32768          # blocks.BlockSize, /root/reference/blocks/types.go:4
 FANOUT = 1200          # pointer.PointersPerBlock, /root/reference/blocks/pointer/params.go:6
 REV = 1
+KERNEL = "k_xxh64_glds<16,3,nt>"  # dominant kernel (storm_amd/csrc/kernels.h), as named in profiles/traffic.json
 
 
 def parse():
@@ -164,7 +165,7 @@ def main():
     if os.path.exists(tpath):
         with open(tpath) as f:
             tj = json.load(f)
-        if tj.get("arena_blocks") == arena_n:
+        if tj.get("arena_blocks") == arena_n and tj.get("kernel") == KERNEL:
             traffic = tj.get("hbm_bytes_per_launch")
 
     if rank == 0:
@@ -179,7 +180,7 @@ def main():
                        "passes_per_step": passes, "parallelism": f"dp{world} (contiguous block ranges)"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "kernel": "k_xxh64_quad<16>", "avg_launch_ms": round(avg_ms, 4),
+                         "kernel": KERNEL, "avg_launch_ms": round(avg_ms, 4),
                          "algorithmic_bytes_per_launch": int(alg_bytes)},
             "root": "0x%016x" % root_t[0],
         }

@@ -165,6 +165,131 @@ __global__ __launch_bounds__(256) void k_xxh64_quad(const uint8_t* __restrict__ 
 }
 
 // ---------------------------------------------------------------------------
+// LDS-staged quad kernel ("glds"): uniform length, 16-byte aligned base/stride.
+// A 256-thread workgroup owns 64 consecutive blocks. Tiles of T stripes (32*T bytes)
+// of all 64 blocks stream HBM -> LDS with global_load_lds_dwordx4 (each wave-
+// instruction moves 1 KiB: 64 lanes x 16 B, 16 B contiguous per lane; the LDS
+// destination is lane-linear, so the layout is set by the per-lane SOURCE address)
+// into a ring of R tile slots, R-1 tiles ahead of the hashing. Lane (b, j) of the
+// quad for block b then reads word j of each stripe with ds_read_b64.
+// Bank-conflict-free reads: within block b's row, 16-byte piece q holds source piece
+// (q + rot(b)) mod 2T, so the 8 blocks read by one 32-lane ds_read_b64 group hit 32
+// distinct 8-byte bank pairs.
+// ---------------------------------------------------------------------------
+template <int T>
+__device__ __forceinline__ uint32_t glds_rot(uint32_t b) {
+    constexpr uint32_t pieces = 2 * T;
+    if constexpr (T >= 8) return (2 * b) % pieces;
+    else return (2 * (b / (8 / T))) % pieces;
+}
+
+// s_waitcnt vmcnt(N) only (expcnt / lgkmcnt left at their "don't wait" maxima).
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+    static_assert(N >= 0 && N < 64, "vmcnt range");
+    constexpr int imm = (N & 0xF) | ((N >> 4) << 14) | (0x7 << 4) | (0xF << 8);
+#if defined(__HIP_DEVICE_COMPILE__)
+    __builtin_amdgcn_s_waitcnt(imm);
+#endif
+}
+
+// One tile's worth of this wave's LDS-DMA pieces: instruction k moves 64 x 16 B from
+// the lanes' sources (advanced by t tiles) to dst + k*1024 (lane-linear). A macro:
+// the builtin's size/aux operands must stay literal constants.
+#if defined(__HIP_DEVICE_COMPILE__)  // target builtin: device pass only (host pass only emits the stub)
+#define STORMCK_GLDS_ISSUE(SRC, DST, T_, NK, ROW_, AUX_)                                              \
+    do {                                                                                           \
+        _Pragma("unroll") for (int k_ = 0; k_ < (NK); ++k_)                                        \
+            __builtin_amdgcn_global_load_lds((SRC)[k_] + static_cast<uint64_t>(T_) * (ROW_),       \
+                                             (DST) + k_ * 1024, 16, 0, (AUX_));                    \
+    } while (0)
+#else
+#define STORMCK_GLDS_ISSUE(SRC, DST, T_, NK, ROW_, AUX_) do { } while (0)
+#endif
+
+template <int T, int R, int AUX, bool HASH = true, bool VERIFY = false>
+__global__ __launch_bounds__(256) void k_xxh64_glds(const uint8_t* __restrict__ base, uint64_t stride, uint32_t len,
+                                                     uint64_t n, uint64_t* __restrict__ out,
+                                                     const uint64_t* __restrict__ expected = nullptr,
+                                                     unsigned long long* __restrict__ first_bad = nullptr,
+                                                     unsigned long long* __restrict__ n_bad = nullptr) {
+    constexpr int BPW = 64;                 // blocks per workgroup
+    constexpr int ROW = 32 * T;             // bytes per block per tile
+    constexpr int TILE = BPW * ROW;         // bytes per tile
+    constexpr int INSTR = TILE / 1024;      // glds wave-instructions per tile (whole workgroup)
+    constexpr int PER_WAVE = INSTR / 4;     // ... per wave
+    static_assert(INSTR % 4 == 0, "tile must split evenly over 4 waves");
+    static_assert(R >= 2, "ring needs >= 2 slots");
+    __shared__ __attribute__((aligned(16))) uint8_t lds[R * TILE];
+
+    const uint32_t tid = threadIdx.x;
+    const uint32_t wave = tid >> 6, lane = tid & 63;
+    const uint64_t blk0 = static_cast<uint64_t>(blockIdx.x) * BPW;
+    const uint32_t nst = len >> 5;
+    const uint32_t ntiles = nst / T;
+
+    // Per-lane source pointers of this wave's PER_WAVE instructions (tile 0).
+    const uint8_t* src[PER_WAVE];
+#pragma unroll
+    for (int k = 0; k < PER_WAVE; ++k) {
+        const uint32_t ii = wave * PER_WAVE + k;            // instruction index within the tile
+        const uint32_t off = ii * 1024 + lane * 16;          // byte offset in the tile image
+        const uint32_t b = off / ROW, q = (off % ROW) / 16;  // block row, LDS piece
+        const uint32_t p = (q + glds_rot<T>(b)) % (2 * T);  // source piece
+        uint64_t gb = blk0 + b;
+        if (gb >= n) gb = n - 1;                             // shadow the last block; never stored
+        src[k] = base + gb * stride + p * 16;
+    }
+
+    const uint32_t b = tid >> 2, j = tid & 3;
+    const uint32_t rot = glds_rot<T>(b);
+    uint64_t acc = acc_seed(j);
+
+    // prologue: R-1 tiles in flight
+#pragma unroll
+    for (int t = 0; t < R - 1; ++t)
+        if (t < static_cast<int>(ntiles))
+            STORMCK_GLDS_ISSUE(src, lds + (t % R) * TILE + wave * PER_WAVE * 1024, t, PER_WAVE, ROW, AUX);
+
+    for (uint32_t t = 0; t < ntiles; ++t) {
+        // tile t landed (this wave's pieces), then every wave's pieces
+        if (t + R - 2 < ntiles) wait_vmcnt<PER_WAVE * (R - 2)>();
+        else wait_vmcnt<0>();
+        __builtin_amdgcn_s_barrier();
+        // all waves finished reading tile t-1: refill its slot with tile t+R-1
+        if (t + R - 1 < ntiles)
+            STORMCK_GLDS_ISSUE(src, lds + ((t + R - 1) % R) * TILE + wave * PER_WAVE * 1024, t + R - 1, PER_WAVE, ROW, AUX);
+        const uint8_t* row = lds + (t % R) * TILE + b * ROW + (j & 1) * 8;
+#pragma unroll
+        for (int s = 0; s < T; ++s) {
+            const uint32_t q = (2 * s + (j >> 1) + 2 * T - rot) % (2 * T);
+            const uint64_t w = *reinterpret_cast<const uint64_t*>(row + q * 16);
+            if constexpr (HASH) acc = round(acc, w);
+            else acc ^= w;  // measurement control: same data movement, no hash arithmetic
+        }
+    }
+    // remainder stripes + tail straight from global memory (none for 32 KiB blocks)
+    const uint64_t gbk = blk0 + b;
+    const uint64_t gb = gbk < n ? gbk : n - 1;
+    const uint8_t* blk_src = base + gb * stride;
+    for (uint32_t s = ntiles * T; s < nst; ++s)
+        acc = round(acc, reinterpret_cast<const uint64_t*>(blk_src)[4 * s + j]);
+    const uint64_t v1 = quad_bcast<0>(acc), v2 = quad_bcast<1>(acc), v3 = quad_bcast<2>(acc), v4 = quad_bcast<3>(acc);
+    if (j == 0 && gbk < n) {
+        const uint64_t h0 = (len >= 32) ? converge(v1, v2, v3, v4) : kP5;
+        const uint64_t h = finish_fast(h0, len, blk_src + 32 * static_cast<uint64_t>(nst), len & 31);
+        if constexpr (VERIFY) {
+            if (h != expected[gbk]) {
+                atomicMin(first_bad, static_cast<unsigned long long>(gbk));
+                atomicAdd(n_bad, 1ULL);
+            }
+        } else {
+            out[gbk] = h;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Lane kernel: 1 lane per block, uniform length, 16-byte aligned blocks
 // (base % 16 == 0, stride % 16 == 0). U stripes (2U dwordx4) per pipelined group.
 // ---------------------------------------------------------------------------

@@ -34,10 +34,17 @@ int fail(int code, const std::string& msg) {
                         std::string(#expr) + ": " + hipGetErrorString(e_));                        \
     } while (0)
 
-// Stripe-loop unroll of the production quad kernel: 16 x 8-byte loads in flight per
+// Stripe-loop unroll of the general quad kernel: 16 x 8-byte loads in flight per
 // lane per pipelined group (design probe, profiles/r01_probe.txt: U=16 with plain
 // loads is the fastest quad variant; non-temporal loads cost 35%).
 constexpr int kU = 16;
+// LDS-staged fast path (profiles/r01_probe_ab.txt): tiles of 16 stripes (512 B per
+// block, 32 KiB per 64-block tile), a ring of 3 tiles (96 KiB LDS), non-temporal
+// LDS-DMA (aux = 2). All T/R variants measured within ~1.5%; this one divides
+// storm's 32 KiB blocks into whole tiles.
+constexpr int kTileStripes = 16;
+constexpr int kRing = 3;
+constexpr int kAuxNT = 2;
 constexpr unsigned kThreads = 256;
 constexpr uint32_t kMaxFanout = 1u << 16;
 
@@ -74,10 +81,25 @@ bool grid_for(uint64_t threads, dim3* grid) {
 int launch_checksum(const uint8_t* base, uint64_t stride, const uint32_t* lens, uint32_t len, const uint64_t* offs,
                     uint64_t n, uint64_t* out, const uint64_t* expected, unsigned long long* first_bad,
                     unsigned long long* n_bad, hipStream_t st) {
+    const bool verify = expected != nullptr;
+    // Fast path: uniform length, 16-byte aligned blocks at a fixed stride, at least one
+    // LDS tile per block -> LDS-staged kernel (global_load_lds, non-temporal).
+    if (!lens && !offs && (reinterpret_cast<uintptr_t>(base) & 15) == 0 && (stride & 15) == 0 &&
+        len >= 32u * kTileStripes) {
+        const uint64_t wgs = (n + 63) / 64;
+        if (wgs > 0x7fffffffULL) return fail(STORMCK_EINVAL, "batch too large for one launch");
+        if (verify)
+            hipLaunchKernelGGL((k_xxh64_glds<kTileStripes, kRing, kAuxNT, true, true>), dim3(static_cast<unsigned>(wgs)),
+                               dim3(kThreads), 0, st, base, stride, len, n, out, expected, first_bad, n_bad);
+        else
+            hipLaunchKernelGGL((k_xxh64_glds<kTileStripes, kRing, kAuxNT, true, false>), dim3(static_cast<unsigned>(wgs)),
+                               dim3(kThreads), 0, st, base, stride, len, n, out, expected, first_bad, n_bad);
+        HIP_TRY(hipGetLastError());
+        return STORMCK_OK;
+    }
     dim3 grid;
     if (!grid_for(n * 4, &grid)) return fail(STORMCK_EINVAL, "batch too large for one launch");
-    const bool verify = expected != nullptr;
-    // Dispatch on the compile-time shape (per-block lengths / explicit offsets / verify).
+    // General path (per-block lengths / explicit offsets / any alignment): register quad kernel.
 #define STORMCK_LAUNCH(LENS, OFFS, VER)                                                                         \
     hipLaunchKernelGGL((k_xxh64_quad<kU, LENS, OFFS, VER>), grid, dim3(kThreads), 0, st, base, stride, lens, len, \
                        offs, n, out, expected, first_bad, n_bad)

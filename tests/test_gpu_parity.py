@@ -102,6 +102,31 @@ def test_synth_vs_oracle_random_lengths(dev):
     assert np.array_equal(_u64(out2), want2)
 
 
+@pytest.mark.parametrize("length", [512, 513, 520, 1000, 8192, 28808, 30000, 31808, 32768])
+def test_uniform_fast_path_lengths(dev, length):
+    """Uniform-length 16-byte-aligned batches take the LDS-staged kernel: whole tiles,
+    remainder stripes and tails, partial last workgroup (n % 64 != 0)."""
+    from oracle import oracle as o
+    from storm_amd import engine
+    rng = np.random.default_rng(length)
+    stride = (length + 15) // 16 * 16 + 16 * (length % 3)
+    for n in (1, 63, 64, 65, 1000):
+        host = rng.integers(0, 256, size=(n, stride), dtype=np.uint8)
+        out = engine.checksum_tensor(_to_dev(host, dev), length=length)
+        torch.cuda.synchronize()
+        want = o.checksum_batch(host, n, stride, length)
+        assert np.array_equal(_u64(out), want), (length, n)
+    # verify through the same path
+    d = _to_dev(host, dev)
+    exp = torch.from_numpy(want.view(np.int64).copy()).to(dev)
+    exp[999] ^= 1
+    exp[500] ^= 1
+    res = torch.zeros(2, dtype=torch.int64, device=dev)
+    engine.verify_device(d.data_ptr(), stride, 1000, exp.data_ptr(), res.data_ptr(), length)
+    torch.cuda.synchronize()
+    assert _u64(res).tolist() == [500, 2]
+
+
 def test_mixed_c5(dev):
     from storm_amd import engine
     g = load_golden("mixed.json")

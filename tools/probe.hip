@@ -5,7 +5,7 @@
 //   3. a compute-only hash loop (no loads) = the VALU ceiling in byte-equivalents
 //   4. v_mul_lo_u32 / v_mad_u64_u32 issue rate vs v_add_u32
 // Every hash variant is checked bit-exact against a host XXH64 of the first blocks.
-// Usage: probe [GiB=64] [reps=5]
+// Usage: probe [GiB=64] [reps=5] [rounds=3]
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -13,6 +13,7 @@
 #include <vector>
 #include <algorithm>
 #include <string>
+#include <functional>
 #include "../storm_amd/csrc/kernels.h"
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { fprintf(stderr, "HIP %s at %s:%d\n", hipGetErrorString(e), __FILE__, __LINE__); exit(1);} } while (0)
@@ -134,26 +135,34 @@ int main(int argc, char** argv) {
         CK(hipMemset(out, 0, K * 8));
     };
 
-    // 1. read peak
-    for (int grid : {2048, 4096, 16384}) {
-        char nm[64];
-        snprintf(nm, 64, "readpeak plain grid=%d", grid);
-        bench(nm, (double)bytes, [&] { hipLaunchKernelGGL(k_readpeak<false>, dim3(grid), dim3(256), 0, 0, (const u64x2*)d, bytes / 16, sink); });
-        snprintf(nm, 64, "readpeak nt grid=%d", grid);
-        bench(nm, (double)bytes, [&] { hipLaunchKernelGGL(k_readpeak<true>, dim3(grid), dim3(256), 0, 0, (const u64x2*)d, bytes / 16, sink); });
-    }
-
-    // 2. hash variants
+    // Interleaved A/B over rounds (guide §5.4 rule 24): every variant once per round.
+    const int rounds = argc > 3 ? atoi(argv[3]) : 3;
     const dim3 gq((unsigned)((n * 4 + 255) / 256));
-    const dim3 gl((unsigned)((n + 255) / 256));
-#define QUAD(U, NT) do { \
-        bench("quad U=" #U " nt=" #NT, (double)bytes, [&] { hipLaunchKernelGGL((k_xxh64_quad<U, false, false, false, NT>), gq, dim3(256), 0, 0, d, L, nullptr, (uint32_t)L, nullptr, n, out, nullptr, nullptr, nullptr); }); \
-        check("quad U=" #U " nt=" #NT); } while (0)
-    QUAD(4, true); QUAD(8, true); QUAD(16, true); QUAD(8, false); QUAD(16, false); QUAD(32, true);
-#define LANE(U, NT) do { \
-        bench("lane U=" #U " nt=" #NT, (double)bytes, [&] { hipLaunchKernelGGL((k_xxh64_lane<U, NT>), gl, dim3(256), 0, 0, d, L, (uint32_t)L, n, out); }); \
-        check("lane U=" #U " nt=" #NT); } while (0)
-    LANE(1, true); LANE(2, true); LANE(4, true); LANE(2, false); LANE(4, false);
+    const dim3 gg((unsigned)((n + 63) / 64));
+    struct V { std::string name; std::function<void()> f; bool hash; };
+    std::vector<V> vs;
+    vs.push_back({"readpeak nt grid=16384", [&] { hipLaunchKernelGGL(k_readpeak<true>, dim3(16384), dim3(256), 0, 0, (const u64x2*)d, bytes / 16, sink); }, false});
+    vs.push_back({"quad U=16", [&] { hipLaunchKernelGGL((k_xxh64_quad<16, false, false, false, false>), gq, dim3(256), 0, 0, d, L, nullptr, (uint32_t)L, nullptr, n, out, nullptr, nullptr, nullptr); }, true});
+#define GV(T, R, AUX) vs.push_back({"glds T=" #T " R=" #R " aux=" #AUX, [&] { hipLaunchKernelGGL((k_xxh64_glds<T, R, AUX>), gg, dim3(256), 0, 0, d, L, (uint32_t)L, n, out, nullptr, nullptr, nullptr); }, true})
+    GV(12, 3, 2); GV(16, 2, 2); GV(16, 3, 2); GV(24, 3, 2); GV(20, 3, 2); GV(32, 2, 2); GV(16, 3, 3); GV(16, 3, 18); GV(16, 3, 19); GV(24, 3, 18);
+    std::vector<std::vector<double>> gbs(vs.size());
+    for (int r = 0; r < rounds; ++r) {
+        for (size_t v = 0; v < vs.size(); ++v) {
+            Timer t;
+            vs[v].f();
+            CK(hipDeviceSynchronize());
+            if (r == 0 && vs[v].hash) check(vs[v].name.c_str());
+            for (int k = 0; k < g_reps; ++k) {
+                t.start(); vs[v].f(); float ms = t.stop();
+                gbs[v].push_back(bytes / (ms * 1e-3) / 1e9);
+            }
+        }
+    }
+    for (size_t v = 0; v < vs.size(); ++v) {
+        auto g = gbs[v]; std::sort(g.begin(), g.end());
+        printf("%-28s max %7.1f  median %7.1f  min %7.1f GB/s  (median %.3f of 8 TB/s)\n", vs[v].name.c_str(), g.back(), g[g.size() / 2], g[0], g[g.size() / 2] / 8000.0);
+    }
+    fflush(stdout);
 
     // 3. compute-only ceiling (byte-equivalent: 8 B per lane per round)
     {
