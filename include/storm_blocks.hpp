@@ -1,0 +1,190 @@
+// storm_blocks.hpp — C++ mirror of storm's Go package `blocks` over libstormck.
+//
+// Same names, argument meaning and error behaviour as the reference:
+//   Hash, BlockAddress, BlockSize, BlockType, Pointer      blocks/types.go:4-39
+//   Checksum(b)                                            blocks/checksum.go:15-17
+//   BlockChecksum(&block)                                  blocks/checksum.go:10-12
+//   VerifyChecksum(address, p, expected) -> error or nil   blocks/checksum.go:20-27
+// plus ChecksumBatch / VerifyChecksumBatch, the entry points the GPU path exists for.
+// Block layouts (Go amd64, padding included) mirror blocks/{pointer,blob,objectlist,
+// spacelist,singularity}/block.go; the `test` build-tag fan-outs are template args.
+//
+// Every hash is computed on the gfx950 device by libstormck; a device failure throws
+// storm::blocks::DeviceError (Go's Checksum cannot fail, so there is no error value).
+#pragma once
+
+#include <cstddef>
+#include <cstdint>
+#include <cstdio>
+#include <optional>
+#include <stdexcept>
+#include <string>
+#include <type_traits>
+#include <vector>
+
+#include "stormck.h"
+
+namespace storm::blocks {
+
+using Hash = uint64_t;
+using BlockAddress = uint64_t;
+using ObjectID = uint64_t;
+using SpaceID = uint64_t;
+
+inline constexpr int64_t BlockSize = 32 * 1024;
+
+enum BlockType : uint8_t { FreeBlockType = 0, PointerBlockType = 1, LeafBlockType = 2 };
+
+struct Pointer {
+    Hash Checksum;
+    BlockAddress Address;
+    uint64_t BirthRevision;
+};
+static_assert(sizeof(Pointer) == 24 && sizeof(Pointer) == sizeof(stormck_pointer));
+
+class DeviceError : public std::runtime_error {
+public:
+    explicit DeviceError(int code)
+        : std::runtime_error("stormck error " + std::to_string(code) + ": " + stormck_last_error()), code_(code) {}
+    int code() const { return code_; }
+
+private:
+    int code_;
+};
+
+// The value VerifyChecksum returns on mismatch (pkg/errors.Errorf in the reference).
+class Error {
+public:
+    explicit Error(std::string msg) : msg_(std::move(msg)) {}
+    const std::string& message() const { return msg_; }  // Go: err.Error()
+
+private:
+    std::string msg_;
+};
+
+namespace detail {
+inline void check(int rc) {
+    if (rc != STORMCK_OK) throw DeviceError(rc);
+}
+// Go's %#v of an unsigned integer: 0x-prefixed lowercase hex without padding.
+inline std::string go_hex(uint64_t v) {
+    char buf[24];
+    std::snprintf(buf, sizeof buf, "0x%llx", static_cast<unsigned long long>(v));
+    return buf;
+}
+}  // namespace detail
+
+// Checksum computes checksum of bytes.
+inline Hash Checksum(const void* b, size_t n) {
+    uint64_t out = 0;
+    detail::check(stormck_checksum(b, n, &out));
+    return out;
+}
+inline Hash Checksum(const std::vector<uint8_t>& b) { return Checksum(b.data(), b.size()); }
+
+// BlockChecksum computes checksum of the block: all sizeof(T) bytes of the live
+// object, padding included (photon.NewFromValue(b).B in the reference).
+template <class T>
+inline Hash BlockChecksum(const T* b) {
+    static_assert(std::is_trivially_copyable_v<T>, "blocks are plain structs");
+    return Checksum(b, sizeof(T));
+}
+
+// VerifyChecksum verifies that checksum of provided data matches the expected one.
+// Returns std::nullopt (Go: nil) on match.
+inline std::optional<Error> VerifyChecksum(BlockAddress address, const void* p, size_t n, Hash expectedChecksum) {
+    const Hash checksum = Checksum(p, n);
+    if (checksum == expectedChecksum) return std::nullopt;
+    return Error("checksum mismatch for block " + std::to_string(address) + ", computed: " + detail::go_hex(checksum) +
+                 ", expected: " + detail::go_hex(expectedChecksum));
+}
+
+// Batched checksums of n host blocks at base + i*stride (length bytes each, or lens[i]).
+inline std::vector<Hash> ChecksumBatch(const void* base, size_t n, size_t stride, uint32_t length,
+                                       const uint32_t* lens = nullptr) {
+    std::vector<Hash> out(n);
+    if (n) detail::check(stormck_checksum_host(base, stride, lens, length, n, out.data()));
+    return out;
+}
+
+struct VerifyResult {
+    uint64_t first_bad;  // n when every block matches
+    uint64_t n_bad;
+};
+
+inline VerifyResult VerifyChecksumBatch(const void* base, size_t n, size_t stride, uint32_t length,
+                                        const Hash* expected, const uint32_t* lens = nullptr) {
+    VerifyResult r{n, 0};
+    if (!n) return r;
+    const int rc = stormck_verify_host(base, stride, lens, length, n, expected, &r.first_bad, &r.n_bad);
+    if (rc != STORMCK_OK && rc != STORMCK_EMISMATCH) throw DeviceError(rc);
+    return r;
+}
+
+// ---- block layouts -------------------------------------------------------------
+
+// pointer.Block (blocks/pointer/block.go:10-13); PointersPerBlock = 1200 (params.go:6),
+// 10 under the `test` tag (params_testing.go:6).
+template <size_t PointersPerBlock = 1200>
+struct PointerBlock {
+    Pointer Pointers[PointersPerBlock];
+    BlockType PointedBlockTypes[PointersPerBlock];
+};
+
+// blob.Block (blocks/blob/block.go:25-29)
+struct BlobBlock {
+    uint8_t Data[BlockSize - 8];
+    uint64_t NUsedSlots;
+};
+
+// objectlist.Block (blocks/objectlist/block.go:29-40); ChunksPerBlock = 600 / 10.
+template <size_t ChunksPerBlock = 600>
+struct ObjectListBlock {
+    uint8_t Blob[ChunksPerBlock * 32];
+    uint64_t KeyTagReminders[ChunksPerBlock];
+    ObjectID ObjectLinks[ChunksPerBlock];
+    uint16_t ChunkPointers[ChunksPerBlock];
+    uint16_t NextChunkPointers[ChunksPerBlock];
+    uint8_t ChunkPointerStates[ChunksPerBlock];
+    uint16_t NUsedChunks;
+    uint16_t FreeChunkIndex;
+};
+
+// spacelist.Space / Block (blocks/spacelist/block.go:21-36); SpacesPerBlock = 400 / 10.
+struct Space {
+    uint64_t SpaceIDTagReminder;
+    ObjectID NextObjectID;
+    Pointer KeyStorePointer;
+    Pointer ObjectStorePointer;
+    BlockType KeyStoreBlockType;
+    BlockType ObjectStoreBlockType;
+    uint8_t State;
+};
+template <size_t SpacesPerBlock = 400>
+struct SpaceListBlock {
+    Space Spaces[SpacesPerBlock];
+    uint16_t NUsedSpaces;
+};
+
+// singularity.Block (blocks/singularity/block.go:8-19)
+struct SingularityBlock {
+    Hash Checksum;
+    uint64_t StormID;
+    uint64_t Revision;
+    uint64_t NBlocks;
+    Pointer SpacePointer;
+    BlockType SpaceBlockType;
+    BlockAddress LastAllocatedBlock;
+};
+
+// Go amd64 sizes (unsafe.Sizeof) — what BlockChecksum hashes.
+static_assert(sizeof(SingularityBlock) == 72);
+static_assert(sizeof(PointerBlock<>) == 30000 && sizeof(PointerBlock<10>) == 256);
+static_assert(sizeof(BlobBlock) == 32768);
+static_assert(sizeof(ObjectListBlock<>) == 31808 && sizeof(ObjectListBlock<10>) == 536);
+static_assert(sizeof(Space) == 72);
+static_assert(sizeof(SpaceListBlock<>) == 28808 && sizeof(SpaceListBlock<10>) == 728);
+static_assert(sizeof(PointerBlock<>) <= BlockSize && sizeof(ObjectListBlock<>) <= BlockSize &&
+              sizeof(SpaceListBlock<>) <= BlockSize);  // blocks/types_test.go:18-32
+
+}  // namespace storm::blocks

@@ -1,0 +1,160 @@
+// C++ mirror of storm's blocks tests, run against libstormck on the GPU.
+// Each TEST mirrors a reference test (file:line in its comment). Relations are
+// asserted here; absolute values are printed as one JSON object for
+// tests/test_cpp_mirror.py to compare with tests/golden/layouts.json.
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "storm_blocks.hpp"
+
+using namespace storm::blocks;
+
+static int g_fail = 0;
+#define EXPECT(cond)                                                               \
+    do {                                                                           \
+        if (!(cond)) {                                                             \
+            std::fprintf(stderr, "FAIL %s:%d: %s\n", __FILE__, __LINE__, #cond);   \
+            ++g_fail;                                                              \
+        }                                                                          \
+    } while (0)
+
+static std::string hex(uint64_t v) {
+    char b[24];
+    std::snprintf(b, sizeof b, "\"0x%016llx\"", static_cast<unsigned long long>(v));
+    return b;
+}
+
+// blocks/pointer/block_test.go:11-35
+static std::string TestPointerChecksum() {
+    auto b = std::make_unique<PointerBlock<>>();
+    std::memset(b.get(), 0, sizeof(*b));
+    std::vector<Hash> seq;
+    seq.push_back(BlockChecksum(b.get()));
+    b->Pointers[0].Checksum = 2;
+    seq.push_back(BlockChecksum(b.get()));
+    b->PointedBlockTypes[0] = LeafBlockType;
+    seq.push_back(BlockChecksum(b.get()));
+    b->PointedBlockTypes[1] = LeafBlockType;
+    seq.push_back(BlockChecksum(b.get()));
+    b->Pointers[1].Address = 2;
+    seq.push_back(BlockChecksum(b.get()));
+    b->Pointers[2].Checksum = 4;
+    seq.push_back(BlockChecksum(b.get()));
+    for (size_t i = 1; i < seq.size(); ++i) EXPECT(seq[i] != seq[i - 1]);
+    std::string out = "[";
+    for (size_t i = 0; i < seq.size(); ++i) out += (i ? "," : "") + hex(seq[i]);
+    return out + "]";
+}
+
+// blocks/blob/block_test.go:13-49: four Object[item]{tag, {f1, f2}, state} in Data
+struct Item {
+    uint64_t Field1;
+    uint8_t Field2;
+};
+struct Object {
+    uint64_t ObjectIDTagReminder;
+    Item Obj;
+    uint8_t State;
+};
+static std::string TestMappingBlobToSlice() {
+    auto block = std::make_unique<BlobBlock>();
+    std::memset(block.get(), 0, sizeof(*block));
+    const Hash before = BlockChecksum(block.get());
+    Object items[4] = {{1, {2, 3}, 1}, {4, {5, 6}, 2}, {7, {8, 9}, 0}, {10, {11, 12}, 1}};
+    static_assert(sizeof(Object) == 32, "Go layout of Object[item]");
+    for (int k = 0; k < 4; ++k) {
+        Object o{};
+        std::memset(&o, 0, sizeof o);  // padding zeroed, as newBlock does (cache/cache.go:282-284)
+        o.ObjectIDTagReminder = items[k].ObjectIDTagReminder;
+        o.Obj.Field1 = items[k].Obj.Field1;
+        o.Obj.Field2 = items[k].Obj.Field2;
+        o.State = items[k].State;
+        std::memcpy(block->Data + 32 * k, &o, sizeof o);
+    }
+    const uint8_t want_rows[4][4] = {{1, 2, 3, 1}, {4, 5, 6, 2}, {7, 8, 9, 0}, {10, 11, 12, 1}};
+    for (int k = 0; k < 4; ++k)
+        for (int q = 0; q < 4; ++q) {
+            EXPECT(block->Data[32 * k + 8 * q] == want_rows[k][q]);
+            for (int z = 1; z < 8; ++z) EXPECT(block->Data[32 * k + 8 * q + z] == 0);
+        }
+    const Hash after = BlockChecksum(block.get());
+    EXPECT(after != before);
+    return hex(after);
+}
+
+// cache/cache_test.go:23-42 + persistence/store_test.go:26-48: singularity checksum
+// over the block with Checksum = 0; a corrupted checksum must fail verification.
+static std::string TestSingularity() {
+    SingularityBlock s;
+    std::memset(&s, 0, sizeof s);
+    s.StormID = 0x73746F726D;
+    s.Revision = 3;
+    s.NBlocks = 1 << 20;
+    s.SpacePointer = Pointer{0x1122334455667788ULL, 42, 2};
+    s.SpaceBlockType = LeafBlockType;
+    s.LastAllocatedBlock = 777;
+    s.Checksum = 0;
+    const Hash cs = BlockChecksum(&s);
+    s.Checksum = cs;
+    SingularityBlock copy = s;
+    copy.Checksum = 0;
+    EXPECT(!VerifyChecksum(0, &copy, sizeof copy, cs).has_value());
+    auto err = VerifyChecksum(0, &copy, sizeof copy, 0);
+    EXPECT(err.has_value());
+    if (err) EXPECT(err->message() == "checksum mismatch for block 0, computed: " + detail::go_hex(cs) + ", expected: 0x0");
+    return hex(cs);
+}
+
+// blocks.Checksum on "abc" and the empty slice (public XXH64 answers)
+static void TestKnownAnswers() {
+    EXPECT(Checksum("abc", 3) == 0x44BC2CF5AD770999ULL);
+    EXPECT(Checksum(nullptr, 0) == 0xEF46DB3751D8E999ULL);
+    auto err = VerifyChecksum(42, "abc", 3, 0);
+    EXPECT(err && err->message() == "checksum mismatch for block 42, computed: 0x44bc2cf5ad770999, expected: 0x0");
+}
+
+// batch == per-block single calls, and verify finds a corrupted block
+static void TestBatch() {
+    const size_t n = 300, stride = 32768;
+    std::vector<uint8_t> buf(n * stride);
+    uint64_t x = 0x9E3779B97F4A7C15ULL;
+    for (auto& c : buf) {
+        x ^= x << 13; x ^= x >> 7; x ^= x << 17;
+        c = static_cast<uint8_t>(x);
+    }
+    auto cs = ChecksumBatch(buf.data(), n, stride, stride);
+    for (size_t i = 0; i < n; i += 37) EXPECT(cs[i] == Checksum(buf.data() + i * stride, stride));
+    auto ok = VerifyChecksumBatch(buf.data(), n, stride, stride, cs.data());
+    EXPECT(ok.first_bad == n && ok.n_bad == 0);
+    buf[123 * stride + 7] ^= 1;
+    auto bad = VerifyChecksumBatch(buf.data(), n, stride, stride, cs.data());
+    EXPECT(bad.first_bad == 123 && bad.n_bad == 1);
+}
+
+// zero blocks of every type (prod sizes and `test`-tag sizes)
+template <class T>
+static std::string zero_cs() {
+    auto b = std::make_unique<T>();
+    std::memset(b.get(), 0, sizeof(T));
+    return hex(BlockChecksum(b.get()));
+}
+
+int main() {
+    std::string ptr = TestPointerChecksum();
+    std::string blob = TestMappingBlobToSlice();
+    std::string sing = TestSingularity();
+    TestKnownAnswers();
+    TestBatch();
+    std::printf("{\"pointer_block_test_sequence\": %s, \"blob_test_block\": %s, \"singularity\": %s, "
+                "\"zero\": {\"prod\": {\"pointer\": %s, \"objectlist\": %s, \"spacelist\": %s, \"blob\": %s, "
+                "\"singularity\": %s}, \"test\": {\"pointer\": %s, \"objectlist\": %s, \"spacelist\": %s}}, "
+                "\"failures\": %d}\n",
+                ptr.c_str(), blob.c_str(), sing.c_str(), zero_cs<PointerBlock<>>().c_str(),
+                zero_cs<ObjectListBlock<>>().c_str(), zero_cs<SpaceListBlock<>>().c_str(), zero_cs<BlobBlock>().c_str(),
+                zero_cs<SingularityBlock>().c_str(), zero_cs<PointerBlock<10>>().c_str(),
+                zero_cs<ObjectListBlock<10>>().c_str(), zero_cs<SpaceListBlock<10>>().c_str(), g_fail);
+    return g_fail ? 1 : 0;
+}

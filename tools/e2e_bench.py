@@ -1,0 +1,96 @@
+"""End-to-end host-memory checksum rate (H2D + kernel + D2H), for DESIGN.md.
+
+storm's blocks live in host memory (cache.data backed by pkg/memdev / pkg/filedev,
+/root/reference/cache/cache.go:36-40), so a drop-in call starts and ends there.
+Measures blocks.ChecksumBatch over a host buffer of synthetic 32 KiB blocks:
+  * pageable memory (library stages through pinned buffers with parallel memcpy)
+  * registered memory (stormck_host_register: DMA straight from the caller's pages)
+and, for reference, the raw pinned H2D copy rate. Results are checked bit-exact
+against the device-resident path on the same blocks.
+
+    python tools/e2e_bench.py [--gib 8] [--reps 3]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+BLOCK = 32768
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gib", type=float, default=8.0)
+    ap.add_argument("--reps", type=int, default=3)
+    a = ap.parse_args()
+    import numpy as np
+    import torch
+
+    from storm_amd import _lib, blocks, engine
+
+    dev = torch.device("cuda:0")
+    n = int(a.gib * 2**30) // BLOCK
+    d = torch.empty((n, BLOCK), dtype=torch.uint8, device=dev)
+    engine.fill_synthetic_device(d.data_ptr(), BLOCK, n, 0, 0x53544F524D)
+    ref = engine.checksum_tensor(d)
+    torch.cuda.synchronize()
+    host = np.empty((n, BLOCK), dtype=np.uint8)
+    torch.from_numpy(host).copy_(d)
+    want = ref.cpu().numpy().view(np.uint64)
+    del d
+    torch.cuda.empty_cache()
+
+    def timed(fn):
+        best = 1e9
+        for _ in range(a.reps):
+            t0 = time.perf_counter()
+            out = fn()
+            best = min(best, time.perf_counter() - t0)
+        return best, out
+
+    res = {"blocks": n, "block_bytes": BLOCK, "gib": round(n * BLOCK / 2**30, 3)}
+    blocks.ChecksumBatch(host[:64], 64, BLOCK, length=BLOCK)  # warm the context / staging
+    t, out = timed(lambda: blocks.ChecksumBatch(host, n, BLOCK, length=BLOCK))
+    assert np.array_equal(out, want), "pageable host path mismatch"
+    res["pageable_gib_s"] = round(n * BLOCK / t / 2**30, 2)
+
+    _lib.check(_lib.lib.stormck_host_register(host.ctypes.data, host.nbytes))
+    try:
+        t, out = timed(lambda: blocks.ChecksumBatch(host, n, BLOCK, length=BLOCK))
+        assert np.array_equal(out, want), "registered host path mismatch"
+        res["registered_gib_s"] = round(n * BLOCK / t / 2**30, 2)
+        # raw H2D copy of the same registered bytes, 256 MiB chunks, for reference
+        buf = torch.empty(256 << 20, dtype=torch.uint8, device=dev)
+        chunk = 256 << 20
+        flat = torch.from_numpy(host.reshape(-1))
+
+        def h2d():
+            for off in range(0, host.nbytes, chunk):
+                m = min(chunk, host.nbytes - off)
+                buf[:m].copy_(flat[off:off + m], non_blocking=True)
+            torch.cuda.synchronize()
+
+        t, _ = timed(h2d)
+        res["raw_h2d_registered_gib_s"] = round(host.nbytes / t / 2**30, 2)
+    finally:
+        _lib.check(_lib.lib.stormck_host_unregister(host.ctypes.data))
+    # single-call latency (blocks.Checksum on one buffer: H2D + launch + D2H)
+    for size in (72, BLOCK):
+        one = host[0, :size].copy()
+        blocks.Checksum(one)
+        k = 2000
+        t0 = time.perf_counter()
+        for _ in range(k):
+            blocks.Checksum(one)
+        res[f"single_call_us_{size}B"] = round((time.perf_counter() - t0) / k * 1e6, 2)
+    print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()
