@@ -43,6 +43,8 @@ def parse():
     p.add_argument("--arena", type=int, default=4 << 20, help="resident arena (blocks)")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget (rank 0, N=1)")
     p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                   help="nccl = RCCL (production); gloo only to rehearse N>1 with ranks sharing a GPU")
     return p.parse_args()
 
 
@@ -93,12 +95,16 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != a.gpus:
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    gpu = local % torch.cuda.device_count()  # == local on a node with one GPU per rank
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
-    engine.init(local)
+        if a.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
+    engine.init(gpu)
 
     n_gpu = a.blocks                      # weak scaling: fixed blocks per GPU
     n_total = n_gpu * world

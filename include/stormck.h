@@ -63,7 +63,8 @@ int stormck_abi_version(void);
 const char* stormck_last_error(void);
 /* Number of visible gfx950 devices (0 on a machine without one). */
 int stormck_device_count(int* count);
-/* Select `device` for the calling thread and create its context (lazy otherwise). */
+/* Select `device` for the calling thread and register its context. Pinned staging
+ * for the host path is allocated lazily by the first _host call on that device. */
 int stormck_init(int device);
 /* Free pinned staging / device buffers of every context. */
 void stormck_shutdown(void);

@@ -187,8 +187,8 @@ __device__ __forceinline__ uint32_t glds_rot(uint32_t b) {
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
     static_assert(N >= 0 && N < 64, "vmcnt range");
-    constexpr int imm = (N & 0xF) | ((N >> 4) << 14) | (0x7 << 4) | (0xF << 8);
 #if defined(__HIP_DEVICE_COMPILE__)
+    constexpr int imm = (N & 0xF) | ((N >> 4) << 14) | (0x7 << 4) | (0xF << 8);
     __builtin_amdgcn_s_waitcnt(imm);
 #endif
 }

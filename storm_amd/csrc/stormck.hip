@@ -365,12 +365,12 @@ int stormck_device_count(int* count) {
 int stormck_init(int device) {
     int rc = device_check();
     if (rc) return rc;
+    int count = 0;
+    HIP_TRY(hipGetDeviceCount(&count));
+    if (device < 0 || device >= count) return fail(STORMCK_EINVAL, "device index out of range");
     HIP_TRY(hipSetDevice(device));
     DeviceCtx* c = nullptr;
-    rc = get_ctx(&c);
-    if (rc) return rc;
-    std::lock_guard<std::mutex> g(c->mu);
-    return ensure_ready(c);
+    return get_ctx(&c);  // host-path staging is allocated on first host call
 }
 
 void stormck_shutdown(void) {

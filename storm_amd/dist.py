@@ -42,8 +42,15 @@ def gather_shard_roots(local_root, group=None):
     import torch.distributed as dist
 
     world = dist.get_world_size(group)
-    table = torch.empty((world, 4), dtype=local_root.dtype, device=local_root.device)
-    dist.all_gather_into_tensor(table, local_root.reshape(1, 4).contiguous(), group=group)
+    row = local_root.reshape(1, 4).contiguous()
+    if local_root.is_cuda and dist.get_backend(group) == "gloo":
+        # rehearsal on CPU collectives (e.g. several ranks sharing one GPU): gloo
+        # gathers host tensors; the production backend is nccl (RCCL over xGMI).
+        table = torch.empty((world, 4), dtype=row.dtype)
+        dist.all_gather_into_tensor(table, row.cpu(), group=group)
+        return table.to(local_root.device)
+    table = torch.empty((world, 4), dtype=row.dtype, device=row.device)
+    dist.all_gather_into_tensor(table, row, group=group)
     return table
 
 
