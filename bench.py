@@ -43,6 +43,9 @@ def parse():
     p.add_argument("--arena", type=int, default=4 << 20, help="resident arena (blocks)")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget (rank 0, N=1)")
     p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--workload", default="c3", choices=["c3", "commit"],
+                   help="c3 = BASELINE metric (default); commit = f1 level-synchronous Cache.Commit of a dirty forest")
+    p.add_argument("--commit-leaves", type=int, default=1 << 20)
     p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                    help="nccl = RCCL (production); gloo only to rehearse N>1 with ranks sharing a GPU")
     return p.parse_args()
@@ -82,8 +85,80 @@ def cpu_baseline(seconds: float):
             "all_threads": {"value": round(multi, 3), "threads": threads}}
 
 
+def cpu_commit_baseline(seconds: float):
+    """storm's serial commit loop (oracle_commit: relocation, XXH64 per block, origin
+    writes, cache/cache.go:87-137) on the host, 1 thread, over a bounded forest of the
+    same shape as the GPU run (32 KiB leaves, fan-out 1200)."""
+    import numpy as np
+    from oracle import oracle as o
+    from storm_amd import commit as sc
+
+    n = 16384  # 512 MiB of leaves
+    b0, size, last = sc.pointer_forest(n, BLOCK, FANOUT, slot=BLOCK, revision=REV)
+    arena = np.zeros(size, dtype=np.uint8)
+    arena[BLOCK:BLOCK + n * BLOCK] = o.fill_synthetic(n, BLOCK, 0)
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        b = b0.copy()
+        o.commit(arena, b, REV, last)
+        reps += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    return {"value": round(reps * n * BLOCK / el / 2**30, 3), "unit": "GiB/s", "cores": 1, "kind": "port",
+            "sample": f"commit of {n} x 32 KiB dirty leaves + {len(b0) - n} pointer blocks, {reps}x in {el:.1f} s, "
+                      f"oracle/xxh64_oracle.c oracle_commit (serial Cache.Commit loop, 1 thread)"}
+
+
+def commit_workload(a):
+    """f1: one step = commit of a dirty forest of `commit_leaves` 32 KiB leaves under
+    fan-out-1200 pointer blocks held in HBM (level-synchronous, stormck_commit_device:
+    children-first planning + relocation on the host, one fused hash+scatter launch per
+    level, metadata H2D / checksums D2H included)."""
+    import numpy as np
+    import torch
+    from storm_amd import commit as sc
+    from storm_amd import engine
+
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    n = a.commit_leaves
+    b0, size, last = sc.pointer_forest(n, BLOCK, FANOUT, slot=BLOCK, revision=REV)
+    arena = torch.zeros(size, dtype=torch.uint8, device=dev)
+    engine.fill_synthetic_device(arena.data_ptr() + BLOCK, BLOCK, n, 0, 0x53544F524D)
+    torch.cuda.synchronize()
+    # every block is new in this revision (birth = REV + 1), so commit relocates nothing
+    # and the metadata array is reusable across steps unchanged
+    for _ in range(a.warmup):
+        sc.commit_device(arena.data_ptr(), b0, REV, last)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        cs, _ = sc.commit_device(arena.data_ptr(), b0, REV, last)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    blocks_bytes = int(b0["length"].sum())
+    value = blocks_bytes * a.steps / el / 2**30
+    res = {"metric": "GiB/s level-synchronous commit (f1) of a dirty block forest", "value": round(value, 2),
+           "unit": "GiB/s", "n_gpus": 1, "steps": a.steps, "warmup": a.warmup,
+           "ms_per_step": round(el / a.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+           "vs_baseline": None, "dtype": "u64", "data": "synthetic",
+           "config": {"workload": f"f1 commit: {n} dirty 32 KiB leaves + {len(b0) - n} pointer blocks (fan-out 1200), "
+                                  "rooted at the singularity", "dirty_blocks": int(len(b0)),
+                      "hashed_bytes": blocks_bytes},
+           "roofline": {"bound": "hbm", "achieved": round(blocks_bytes / (el / a.steps) / 1e9, 1), "peak": HBM_PEAK_GBS,
+                        "unit": "GB/s", "frac": round(blocks_bytes / (el / a.steps) / 1e9 / HBM_PEAK_GBS, 4),
+                        "traffic": None, "kernel": "k_commit_level<16> (whole call, host planning included)"},
+           "root": "0x%016x" % int(cs[-1])}
+    if not a.no_cpu:
+        res["cpu_baseline"] = cpu_commit_baseline(a.cpu_seconds)
+    print(json.dumps(res), flush=True)
+
+
 def main():
     a = parse()
+    if a.workload == "commit":
+        return commit_workload(a)
     import numpy as np
     import torch
 

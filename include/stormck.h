@@ -134,6 +134,46 @@ int stormck_merkle_root_device(const uint64_t* d_leaf_cs, uint64_t n, uint64_t l
                                uint64_t workspace_bytes, stormck_pointer* d_root, uint8_t* d_root_type,
                                void* stream);
 
+/* ---- f1: level-synchronous batched commit ----------------------------------
+ * storm's Cache.Commit hashes dirty blocks children-first, one at a time
+ * (commitData / commitBlock, /root/reference/cache/cache.go:87-137) and each
+ * block's PostCommitFunc stores {Checksum, Address, BirthRevision} and its type
+ * into the parent through a BlockOrigin (/root/reference/cache/trace.go:274-320,
+ * cache/types.go BlockOrigin). Blocks at the same height are independent, so the
+ * library commits a whole dirty forest one LEVEL per launch: hash every block of
+ * the level (gather), then scatter its Pointer and type into its origin.
+ *
+ * One entry per dirty block (blockMetadata + BlockOrigin), offsets relative to the
+ * device arena (storm's cache.data): */
+#define STORMCK_NO_ORIGIN UINT64_MAX
+#define STORMCK_NO_PARENT (-1)
+typedef struct stormck_dirty_block {
+    uint64_t data_offset;    /* block bytes: d_arena + data_offset (blockMetadata.Data) */
+    uint64_t origin_pointer; /* arena offset of the blocks.Pointer the parent keeps for this block
+                              * (BlockOrigin.Pointer; 8-byte aligned), or STORMCK_NO_ORIGIN */
+    uint64_t origin_type;    /* arena offset of the parent's BlockType byte (BlockOrigin.BlockType) */
+    int64_t parent;          /* index of the dirty block that holds the origin, or STORMCK_NO_PARENT
+                              * (origin outside the batch, e.g. the singularity) */
+    uint64_t address;        /* in/out: blockMetadata.Address */
+    uint64_t birth_revision; /* in/out: blockMetadata.BirthRevision */
+    uint32_t length;         /* bytes hashed = unsafe.Sizeof(T) */
+    uint8_t type;            /* STORMCK_LEAF_BLOCK / STORMCK_POINTER_BLOCK, stored at origin_type */
+    uint8_t reserved[3];
+} stormck_dirty_block;
+
+/* Commit the dirty forest blocks[0..n) held in d_arena:
+ *  - order: children before parents (by height), index order within a height;
+ *  - relocation, in that order (cache/cache.go:114-118): if birth_revision <=
+ *    revision then address = ++*last_allocated_block, birth_revision = revision + 1;
+ *  - per block: cs = XXH64(arena + data_offset, length); if origin_pointer is set,
+ *    arena[origin_pointer] = Pointer{cs, address, birth_revision} and
+ *    arena[origin_type] = type.
+ * Writes out_checksums[i] (host) and updates blocks[i].address / birth_revision.
+ * Synchronous on `stream`. Any children-first order is a valid storm commit order
+ * (storm's own order follows Go map iteration); this one is deterministic. */
+int stormck_commit_device(void* d_arena, stormck_dirty_block* blocks, uint64_t n, uint64_t revision,
+                          uint64_t* last_allocated_block, uint64_t* out_checksums, void* stream);
+
 /* ---- synthetic data (benchmarks / tests) -----------------------------------
  * Word w of block i = splitmix64(seed ^ (((first + i) << 20) + w)), w < stride/8,
  * little-endian. stride % 16 == 0, d_dst 16-byte aligned. */

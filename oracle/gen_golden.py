@@ -218,6 +218,74 @@ def gen_layouts() -> None:
     })
 
 
+def gen_commit() -> None:
+    """f1 fixture: a storm-shaped dirty forest (leaves under fan-out-10 pointer blocks,
+    rooted at the singularity's SpacePointer) committed by an independent restatement
+    of Cache.Commit's loop (cache/cache.go:87-137, trace.go:274-320), hashed with
+    libxxhash. Iteration order (height, index), as libstormck documents."""
+    slot, fanout, revision, n_leaves = 1024, 10, 5, 137
+    rng = np.random.default_rng(2024)
+    lens = [int(x) for x in rng.choice([72, 256, 536, 728, 1000, 1024], size=n_leaves)]
+    # layout: slot 0 singularity, slots 1..n leaves, then pointer blocks level by level
+    recs = []  # dicts: off, len, type, parent, optr, otyp, addr, birth
+    for i in range(n_leaves):
+        recs.append({"off": (i + 1) * slot, "len": lens[i], "type": 2})
+    start, count = 0, n_leaves
+    while count > 1:
+        pc = (count + fanout - 1) // fanout
+        base = len(recs)
+        for j in range(pc):
+            recs.append({"off": (base + j + 1) * slot, "len": (25 * fanout + 7) & ~7, "type": 1})
+        for c in range(count):
+            p = base + c // fanout
+            recs[start + c]["parent"] = p
+            recs[start + c]["optr"] = recs[p]["off"] + 24 * (c % fanout)
+            recs[start + c]["otyp"] = recs[p]["off"] + 24 * fanout + c % fanout
+        start, count = base, pc
+    recs[start].update(parent=-1, optr=32, otyp=56)
+    existing = rng.random(len(recs)) < 0.3
+    for i, r in enumerate(recs):
+        r["addr"] = 1 + i
+        r["birth"] = revision if existing[i] else revision + 1
+    last = len(recs)
+    arena = bytearray((len(recs) + 1) * slot)
+    leaf_bytes = rng.integers(0, 256, size=n_leaves * slot, dtype=np.uint8).tobytes()
+    for i in range(n_leaves):
+        arena[(i + 1) * slot:(i + 2) * slot] = leaf_bytes[i * slot:(i + 1) * slot]
+    initial = bytes(arena)
+    # heights by walking up, order by (height, index)
+    height = [0] * len(recs)
+    for i in range(len(recs)):
+        h_, p = 0, recs[i]["parent"]
+        while p >= 0:
+            h_ += 1
+            height[p] = max(height[p], h_)
+            p = recs[p]["parent"]
+    order = sorted(range(len(recs)), key=lambda i: (height[i], i))
+    cs = [0] * len(recs)
+    for i in order:  # every child precedes its parent in this order
+        r = recs[i]
+        if r["birth"] <= revision:
+            last += 1
+            r["addr"], r["birth"] = last, revision + 1
+        cs[i] = xx(arena[r["off"]:r["off"] + r["len"]])
+        struct.pack_into("<QQQ", arena, r["optr"], cs[i], r["addr"], r["birth"])
+        arena[r["otyp"]] = r["type"]
+    # then the singularity step (cache/cache.go:71-73): Revision++, Checksum = 0, hash 72 B
+    struct.pack_into("<Q", arena, 16, revision + 1)
+    struct.pack_into("<Q", arena, 64, last)
+    struct.pack_into("<Q", arena, 0, 0)
+    sing = xx(arena[:72])
+    write("commit.json", {
+        "desc": "dirty forest committed children-first; see oracle/gen_golden.py gen_commit",
+        "slot": slot, "fanout": fanout, "revision": revision, "n_leaves": n_leaves, "leaf_lens": lens,
+        "existing": [int(x) for x in existing], "initial_arena_xxh64": h(xx(initial)),
+        "leaf_bytes_seed": 2024,
+        "checksums": [h(v) for v in cs], "addresses": [r["addr"] for r in recs],
+        "last_allocated": last, "final_arena_xxh64": h(xx(arena[72:])), "singularity_checksum": h(sing),
+    })
+
+
 def gen_big() -> None:
     """Digests (XXH64 of the little-endian checksum array) of the c2 (1M) and c3 (16M)
     synthetic 32 KiB block sets. Blocks are generated with the C oracle's generator
@@ -248,5 +316,6 @@ if __name__ == "__main__":
     gen_mixed()
     gen_layouts()
     gen_merkle()
+    gen_commit()
     if "--big" in sys.argv:
         gen_big()

@@ -55,6 +55,8 @@ def _load():
     lib.oracle_merkle_root.restype = c_size_t
     lib.oracle_merkle_root.argtypes = [c_void_p, c_size_t, c_uint64, c_uint64, c_uint64, c_uint32,
                                        POINTER(c_uint64), POINTER(c_uint8)]
+    lib.oracle_commit.restype = c_int
+    lib.oracle_commit.argtypes = [c_void_p, c_void_p, c_size_t, c_uint64, POINTER(c_uint64), c_void_p]
     return lib
 
 
@@ -188,3 +190,54 @@ def synth_leaf_checksums(n: int, seed: int = SYNTH_SEED) -> np.ndarray:
         x = (x ^ (x >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
         x = (x ^ (x >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
     return x ^ (x >> np.uint64(31))
+
+
+def commit(arena: np.ndarray, blocks: np.ndarray, revision: int, last_allocated: int):
+    """storm's serial commit loop (oracle_commit) over a host arena copy; `blocks` is a
+    storm_amd.commit.DIRTY_DTYPE array (updated in place). Returns (checksums, last)."""
+    assert blocks.dtype.itemsize == 56 and blocks.flags["C_CONTIGUOUS"]
+    assert arena.dtype == np.uint8 and arena.flags["C_CONTIGUOUS"]
+    out = np.zeros(blocks.shape[0], dtype=np.uint64)
+    la = c_uint64(last_allocated)
+    rc = lib.oracle_commit(arena.ctypes.data, blocks.ctypes.data, blocks.shape[0], revision, ctypes.byref(la),
+                           out.ctypes.data)
+    if rc != 0:
+        raise ValueError("oracle_commit: cyclic or unreachable dirty set")
+    return out, la.value
+
+
+def commit_py(arena: bytearray, blocks, revision: int, last_allocated: int):
+    """Pure-Python restatement of the same loop for small forests (cross-checks the C
+    oracle). `blocks` is a list of dicts with the stormck_dirty_block fields."""
+    n = len(blocks)
+    height = [0] * n
+    for i in range(n):  # walk each leaf-to-root chain
+        h, p = 0, blocks[i]["parent"]
+        while p >= 0:
+            h += 1
+            height[p] = max(height[p], h)
+            p = blocks[p]["parent"]
+    pending = [0] * n
+    for b in blocks:
+        if b["parent"] >= 0:
+            pending[b["parent"]] += 1
+    order = sorted(range(n), key=lambda i: (height[i], i))
+    cs = [0] * n
+    done = [False] * n
+    while not all(done):
+        for i in order:
+            b = blocks[i]
+            if done[i] or pending[i]:
+                continue
+            if b["birth_revision"] <= revision:
+                last_allocated += 1
+                b["address"], b["birth_revision"] = last_allocated, revision + 1
+            off = b["data_offset"]
+            cs[i] = xxh64_py(bytes(arena[off:off + b["length"]]))
+            if b["origin_pointer"] != M64:
+                struct.pack_into("<QQQ", arena, b["origin_pointer"], cs[i], b["address"], b["birth_revision"])
+                arena[b["origin_type"]] = b["type"]
+            if b["parent"] >= 0:
+                pending[b["parent"]] -= 1
+            done[i] = True
+    return cs, last_allocated

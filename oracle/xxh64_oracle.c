@@ -239,3 +239,82 @@ size_t oracle_merkle_root(const uint64_t* leaf_cs, size_t n, uint64_t leaf_addr_
     free(cs); free(ad); free(blk); free(revs); free(types);
     return nodes;
 }
+
+/* ---- storm commit (f1 checker) ----
+ * Serial restatement of Cache.Commit's data phase (/root/reference/cache/cache.go:87-137)
+ * with the post-commit pointer write of newPointerBlockPostCommitFunc /
+ * newLeafBlockPostCommitFunc (/root/reference/cache/trace.go:274-320):
+ *   repeat: for meta in dirty (iteration order below): if it still has uncommitted
+ *   dirty children (NReferences > 0) skip; else commitBlock: relocate if
+ *   BirthRevision <= Revision (LastAllocatedBlock++), hash the block, store
+ *   {Checksum, Address, BirthRevision} + type at its BlockOrigin, release the parent.
+ * storm iterates a Go map (unspecified order); the checker iterates by (height,
+ * index), the order libstormck documents, so addresses are comparable. Heights are
+ * computed here by fixpoint relaxation (independent of the library's walk-up). */
+typedef struct {
+    uint64_t data_offset, origin_pointer, origin_type;
+    int64_t parent;
+    uint64_t address, birth_revision;
+    uint32_t length;
+    uint8_t type, reserved[3];
+} oracle_dirty_block;
+
+static const oracle_dirty_block* g_sort_blocks;
+static const uint32_t* g_sort_height;
+static int cmp_order(const void* a, const void* b) {
+    size_t x = *(const size_t*)a, y = *(const size_t*)b;
+    if (g_sort_height[x] != g_sort_height[y]) return g_sort_height[x] < g_sort_height[y] ? -1 : 1;
+    return x < y ? -1 : (x > y);
+}
+
+int oracle_commit(uint8_t* arena, oracle_dirty_block* blocks, size_t n, uint64_t revision,
+                  uint64_t* last_allocated, uint64_t* out_cs) {
+    uint32_t* height = (uint32_t*)calloc(n ? n : 1, sizeof(uint32_t));
+    uint64_t* pending = (uint64_t*)calloc(n ? n : 1, sizeof(uint64_t));
+    uint8_t* done = (uint8_t*)calloc(n ? n : 1, 1);
+    size_t* order = (size_t*)malloc((n ? n : 1) * sizeof(size_t));
+    for (int changed = 1, rounds = 0; changed; ++rounds) {
+        if (rounds > (int)n + 1) { free(height); free(pending); free(done); free(order); return -1; }
+        changed = 0;
+        for (size_t i = 0; i < n; ++i) {
+            int64_t p = blocks[i].parent;
+            if (p >= 0 && height[p] < height[i] + 1) { height[p] = height[i] + 1; changed = 1; }
+        }
+    }
+    for (size_t i = 0; i < n; ++i) {
+        order[i] = i;
+        if (blocks[i].parent >= 0) pending[blocks[i].parent]++;
+    }
+    g_sort_blocks = blocks;
+    g_sort_height = height;
+    qsort(order, n, sizeof(size_t), cmp_order);
+    size_t remaining = n;
+    while (remaining > 0) {
+        size_t progressed = 0;
+        for (size_t k = 0; k < n; ++k) {
+            size_t i = order[k];
+            if (done[i] || pending[i] > 0) continue;
+            oracle_dirty_block* b = &blocks[i];
+            if (b->birth_revision <= revision) {          /* cache.go:114-118 */
+                *last_allocated += 1;
+                b->address = *last_allocated;
+                b->birth_revision = revision + 1;
+            }
+            uint64_t cs = oracle_xxh64(arena + b->data_offset, b->length);  /* BlockChecksum */
+            out_cs[i] = cs;
+            if (b->origin_pointer != UINT64_MAX) {       /* *origin.Pointer = ...; *origin.BlockType = ... */
+                memcpy(arena + b->origin_pointer, &cs, 8);
+                memcpy(arena + b->origin_pointer + 8, &b->address, 8);
+                memcpy(arena + b->origin_pointer + 16, &b->birth_revision, 8);
+                arena[b->origin_type] = b->type;
+            }
+            if (b->parent >= 0) pending[b->parent]--;    /* parent.NReferences -= NCommits */
+            done[i] = 1;
+            remaining--;
+            progressed++;
+        }
+        if (!progressed) { free(height); free(pending); free(done); free(order); return -1; }
+    }
+    free(height); free(pending); free(done); free(order);
+    return 0;
+}

@@ -60,11 +60,20 @@ SIGNATURES = {
     "stormck_merkle_workspace_bytes": (c_uint64, [c_uint64, c_uint32]),
     "stormck_merkle_root_device": (
         c_int, [c_void_p, c_uint64, c_uint64, c_uint64, c_uint64, c_uint32, c_void_p, c_uint64, c_void_p, c_void_p, c_void_p]),
+    "stormck_commit_device": (c_int, [c_void_p, c_void_p, c_uint64, c_uint64, POINTER(c_uint64), c_void_p, c_void_p]),
     "stormck_fill_synthetic_device": (c_int, [c_void_p, c_uint64, c_uint64, c_uint64, c_uint64, c_void_p]),
 }
 
 
 def _load() -> ctypes.CDLL:
+    # One HIP runtime per process: torch's libtorch_hip NEEDs the unversioned
+    # "libamdhip64.so", so if libstormck (NEEDED "libamdhip64.so.7") were loaded first,
+    # torch would map a second copy of the runtime and the two would contend for the
+    # device. Loading torch first lets libstormck bind to torch's runtime by soname.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     if not os.path.exists(LIB_PATH):
         raise ImportError(
             f"libstormck not built ({LIB_PATH} missing): run `python -c 'import __graft_entry__ as g; g.build()'`")

@@ -16,6 +16,7 @@
 // The per-block sizes (stride / explicit offsets) and lengths (uniform / per-block)
 // cover storm's block types: 72, 28808, 30000, 31808, 32768 bytes.
 #pragma once
+#include "../../include/stormck.h"
 #include "xxh64_dev.h"
 
 namespace stormck {
@@ -473,6 +474,49 @@ __global__ void k_set_root(const uint64_t* __restrict__ cs, uint64_t addr, uint6
         root[1] = addr;
         root[2] = rev;
         *root_type = type;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// f1: one level of a level-synchronous commit (order[0..cnt) = the caller's indices
+// of this level's blocks). Quad per dirty block: hash the
+// block's bytes (gather by data_offset, per-block length), then lane 0 performs
+// storm's PostCommitFunc (cache/trace.go:274-320): Pointer{cs, address,
+// birth_revision} into the parent's origin slot and the block type into the origin
+// type byte. Origins belong to blocks of later levels (parents), which this launch
+// never reads.
+// ---------------------------------------------------------------------------
+template <int U>
+__global__ __launch_bounds__(256) void k_commit_level(uint8_t* __restrict__ arena,
+                                                       const stormck_dirty_block* __restrict__ blocks,
+                                                       const uint32_t* __restrict__ order, uint64_t cnt,
+                                                       uint64_t* __restrict__ out_cs) {
+    const uint64_t gtid = static_cast<uint64_t>(blockIdx.x) * 256 + threadIdx.x;
+    const uint64_t k = gtid >> 2;
+    const uint32_t j = threadIdx.x & 3;
+    const bool live = k < cnt;
+    const uint64_t idx = order[live ? k : cnt - 1];  // caller's index of this level's k-th block
+    const stormck_dirty_block b = blocks[idx];
+    const uint8_t* src = arena + b.data_offset;
+    const uint32_t L = b.length;
+    const uint32_t nst = L >> 5;
+    uint64_t acc = acc_seed(j);
+    if ((reinterpret_cast<uintptr_t>(src) & 7) == 0)
+        acc = quad_stripes_aligned<U>(reinterpret_cast<const uint64_t*>(src) + j, nst, acc);
+    else
+        acc = quad_stripes_unaligned(src + 8 * j, nst, acc);
+    const uint64_t v1 = quad_bcast<0>(acc), v2 = quad_bcast<1>(acc), v3 = quad_bcast<2>(acc), v4 = quad_bcast<3>(acc);
+    if (j == 0 && live) {
+        const uint64_t h0 = (L >= 32) ? converge(v1, v2, v3, v4) : kP5;
+        const uint64_t h = finish_fast(h0, L, src + 32 * static_cast<uint64_t>(nst), L & 31);
+        out_cs[idx] = h;
+        if (b.origin_pointer != STORMCK_NO_ORIGIN) {
+            uint64_t* p = reinterpret_cast<uint64_t*>(arena + b.origin_pointer);
+            p[0] = h;
+            p[1] = b.address;
+            p[2] = b.birth_revision;
+            arena[b.origin_type] = b.type;
+        }
     }
 }
 

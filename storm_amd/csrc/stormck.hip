@@ -151,6 +151,8 @@ struct DeviceCtx {
     int device = -1;
     bool ready = false;
     Stage st[kStages];
+    void* commit_scratch = nullptr;  // f1: dirty records + checksums + commit order
+    uint64_t commit_scratch_bytes = 0;
 };
 
 std::mutex g_ctx_mu;
@@ -189,7 +191,7 @@ int ensure_ready(DeviceCtx* c) {
 }
 
 void release_ctx(DeviceCtx* c) {
-    if (!c || !c->ready) return;
+    if (!c || (!c->ready && !c->commit_scratch)) return;
     int prev = 0;
     (void)hipGetDevice(&prev);
     (void)hipSetDevice(c->device);
@@ -208,6 +210,9 @@ void release_ctx(DeviceCtx* c) {
         s = Stage();
     }
     c->ready = false;
+    if (c->commit_scratch) (void)hipFree(c->commit_scratch);
+    c->commit_scratch = nullptr;
+    c->commit_scratch_bytes = 0;
     (void)hipSetDevice(prev);
 }
 
@@ -554,6 +559,89 @@ int stormck_merkle_root_device(const uint64_t* d_leaf_cs, uint64_t n, uint64_t l
     }
     hipLaunchKernelGGL(k_set_root, dim3(1), dim3(64), 0, st, cur, addr_base, rev, type, root, d_root_type);
     HIP_TRY(hipGetLastError());
+    return STORMCK_OK;
+}
+
+int stormck_commit_device(void* d_arena, stormck_dirty_block* blocks, uint64_t n, uint64_t revision,
+                          uint64_t* last_allocated_block, uint64_t* out_checksums, void* stream) {
+    static_assert(sizeof(stormck_dirty_block) == 56, "stormck_dirty_block ABI");
+    int rc = device_check();
+    if (rc) return rc;
+    if (n == 0) return STORMCK_OK;
+    if (!d_arena || !blocks || !last_allocated_block || !out_checksums) return fail(STORMCK_EINVAL, "null argument");
+    if (n > 0xffffffffULL) return fail(STORMCK_EINVAL, "more than 2^32 dirty blocks");
+    for (uint64_t i = 0; i < n; ++i) {
+        const stormck_dirty_block& b = blocks[i];
+        if (b.parent != STORMCK_NO_PARENT && (b.parent < 0 || static_cast<uint64_t>(b.parent) >= n))
+            return fail(STORMCK_EINVAL, "parent index out of range");
+        if (b.origin_pointer != STORMCK_NO_ORIGIN && ((b.origin_pointer & 7) != 0))
+            return fail(STORMCK_EINVAL, "origin_pointer must be 8-byte aligned (Go blocks.Pointer alignment)");
+    }
+    // heights: 0 = no dirty child; walking up each chain raises ancestors to >= depth
+    std::vector<uint32_t> height(n, 0);
+    uint32_t max_h = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        uint64_t cur = i;
+        uint32_t h = 0;
+        while (blocks[cur].parent != STORMCK_NO_PARENT) {
+            const uint64_t p = static_cast<uint64_t>(blocks[cur].parent);
+            ++h;
+            if (height[p] >= h) break;  // already this high, and so are its ancestors
+            height[p] = h;
+            if (h > n) return fail(STORMCK_EINVAL, "parent links form a cycle");
+            cur = p;
+        }
+    }
+    for (uint64_t i = 0; i < n; ++i) max_h = std::max(max_h, height[i]);
+    // children-first commit order: counting sort by height (stable: index order within a level)
+    std::vector<uint64_t> level_start(static_cast<size_t>(max_h) + 2, 0);
+    for (uint64_t i = 0; i < n; ++i) level_start[height[i] + 1]++;
+    for (uint32_t l = 0; l <= max_h; ++l) level_start[l + 1] += level_start[l];
+    std::vector<uint32_t> order(n);
+    {
+        std::vector<uint64_t> pos(level_start.begin(), level_start.end() - 1);
+        for (uint64_t i = 0; i < n; ++i) order[pos[height[i]]++] = static_cast<uint32_t>(i);
+    }
+    // relocation in commit order (cache/cache.go:114-118), in place like commitBlock
+    uint64_t last = *last_allocated_block;
+    for (uint64_t k = 0; k < n; ++k) {
+        stormck_dirty_block& b = blocks[order[k]];
+        if (b.birth_revision <= revision) {
+            b.address = ++last;
+            b.birth_revision = revision + 1;
+        }
+    }
+    *last_allocated_block = last;
+
+    DeviceCtx* c = nullptr;
+    rc = get_ctx(&c);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> g(c->mu);
+    const uint64_t need = n * sizeof(stormck_dirty_block) + n * 4 + n * 8;
+    if (c->commit_scratch_bytes < need) {
+        if (c->commit_scratch) (void)hipFree(c->commit_scratch);
+        c->commit_scratch = nullptr;
+        c->commit_scratch_bytes = 0;
+        HIP_TRY(hipMalloc(&c->commit_scratch, need));
+        c->commit_scratch_bytes = need;
+    }
+    auto* d_blocks = static_cast<stormck_dirty_block*>(c->commit_scratch);
+    auto* d_cs = reinterpret_cast<uint64_t*>(d_blocks + n);
+    auto* d_order = reinterpret_cast<uint32_t*>(d_cs + n);
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    HIP_TRY(hipMemcpyAsync(d_blocks, blocks, n * sizeof(stormck_dirty_block), hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(d_order, order.data(), n * 4, hipMemcpyHostToDevice, st));
+    for (uint32_t l = 0; l <= max_h; ++l) {
+        const uint64_t lo = level_start[l], cnt = level_start[l + 1] - lo;
+        if (cnt == 0) continue;
+        dim3 grid;
+        if (!grid_for(cnt * 4, &grid)) return fail(STORMCK_EINVAL, "level too large");
+        hipLaunchKernelGGL(k_commit_level<kU>, grid, dim3(kThreads), 0, st, static_cast<uint8_t*>(d_arena), d_blocks,
+                           d_order + lo, cnt, d_cs);
+        HIP_TRY(hipGetLastError());
+    }
+    HIP_TRY(hipMemcpyAsync(out_checksums, d_cs, n * 8, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
     return STORMCK_OK;
 }
 

@@ -358,3 +358,19 @@ def test_combine_roots_device(dev):
     r = engine.as_tuple(groot)
     assert list(r[:3]) == [hx(v) for v in g["global_root"][:3]]
     assert r[3] == g["global_root"][3]
+
+
+def test_one_hip_runtime_whatever_the_import_order(dev):
+    """storm_amd imported before torch must still share torch's HIP runtime
+    (storm_amd/_lib.py loads torch first): a fresh process computes on both."""
+    import subprocess
+    import sys
+    code = ("from storm_amd import blocks\n"
+            "import torch\n"
+            "x = torch.ones(4, device='cuda:0')\n"
+            "assert blocks.Checksum(b'abc') == 0x44BC2CF5AD770999\n"
+            "assert float(x.sum()) == 4.0\n"
+            "print('ok')\n")
+    from tests.conftest import ROOT
+    r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stderr[-2000:]
