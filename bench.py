@@ -43,8 +43,9 @@ def parse():
     p.add_argument("--arena", type=int, default=4 << 20, help="resident arena (blocks)")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget (rank 0, N=1)")
     p.add_argument("--no-cpu", action="store_true")
-    p.add_argument("--workload", default="c3", choices=["c3", "commit"],
-                   help="c3 = BASELINE metric (default); commit = f1 level-synchronous Cache.Commit of a dirty forest")
+    p.add_argument("--workload", default="c3", choices=["c3", "commit", "keytags"],
+                   help="c3 = BASELINE metric (default); commit = f1 level-synchronous Cache.Commit of a dirty "
+                        "forest; keytags = f4 xxhash.Sum64 of 48-byte keys")
     p.add_argument("--commit-leaves", type=int, default=1 << 20)
     p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                    help="nccl = RCCL (production); gloo only to rehearse N>1 with ranks sharing a GPU")
@@ -155,10 +156,61 @@ def commit_workload(a):
     print(json.dumps(res), flush=True)
 
 
+def keytags_workload(a):
+    """f4: one step = xxhash.Sum64 of 64M 48-byte keys resident in HBM (the key shape of
+    keystore/benchmark_test.go:27-32), one lane per key (stormck_key_tags_device)."""
+    import numpy as np
+    import torch
+    from storm_amd import engine
+
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    n, klen = 64 << 20, 48
+    keys = torch.empty(n * klen, dtype=torch.uint8, device=dev)
+    engine.fill_synthetic_device(keys.data_ptr(), 48 * 1024, n * klen // (48 * 1024), 0, 0x53544F524D)
+    out = torch.empty(n, dtype=torch.int64, device=dev)
+    st = torch.cuda.current_stream(dev).cuda_stream
+    for _ in range(a.warmup):
+        engine.key_tags_device(keys.data_ptr(), n, out.data_ptr(), stride=klen, length=klen, stream=st)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record()
+    for _ in range(a.steps):
+        engine.key_tags_device(keys.data_ptr(), n, out.data_ptr(), stride=klen, length=klen, stream=st)
+    e1.record()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    kms = e0.elapsed_time(e1) / a.steps
+    res = {"metric": "G keys/s key-tag hashing (f4, xxhash.Sum64 of 48-byte keys)",
+           "value": round(n * a.steps / el / 1e9, 3), "unit": "Gkeys/s", "n_gpus": 1, "steps": a.steps,
+           "warmup": a.warmup, "ms_per_step": round(el / a.steps * 1e3, 3), "higher_is_better": True,
+           "scaling": "weak", "vs_baseline": None, "dtype": "u64", "data": "synthetic",
+           "config": {"workload": "f4: 64M x 48-byte keys in HBM, one tag per key", "keys": n, "key_bytes": klen},
+           "roofline": {"bound": "hbm", "achieved": round(n * (klen + 8) / (kms * 1e-3) / 1e9, 1),
+                        "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(n * (klen + 8) / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
+                        "kernel": "k_key_tags<false,false>", "avg_launch_ms": round(kms, 4)}}
+    if not a.no_cpu:
+        from oracle import oracle as o
+        m = 1 << 20
+        host = keys[:m * klen].cpu().numpy()
+        reps, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < a.cpu_seconds:
+            o.checksum_batch(host, m, klen, klen)
+            reps += 1
+        el = time.perf_counter() - t0
+        res["cpu_baseline"] = {"value": round(reps * m / el / 1e9, 4), "unit": "Gkeys/s", "cores": 1, "kind": "port",
+                               "sample": f"{m} 48-byte keys hashed {reps}x in {el:.1f} s by oracle/xxh64_oracle.c"}
+    print(json.dumps(res), flush=True)
+
+
 def main():
     a = parse()
     if a.workload == "commit":
         return commit_workload(a)
+    if a.workload == "keytags":
+        return keytags_workload(a)
     import numpy as np
     import torch
 

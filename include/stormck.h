@@ -134,6 +134,34 @@ int stormck_merkle_root_device(const uint64_t* d_leaf_cs, uint64_t n, uint64_t l
                                uint64_t workspace_bytes, stormck_pointer* d_root, uint8_t* d_root_type,
                                void* stream);
 
+/* ---- f2/f3: batched cold read + verify from a file device -------------------
+ * storm's cold fetch reads a block from its Dev and verifies it
+ * (cache.fetchBlock: Store.ReadBlock(address, Data[:Sizeof(T)]) then
+ * blocks.VerifyChecksum, /root/reference/cache/cache.go:139-167,
+ * persistence/store.go:39-51; filedev = *os.File, pkg/filedev/filedev.go). This
+ * does it for n blocks at once: block i (lens[i] bytes at file offset
+ * addresses[i] * block_size) is read with parallel pread() into
+ * dst + i*dst_stride (e.g. the cache slots), then all n are verified on the GPU
+ * against expected[i]. With STORMCK_READ_FULL_BLOCK each read covers block_size
+ * bytes (what an O_DIRECT descriptor needs; dst/dst_stride must then satisfy the
+ * descriptor's alignment) while lens[i] bytes are still what is hashed.
+ * *first_bad = first mismatching index (n if none), *n_bad = count; returns
+ * STORMCK_EMISMATCH if any block fails, STORMCK_EINVAL on a short read. */
+#define STORMCK_READ_FULL_BLOCK 1u
+int stormck_read_verify_fd(int fd, const uint64_t* addresses, const uint32_t* lens, uint64_t n, uint64_t block_size,
+                           void* dst, uint64_t dst_stride, const uint64_t* expected, uint32_t flags,
+                           uint64_t* first_bad, uint64_t* n_bad);
+
+/* ---- f4: key tags ----------------------------------------------------------
+ * xxhash.Sum64(key) for a batch of short keys (keystore.GetObjectID /
+ * EnsureObjectID hash each key to a tree tag: /root/reference/keystore/keystore.go:33,66;
+ * keys are 1..256 bytes, objectlist.MaxKeyComponentLength). Key i is at
+ * d_keys + (d_offsets ? d_offsets[i] : i*stride), (d_lens ? d_lens[i] : len) bytes;
+ * any alignment. One lane per key. Same results as stormck_checksum_device, which
+ * remains correct for keys of any length. */
+int stormck_key_tags_device(const void* d_keys, uint64_t stride, const uint64_t* d_offsets, const uint32_t* d_lens,
+                            uint32_t len, uint64_t n, uint64_t* d_out, void* stream);
+
 /* ---- f1: level-synchronous batched commit ----------------------------------
  * storm's Cache.Commit hashes dirty blocks children-first, one at a time
  * (commitData / commitBlock, /root/reference/cache/cache.go:87-137) and each

@@ -60,6 +60,9 @@ SIGNATURES = {
     "stormck_merkle_workspace_bytes": (c_uint64, [c_uint64, c_uint32]),
     "stormck_merkle_root_device": (
         c_int, [c_void_p, c_uint64, c_uint64, c_uint64, c_uint64, c_uint32, c_void_p, c_uint64, c_void_p, c_void_p, c_void_p]),
+    "stormck_read_verify_fd": (
+        c_int, [c_int, c_void_p, c_void_p, c_uint64, c_uint64, c_void_p, c_uint64, c_void_p, c_uint32, c_void_p, c_void_p]),
+    "stormck_key_tags_device": (c_int, [c_void_p, c_uint64, c_void_p, c_void_p, c_uint32, c_uint64, c_void_p, c_void_p]),
     "stormck_commit_device": (c_int, [c_void_p, c_void_p, c_uint64, c_uint64, POINTER(c_uint64), c_void_p, c_void_p]),
     "stormck_fill_synthetic_device": (c_int, [c_void_p, c_uint64, c_uint64, c_uint64, c_uint64, c_void_p]),
 }

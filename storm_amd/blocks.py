@@ -135,3 +135,34 @@ def VerifyChecksumBatch(buf, n: int, stride: int, expected: Sequence[int], lengt
     if rc != _lib.EMISMATCH:
         _lib.check(rc)
     return fb.value, nb.value
+
+
+READ_FULL_BLOCK = 1  # STORMCK_READ_FULL_BLOCK
+
+
+def ReadVerifyBatch(fd: int, addresses, lens, expected, dst, dst_stride: int, block_size: int = BLOCK_SIZE,
+                    full_block: bool = False) -> Tuple[int, int]:
+    """Batched cold read + verify (cache.fetchBlock for many blocks: Store.ReadBlock,
+    persistence/store.go:39-51, then VerifyChecksum): reads block i from file `fd` at
+    addresses[i] * block_size into dst + i*dst_stride and verifies it on the GPU.
+    Returns (first_bad, n_bad); first_bad == n when every block verifies."""
+    ad = np.ascontiguousarray(np.asarray(addresses, dtype=np.uint64))
+    la = np.ascontiguousarray(np.asarray(lens, dtype=np.uint32))
+    ex = np.ascontiguousarray(np.asarray(expected, dtype=np.uint64))
+    d = _as_u8(dst)
+    if not d.flags.writeable:
+        raise ValueError("dst must be writable (the blocks are read into it)")
+    n = ad.size
+    if la.size != n or ex.size != n:
+        raise ValueError("addresses, lens and expected need one entry per block")
+    if n and d.size < (n - 1) * dst_stride + (block_size if full_block else int(la.max())):
+        raise ValueError("dst too small")
+    if n == 0:
+        return 0, 0
+    fb, nb = ctypes.c_uint64(0), ctypes.c_uint64(0)
+    rc = _lib.lib.stormck_read_verify_fd(fd, ad.ctypes.data, la.ctypes.data, n, block_size, d.ctypes.data, dst_stride,
+                                         ex.ctypes.data, READ_FULL_BLOCK if full_block else 0, ctypes.byref(fb),
+                                         ctypes.byref(nb))
+    if rc != _lib.EMISMATCH:
+        _lib.check(rc)
+    return fb.value, nb.value

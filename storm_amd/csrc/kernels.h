@@ -521,6 +521,45 @@ __global__ __launch_bounds__(256) void k_commit_level(uint8_t* __restrict__ aren
 }
 
 // ---------------------------------------------------------------------------
+// f4: key tags — xxhash.Sum64(key) for short keys (keystore/keystore.go:33,66;
+// keys are 1..256 bytes, objectlist.MaxKeyComponentLength). One lane per key (all
+// four accumulators in the lane): for inputs of a few stripes the merge and tail
+// dominate, and a quad would leave three lanes idle through them. Key i is at
+// keys + (OFFS ? offs[i] : i*stride), LENS ? lens[i] : len bytes; 8-byte loads when
+// the key is 8-byte aligned, byte loads otherwise.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t ld64_any(const uint8_t* p, bool aligned) {
+    return aligned ? *reinterpret_cast<const uint64_t*>(p) : ld64_unaligned(p);
+}
+
+template <bool OFFS, bool LENS>
+__global__ __launch_bounds__(256) void k_key_tags(const uint8_t* __restrict__ keys, uint64_t stride,
+                                                   const uint64_t* __restrict__ offs, const uint32_t* __restrict__ lens,
+                                                   uint32_t len, uint64_t n, uint64_t* __restrict__ out) {
+    const uint64_t i = static_cast<uint64_t>(blockIdx.x) * 256 + threadIdx.x;
+    if (i >= n) return;
+    const uint8_t* p = keys + (OFFS ? offs[i] : i * stride);
+    const uint32_t L = LENS ? lens[i] : len;
+    const bool al = (reinterpret_cast<uintptr_t>(p) & 7) == 0;
+    const uint32_t nst = L >> 5;
+    uint64_t h;
+    if (L >= 32) {
+        uint64_t v1 = kV1, v2 = kV2, v3 = kV3, v4 = kV4;
+        for (uint32_t s = 0; s < nst; ++s) {
+            const uint8_t* q = p + 32 * s;
+            v1 = round(v1, ld64_any(q, al));
+            v2 = round(v2, ld64_any(q + 8, al));
+            v3 = round(v3, ld64_any(q + 16, al));
+            v4 = round(v4, ld64_any(q + 24, al));
+        }
+        h = converge(v1, v2, v3, v4);
+    } else {
+        h = kP5;
+    }
+    out[i] = finish_fast(h, L, p + 32 * nst, L & 31);
+}
+
+// ---------------------------------------------------------------------------
 // Synthetic block generator: word w of logical block (first + i)
 // = splitmix64(seed ^ ((first + i) << 20 + w)). One 16-byte store per lane,
 // grid-stride over the whole [n x stride] region (stride % 16 == 0).

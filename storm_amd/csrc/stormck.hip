@@ -4,6 +4,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <condition_variable>
 #include <cstdio>
 #include <cstring>
 #include <memory>
@@ -11,6 +12,8 @@
 #include <string>
 #include <thread>
 #include <vector>
+
+#include <unistd.h>
 
 #include "../../include/stormck.h"
 #include "kernels.h"
@@ -558,6 +561,124 @@ int stormck_merkle_root_device(const uint64_t* d_leaf_cs, uint64_t n, uint64_t l
         type = STORMCK_POINTER_BLOCK;
     }
     hipLaunchKernelGGL(k_set_root, dim3(1), dim3(64), 0, st, cur, addr_base, rev, type, root, d_root_type);
+    HIP_TRY(hipGetLastError());
+    return STORMCK_OK;
+}
+
+int stormck_read_verify_fd(int fd, const uint64_t* addresses, const uint32_t* lens, uint64_t n, uint64_t block_size,
+                           void* dst, uint64_t dst_stride, const uint64_t* expected, uint32_t flags,
+                           uint64_t* first_bad, uint64_t* n_bad) {
+    if (!first_bad || !n_bad) return fail(STORMCK_EINVAL, "null result pointer");
+    *first_bad = n;
+    *n_bad = 0;
+    if (n == 0) return STORMCK_OK;
+    int rc = device_check();
+    if (rc) return rc;
+    if (fd < 0 || !addresses || !lens || !dst || !expected) return fail(STORMCK_EINVAL, "null argument");
+    const bool full = (flags & STORMCK_READ_FULL_BLOCK) != 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        const uint64_t want = full ? block_size : lens[i];
+        if (lens[i] > block_size || want > dst_stride) return fail(STORMCK_EINVAL, "block does not fit its slot");
+    }
+    // Reads (Store.ReadBlock: Seek(address*BlockSize) + Read) run on a reader thread
+    // one super-chunk ahead of the GPU verify of the previous super-chunk.
+    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+    const unsigned nt = std::min(16u, hw);
+    const uint64_t per_super = std::max<uint64_t>(1, (1ULL << 30) / std::max<uint64_t>(dst_stride, 1));
+    const uint64_t nsuper = (n + per_super - 1) / per_super;
+    std::atomic<int> err{0};
+    std::atomic<uint64_t> bad_index{n};
+    std::atomic<uint64_t> ready{0};  // super-chunks fully read
+    std::atomic<bool> stop{false};
+    std::mutex mu;
+    std::condition_variable cv;
+    auto read_range = [&](uint64_t lo, uint64_t hi) {
+        for (uint64_t i = lo; i < hi && !err.load(std::memory_order_relaxed); ++i) {
+            uint8_t* d = static_cast<uint8_t*>(dst) + i * dst_stride;
+            const uint64_t want = full ? block_size : lens[i];
+            uint64_t got = 0;
+            while (got < want) {
+                const ssize_t r = pread(fd, d + got, want - got, static_cast<off_t>(addresses[i] * block_size + got));
+                if (r <= 0) {
+                    err.store(r < 0 ? 1 : 2);
+                    bad_index.store(i);
+                    return;
+                }
+                got += static_cast<uint64_t>(r);
+            }
+        }
+    };
+    std::thread reader([&] {
+        for (uint64_t s = 0; s < nsuper && !stop.load() && !err.load(); ++s) {
+            const uint64_t lo = s * per_super, hi = std::min(n, lo + per_super);
+            const unsigned k = static_cast<unsigned>(std::min<uint64_t>(nt, (hi - lo + 63) / 64));
+            if (k <= 1) {
+                read_range(lo, hi);
+            } else {
+                std::vector<std::thread> th;
+                for (unsigned t = 0; t < k; ++t)
+                    th.emplace_back(read_range, lo + (hi - lo) * t / k, lo + (hi - lo) * (t + 1) / k);
+                for (auto& x : th) x.join();
+            }
+            {
+                std::lock_guard<std::mutex> g(mu);
+                ready.store(s + 1);
+            }
+            cv.notify_all();
+        }
+        std::lock_guard<std::mutex> g(mu);
+        stop.store(true);
+        cv.notify_all();
+    });
+    rc = STORMCK_OK;
+    for (uint64_t s = 0; s < nsuper; ++s) {
+        {
+            std::unique_lock<std::mutex> g(mu);
+            cv.wait(g, [&] { return ready.load() > s || stop.load() || err.load(); });
+        }
+        if (err.load() || ready.load() <= s) break;
+        const uint64_t lo = s * per_super, hi = std::min(n, lo + per_super);
+        uint64_t fb = 0, nb = 0;
+        rc = host_pipeline(static_cast<uint8_t*>(dst) + lo * dst_stride, dst_stride, lens + lo, 0, hi - lo, nullptr,
+                           expected + lo, &fb, &nb);
+        if (rc) break;
+        if (nb) {
+            *n_bad += nb;
+            *first_bad = std::min<uint64_t>(*first_bad, lo + fb);
+        }
+    }
+    stop.store(true);
+    reader.join();
+    if (err.load()) {
+        return fail(STORMCK_EINVAL, std::string(err.load() == 1 ? "pread failed" : "short read (block beyond end of device)") +
+                                        " at block index " + std::to_string(bad_index.load()));
+    }
+    if (rc) return rc;
+    if (*n_bad > 0) {
+        g_last_error = "checksum mismatch";
+        return STORMCK_EMISMATCH;
+    }
+    return STORMCK_OK;
+}
+
+int stormck_key_tags_device(const void* d_keys, uint64_t stride, const uint64_t* d_offsets, const uint32_t* d_lens,
+                            uint32_t len, uint64_t n, uint64_t* d_out, void* stream) {
+    if (n == 0) return STORMCK_OK;
+    int rc = device_check();
+    if (rc) return rc;
+    if (!d_keys || !d_out) return fail(STORMCK_EINVAL, "null device pointer");
+    dim3 grid;
+    if (!grid_for(n, &grid)) return fail(STORMCK_EINVAL, "batch too large for one launch");
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    const uint8_t* k = static_cast<const uint8_t*>(d_keys);
+    if (d_offsets && d_lens)
+        hipLaunchKernelGGL((k_key_tags<true, true>), grid, dim3(kThreads), 0, st, k, stride, d_offsets, d_lens, len, n, d_out);
+    else if (d_offsets)
+        hipLaunchKernelGGL((k_key_tags<true, false>), grid, dim3(kThreads), 0, st, k, stride, d_offsets, d_lens, len, n, d_out);
+    else if (d_lens)
+        hipLaunchKernelGGL((k_key_tags<false, true>), grid, dim3(kThreads), 0, st, k, stride, d_offsets, d_lens, len, n, d_out);
+    else
+        hipLaunchKernelGGL((k_key_tags<false, false>), grid, dim3(kThreads), 0, st, k, stride, d_offsets, d_lens, len, n, d_out);
     HIP_TRY(hipGetLastError());
     return STORMCK_OK;
 }

@@ -29,6 +29,13 @@ def verify_device(d_base: int, stride: int, n: int, d_expected: int, d_result: i
     check(lib.stormck_verify_device(d_base, stride, d_lens or None, length, n, d_expected, d_result, stream or None))
 
 
+def key_tags_device(d_keys: int, n: int, d_out: int, stride: int = 0, length: int = 0, d_offsets: int = 0,
+                    d_lens: int = 0, stream: int = 0) -> None:
+    """f4: xxhash.Sum64(key) per key (keystore/keystore.go:33,66), one lane per key."""
+    check(lib.stormck_key_tags_device(d_keys, stride, d_offsets or None, d_lens or None, length, n, d_out,
+                                      stream or None))
+
+
 def fill_synthetic_device(d_dst: int, stride: int, n: int, first: int, seed: int, stream: int = 0) -> None:
     check(lib.stormck_fill_synthetic_device(d_dst, stride, n, first, seed, stream or None))
 

@@ -374,3 +374,65 @@ def test_one_hip_runtime_whatever_the_import_order(dev):
     from tests.conftest import ROOT
     r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stderr[-2000:]
+
+
+def test_key_tags_f4(dev):
+    """f4: xxhash.Sum64(key) for storm keys (keystore/keystore.go:33,66): 48-byte keys
+    as in keystore/benchmark_test.go:27-32, and packed ragged keys of 1..256 bytes
+    (objectlist.MaxKeyComponentLength) at arbitrary alignment; lane-per-key kernel ==
+    oracle == the general quad path."""
+    from oracle import oracle as o
+    from storm_amd import engine
+    rng = np.random.default_rng(48)
+    n = 30000
+    keys = rng.integers(0, 256, size=(n, 48), dtype=np.uint8)
+    d = _to_dev(keys, dev)
+    out = torch.empty(n, dtype=torch.int64, device=dev)
+    engine.key_tags_device(d.data_ptr(), n, out.data_ptr(), stride=48, length=48)
+    torch.cuda.synchronize()
+    assert np.array_equal(_u64(out), o.checksum_batch(keys, n, 48, 48))
+    lens = rng.integers(1, 257, size=n).astype(np.uint32)
+    offs = np.concatenate([[0], np.cumsum(lens[:-1])]).astype(np.uint64)
+    packed = rng.integers(0, 256, size=int(lens.sum()), dtype=np.uint8)
+    want = np.array([o.xxh64(packed[int(offs[i]):int(offs[i]) + int(lens[i])]) for i in range(n)], dtype=np.uint64)
+    dp, do, dl = _to_dev(packed, dev), _to_dev(offs.view(np.int64), dev), _to_dev(lens.view(np.int32), dev)
+    engine.key_tags_device(dp.data_ptr(), n, out.data_ptr(), d_offsets=do.data_ptr(), d_lens=dl.data_ptr())
+    quad = torch.empty(n, dtype=torch.int64, device=dev)
+    engine.checksum_gather_device(dp.data_ptr(), do.data_ptr(), n, quad.data_ptr(), 0, dl.data_ptr())
+    torch.cuda.synchronize()
+    assert np.array_equal(_u64(out), want)
+    assert np.array_equal(_u64(quad), want)
+
+
+def test_read_verify_fd_f2(dev, tmp_path):
+    """f2/f3: batched cold read + verify from a file device (cache.fetchBlock =
+    Store.ReadBlock + VerifyChecksum, cache/cache.go:139-167): data lands in the
+    slots, clean blocks verify, corrupted ones are found, short reads are errors."""
+    import os
+    from oracle import oracle as o
+    from storm_amd import _lib, blocks
+    rng = np.random.default_rng(7)
+    nblocks, bs = 2048, 32768
+    image = rng.integers(0, 256, size=(nblocks, bs), dtype=np.uint8)
+    path = tmp_path / "dev.img"
+    image.tofile(path)
+    n = 1500
+    addresses = rng.choice(nblocks, size=n, replace=False).astype(np.uint64)
+    lens = rng.choice([72, 28808, 30000, 31808, 32768, 536], size=n).astype(np.uint32)
+    expected = np.array([o.xxh64(image[a, :l]) for a, l in zip(addresses, lens)], dtype=np.uint64)
+    dst = np.zeros((n, bs), dtype=np.uint8)
+    fd = os.open(path, os.O_RDONLY)
+    try:
+        assert blocks.ReadVerifyBatch(fd, addresses, lens, expected, dst, bs) == (n, 0)
+        for i in range(0, n, 97):
+            assert np.array_equal(dst[i, :lens[i]], image[addresses[i], :lens[i]])
+        bad = expected.copy()
+        bad[[900, 12]] ^= 1
+        assert blocks.ReadVerifyBatch(fd, addresses, lens, bad, dst, bs) == (12, 2)
+        with pytest.raises(_lib.StormckError):
+            blocks.ReadVerifyBatch(fd, [nblocks + 5], [100], [0], dst, bs)
+        dst2 = np.zeros((n, bs), dtype=np.uint8)
+        assert blocks.ReadVerifyBatch(fd, addresses, lens, expected, dst2, bs, full_block=True) == (n, 0)
+        assert np.array_equal(dst2[5], image[addresses[5]])
+    finally:
+        os.close(fd)
