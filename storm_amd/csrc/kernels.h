@@ -208,18 +208,18 @@ __device__ __forceinline__ void wait_vmcnt() {
 #define STORMCK_GLDS_ISSUE(SRC, DST, T_, NK, ROW_, AUX_) do { } while (0)
 #endif
 
-template <int T, int R, int AUX, bool HASH = true, bool VERIFY = false>
-__global__ __launch_bounds__(256) void k_xxh64_glds(const uint8_t* __restrict__ base, uint64_t stride, uint32_t len,
+template <int T, int R, int AUX, bool HASH = true, bool VERIFY = false, int WAVES = 4>
+__global__ __launch_bounds__(64 * WAVES) void k_xxh64_glds(const uint8_t* __restrict__ base, uint64_t stride, uint32_t len,
                                                      uint64_t n, uint64_t* __restrict__ out,
                                                      const uint64_t* __restrict__ expected = nullptr,
                                                      unsigned long long* __restrict__ first_bad = nullptr,
                                                      unsigned long long* __restrict__ n_bad = nullptr) {
-    constexpr int BPW = 64;                 // blocks per workgroup
+    constexpr int BPW = 16 * WAVES;         // blocks per workgroup (a quad of lanes per block)
     constexpr int ROW = 32 * T;             // bytes per block per tile
     constexpr int TILE = BPW * ROW;         // bytes per tile
     constexpr int INSTR = TILE / 1024;      // glds wave-instructions per tile (whole workgroup)
-    constexpr int PER_WAVE = INSTR / 4;     // ... per wave
-    static_assert(INSTR % 4 == 0, "tile must split evenly over 4 waves");
+    constexpr int PER_WAVE = INSTR / WAVES; // ... per wave
+    static_assert(INSTR % WAVES == 0, "tile must split evenly over the waves");
     static_assert(R >= 2, "ring needs >= 2 slots");
     __shared__ __attribute__((aligned(16))) uint8_t lds[R * TILE];
 

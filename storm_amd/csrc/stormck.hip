@@ -41,12 +41,16 @@ int fail(int code, const std::string& msg) {
 // lane per pipelined group (design probe, profiles/r01_probe.txt: U=16 with plain
 // loads is the fastest quad variant; non-temporal loads cost 35%).
 constexpr int kU = 16;
-// LDS-staged fast path (profiles/r01_probe_ab.txt): tiles of 16 stripes (512 B per
-// block, 32 KiB per 64-block tile), a ring of 3 tiles (96 KiB LDS), non-temporal
-// LDS-DMA (aux = 2). All T/R variants measured within ~1.5%; this one divides
-// storm's 32 KiB blocks into whole tiles.
+// LDS-staged fast path: 8-wave (512-thread) workgroups of 128 blocks, tiles of 16
+// stripes (512 B per block, 64 KiB per tile), a ring of 2 tiles (128 KiB LDS, one
+// workgroup per CU), non-temporal LDS-DMA (aux = 2). Measured best of the swept
+// waves x tile x ring grid (profiles/r01_probe_8wave.txt: 0.886 of 8 TB/s median vs
+// 0.840 for 4 waves / 3 x 32 KiB); 16 stripes divide storm's 32 KiB blocks.
 constexpr int kTileStripes = 16;
-constexpr int kRing = 3;
+constexpr int kRing = 2;
+constexpr int kGldsWaves = 8;
+constexpr unsigned kGldsThreads = 64 * kGldsWaves;
+constexpr unsigned kGldsBlocks = 16 * kGldsWaves;
 constexpr int kAuxNT = 2;
 constexpr unsigned kThreads = 256;
 constexpr uint32_t kMaxFanout = 1u << 16;
@@ -89,14 +93,16 @@ int launch_checksum(const uint8_t* base, uint64_t stride, const uint32_t* lens, 
     // LDS tile per block -> LDS-staged kernel (global_load_lds, non-temporal).
     if (!lens && !offs && (reinterpret_cast<uintptr_t>(base) & 15) == 0 && (stride & 15) == 0 &&
         len >= 32u * kTileStripes) {
-        const uint64_t wgs = (n + 63) / 64;
+        const uint64_t wgs = (n + kGldsBlocks - 1) / kGldsBlocks;
         if (wgs > 0x7fffffffULL) return fail(STORMCK_EINVAL, "batch too large for one launch");
         if (verify)
-            hipLaunchKernelGGL((k_xxh64_glds<kTileStripes, kRing, kAuxNT, true, true>), dim3(static_cast<unsigned>(wgs)),
-                               dim3(kThreads), 0, st, base, stride, len, n, out, expected, first_bad, n_bad);
+            hipLaunchKernelGGL((k_xxh64_glds<kTileStripes, kRing, kAuxNT, true, true, kGldsWaves>),
+                               dim3(static_cast<unsigned>(wgs)), dim3(kGldsThreads), 0, st, base, stride, len, n, out,
+                               expected, first_bad, n_bad);
         else
-            hipLaunchKernelGGL((k_xxh64_glds<kTileStripes, kRing, kAuxNT, true, false>), dim3(static_cast<unsigned>(wgs)),
-                               dim3(kThreads), 0, st, base, stride, len, n, out, expected, first_bad, n_bad);
+            hipLaunchKernelGGL((k_xxh64_glds<kTileStripes, kRing, kAuxNT, true, false, kGldsWaves>),
+                               dim3(static_cast<unsigned>(wgs)), dim3(kGldsThreads), 0, st, base, stride, len, n, out,
+                               expected, first_bad, n_bad);
         HIP_TRY(hipGetLastError());
         return STORMCK_OK;
     }
