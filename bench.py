@@ -47,6 +47,8 @@ def parse():
                    help="c3 = BASELINE metric (default); commit = f1 level-synchronous Cache.Commit of a dirty "
                         "forest; keytags = f4 xxhash.Sum64 of 48-byte keys")
     p.add_argument("--commit-leaves", type=int, default=1 << 20)
+    p.add_argument("--force-dist", action="store_true",
+                   help="take the multi-rank path (process group, root all-gather, combine) even at N=1")
     p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                    help="nccl = RCCL (production); gloo only to rehearse N>1 with ranks sharing a GPU")
     return p.parse_args()
@@ -225,7 +227,8 @@ def main():
     gpu = local % torch.cuda.device_count()  # == local on a node with one GPU per rank
     torch.cuda.set_device(gpu)
     dev = torch.device("cuda", gpu)
-    if world > 1:
+    distributed = world > 1 or a.force_dist
+    if distributed:
         import torch.distributed as dist
         if a.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
@@ -260,25 +263,25 @@ def main():
                 e1.record(stream)
                 ev.append((e0, e1, cnt))
         root = engine.merkle_root_tensor(cs, lo, sdist.shard_node_addr_base(n_total, lo), REV, FANOUT, ws)
-        if world > 1:
+        if distributed:
             root, _ = sdist.global_root(root, REV, n_total, lambda t, r, ad: engine.combine_roots_tensor(t, r, ad, FANOUT))
         return root
 
     for _ in range(a.warmup):
         step(False)
     torch.cuda.synchronize()
-    if world > 1:
+    if distributed:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(a.steps):
         root = step(True)
     torch.cuda.synchronize()
-    if world > 1:
+    if distributed:
         dist.barrier()
     t1 = time.perf_counter()
     elapsed = t1 - t0
-    if world > 1:
+    if distributed:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
@@ -308,7 +311,7 @@ def main():
             "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "u64", "data": "synthetic",
             "config": {"workload": "c3: 16M x 32 KiB blocks per GPU, XXH64 seed 0 (blocks.Checksum) "
-                                   "+ shard Merkle pointer tree" + (" + RCCL all-gather of shard roots" if world > 1 else ""),
+                                   "+ shard Merkle pointer tree" + (" + RCCL all-gather of shard roots" if distributed else ""),
                        "blocks_per_gpu": n_gpu, "block_bytes": BLOCK, "arena_blocks": arena_n,
                        "passes_per_step": passes, "parallelism": f"dp{world} (contiguous block ranges)"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -320,7 +323,7 @@ def main():
         if world == 1 and not a.no_cpu:
             res["cpu_baseline"] = cpu_baseline(a.cpu_seconds)
         print(json.dumps(res), flush=True)
-    if world > 1:
+    if distributed:
         dist.destroy_process_group()
 
 
