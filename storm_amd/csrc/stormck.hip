@@ -282,6 +282,12 @@ int host_pipeline(const void* base, uint64_t stride, const uint32_t* lens, uint3
     rc = ensure_ready(c);
     if (rc) return rc;
 
+    {
+        hipPointerAttribute_t a;
+        if (hipPointerGetAttributes(&a, base) == hipSuccess && a.type == hipMemoryTypeDevice)
+            return fail(STORMCK_EINVAL, "base is device memory: use the _device entry points");
+        (void)hipGetLastError();
+    }
     const bool direct = is_pinned(base);
     const uint8_t* src = static_cast<const uint8_t*>(base);
     uint64_t fb = n, nb = 0;
