@@ -23,6 +23,7 @@ package blocks
 import "C"
 
 import (
+	"os"
 	"unsafe"
 
 	"github.com/outofforest/photon"
@@ -92,6 +93,30 @@ func VerifyChecksumBatch(data []byte, n, stride, length int, expected []Hash) (f
 	var fb, nb C.uint64_t
 	rc := C.stormck_verify_host(bytesPtr(data), C.uint64_t(stride), nil, C.uint32_t(length), C.uint64_t(n),
 		(*C.uint64_t)(unsafe.Pointer(&expected[0])), &fb, &nb)
+	if rc != C.STORMCK_OK && rc != C.STORMCK_EMISMATCH {
+		return 0, 0, stormckError(rc)
+	}
+	return int(fb), int(nb), nil
+}
+
+// ReadVerifyBatch reads len(addresses) blocks from the device file f (block i:
+// lens[i] bytes at addresses[i]*BlockSize, as persistence.Store.ReadBlock does) into
+// dst[i*dstStride:] and verifies each against expected[i] on the GPU — a batched
+// cache.fetchBlock cold read (cache/cache.go:139-167). It returns the first
+// mismatching index (len(addresses) when all verify) and the mismatch count.
+func ReadVerifyBatch(f *os.File, addresses []BlockAddress, lens []uint32, expected []Hash,
+	dst []byte, dstStride int) (firstBad, nBad int, err error) {
+	n := len(addresses)
+	if n == 0 {
+		return 0, 0, nil
+	}
+	if len(lens) != n || len(expected) != n || len(dst) < (n-1)*dstStride+int(BlockSize) {
+		return 0, 0, errors.New("ReadVerifyBatch: argument sizes")
+	}
+	var fb, nb C.uint64_t
+	rc := C.stormck_read_verify_fd(C.int(f.Fd()), (*C.uint64_t)(unsafe.Pointer(&addresses[0])),
+		(*C.uint32_t)(unsafe.Pointer(&lens[0])), C.uint64_t(n), C.uint64_t(BlockSize), bytesPtr(dst),
+		C.uint64_t(dstStride), (*C.uint64_t)(unsafe.Pointer(&expected[0])), 0, &fb, &nb)
 	if rc != C.STORMCK_OK && rc != C.STORMCK_EMISMATCH {
 		return 0, 0, stormckError(rc)
 	}
