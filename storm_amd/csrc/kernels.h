@@ -489,13 +489,16 @@ __global__ void k_set_root(const uint64_t* __restrict__ cs, uint64_t addr, uint6
 template <int U>
 __global__ __launch_bounds__(256) void k_commit_level(uint8_t* __restrict__ arena,
                                                        const stormck_dirty_block* __restrict__ blocks,
-                                                       const uint32_t* __restrict__ order, uint64_t cnt,
-                                                       uint64_t* __restrict__ out_cs) {
+                                                       const uint32_t* __restrict__ order, uint64_t lo,
+                                                       uint64_t cnt, uint64_t* __restrict__ out_cs) {
     const uint64_t gtid = static_cast<uint64_t>(blockIdx.x) * 256 + threadIdx.x;
     const uint64_t k = gtid >> 2;
     const uint32_t j = threadIdx.x & 3;
     const bool live = k < cnt;
-    const uint64_t idx = order[live ? k : cnt - 1];  // caller's index of this level's k-th block
+    const uint64_t kk = live ? k : cnt - 1;
+    // caller's index of this level's k-th block (identity when the caller's array is
+    // already children-first); checksums are written in commit order (lo + k)
+    const uint64_t idx = order ? order[kk] : lo + kk;
     const stormck_dirty_block b = blocks[idx];
     const uint8_t* src = arena + b.data_offset;
     const uint32_t L = b.length;
@@ -509,13 +512,140 @@ __global__ __launch_bounds__(256) void k_commit_level(uint8_t* __restrict__ aren
     if (j == 0 && live) {
         const uint64_t h0 = (L >= 32) ? converge(v1, v2, v3, v4) : kP5;
         const uint64_t h = finish_fast(h0, L, src + 32 * static_cast<uint64_t>(nst), L & 31);
-        out_cs[idx] = h;
+        out_cs[lo + kk] = h;
         if (b.origin_pointer != STORMCK_NO_ORIGIN) {
             uint64_t* p = reinterpret_cast<uint64_t*>(arena + b.origin_pointer);
             p[0] = h;
             p[1] = b.address;
             p[2] = b.birth_revision;
             arena[b.origin_type] = b.type;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// f1 fast path: one commit level through the LDS-DMA ring (the k_xxh64_glds scheme
+// with a ring of 2 tiles) for arenas whose block offsets are 16-byte aligned. Blocks
+// of a workgroup may differ in length: block b streams floor(nst_b / T) whole tiles,
+// the workgroup runs the longest block's tile count, and LDS-DMA lanes of blocks that
+// have run out of tiles are switched off (exec mask). With a 2-slot ring every tile
+// is waited for with vmcnt(0), so a wave that issued fewer pieces cannot mis-count.
+// Remainder stripes and the tail come from global memory; lane 0 of each quad then
+// performs the PostCommitFunc store (see k_commit_level).
+// ---------------------------------------------------------------------------
+template <int T, int AUX, int WAVES>
+__global__ __launch_bounds__(64 * WAVES) void k_commit_level_glds(uint8_t* __restrict__ arena,
+                                                                   const stormck_dirty_block* __restrict__ blocks,
+                                                                   const uint32_t* __restrict__ order, uint64_t lo,
+                                                                   uint64_t cnt, uint64_t* __restrict__ out_cs) {
+    constexpr int R = 2;
+    constexpr int BPW = 16 * WAVES;
+    constexpr int ROW = 32 * T;
+    constexpr int TILE = BPW * ROW;
+    constexpr int INSTR = TILE / 1024;
+    constexpr int PER_WAVE = INSTR / WAVES;
+    static_assert(INSTR % WAVES == 0, "tile must split evenly over the waves");
+    __shared__ __attribute__((aligned(16))) uint8_t lds[R * TILE];
+
+    const uint32_t tid = threadIdx.x;
+    const uint32_t wave = tid >> 6, lane = tid & 63;
+    const uint64_t k0 = static_cast<uint64_t>(blockIdx.x) * BPW;  // first level-local block of this workgroup
+
+    // per-lane LDS-DMA sources: block of each of this wave's PER_WAVE pieces. Loads are
+    // batched (all indices, then all record fields) and branch-free so they overlap.
+    const uint8_t* src[PER_WAVE];
+    uint32_t ntl[PER_WAVE];
+    uint64_t ridx[PER_WAVE];
+    uint32_t piece[PER_WAVE];
+    bool plive[PER_WAVE];
+#pragma unroll
+    for (int k = 0; k < PER_WAVE; ++k) {
+        const uint32_t ii = wave * PER_WAVE + k;
+        const uint32_t off = ii * 1024 + lane * 16;
+        const uint32_t bb = off / ROW, q = (off % ROW) / 16;
+        piece[k] = (q + glds_rot<T>(bb)) % (2 * T);
+        const uint64_t kk = k0 + bb;
+        plive[k] = kk < cnt;
+        ridx[k] = plive[k] ? kk : cnt - 1;
+    }
+    if (order) {
+#pragma unroll
+        for (int k = 0; k < PER_WAVE; ++k) ridx[k] = order[ridx[k]];
+    } else {
+#pragma unroll
+        for (int k = 0; k < PER_WAVE; ++k) ridx[k] += lo;
+    }
+    uint64_t doff[PER_WAVE];
+    uint32_t dlen[PER_WAVE];
+#pragma unroll
+    for (int k = 0; k < PER_WAVE; ++k) {
+        doff[k] = blocks[ridx[k]].data_offset;
+        dlen[k] = blocks[ridx[k]].length;
+    }
+#pragma unroll
+    for (int k = 0; k < PER_WAVE; ++k) {
+        src[k] = arena + doff[k] + piece[k] * 16;
+        ntl[k] = plive[k] ? (dlen[k] >> 5) / T : 0;
+    }
+    // this lane's hash block (quad) and the workgroup's tile count
+    const uint32_t b = tid >> 2, j = tid & 3;
+    const uint64_t kb = k0 + b;
+    const bool live = kb < cnt;
+    const uint64_t idx = order ? order[live ? kb : cnt - 1] : lo + (live ? kb : cnt - 1);
+    const stormck_dirty_block rec = blocks[idx];
+    const uint32_t L = rec.length, nst = L >> 5;
+    const uint32_t my_tiles = live ? nst / T : 0;
+    uint32_t wg_tiles = my_tiles;
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) wg_tiles = max(wg_tiles, static_cast<uint32_t>(__shfl_xor(static_cast<int>(wg_tiles), m)));
+    uint32_t* red = reinterpret_cast<uint32_t*>(lds);
+    if (lane == 0) red[wave] = wg_tiles;
+    __syncthreads();
+    wg_tiles = 0;
+    for (int w = 0; w < WAVES; ++w) wg_tiles = max(wg_tiles, red[w]);
+    __syncthreads();  // the reduction slots are reused by the ring
+
+    const uint32_t rot = glds_rot<T>(b);
+    uint64_t acc = acc_seed(j);
+#if defined(__HIP_DEVICE_COMPILE__)
+#define STORMCK_GLDS_ISSUE_MASKED(T_, SLOT)                                                              \
+    do {                                                                                              \
+        uint8_t* dst_ = lds + (SLOT) * TILE + wave * PER_WAVE * 1024;                                \
+        _Pragma("unroll") for (int k_ = 0; k_ < PER_WAVE; ++k_) if ((T_) < ntl[k_])                   \
+            __builtin_amdgcn_global_load_lds(src[k_] + static_cast<uint64_t>(T_) * ROW, dst_ + k_ * 1024, \
+                                             16, 0, AUX);                                             \
+    } while (0)
+#else
+#define STORMCK_GLDS_ISSUE_MASKED(T_, SLOT) do { } while (0)
+#endif
+    if (wg_tiles > 0) STORMCK_GLDS_ISSUE_MASKED(0u, 0);
+    for (uint32_t t = 0; t < wg_tiles; ++t) {
+        wait_vmcnt<0>();
+        __builtin_amdgcn_s_barrier();
+        if (t + 1 < wg_tiles) STORMCK_GLDS_ISSUE_MASKED(t + 1, (t + 1) & 1);
+        if (t < my_tiles) {
+            const uint8_t* row = lds + (t & 1) * TILE + b * ROW + (j & 1) * 8;
+#pragma unroll
+            for (int s = 0; s < T; ++s) {
+                const uint32_t q = (2 * s + (j >> 1) + 2 * T - rot) % (2 * T);
+                acc = round(acc, *reinterpret_cast<const uint64_t*>(row + q * 16));
+            }
+        }
+    }
+#undef STORMCK_GLDS_ISSUE_MASKED
+    const uint8_t* bsrc = arena + rec.data_offset;
+    for (uint32_t s = my_tiles * T; s < nst; ++s) acc = round(acc, reinterpret_cast<const uint64_t*>(bsrc)[4 * s + j]);
+    const uint64_t v1 = quad_bcast<0>(acc), v2 = quad_bcast<1>(acc), v3 = quad_bcast<2>(acc), v4 = quad_bcast<3>(acc);
+    if (j == 0 && live) {
+        const uint64_t h0 = (L >= 32) ? converge(v1, v2, v3, v4) : kP5;
+        const uint64_t h = finish_fast(h0, L, bsrc + 32 * static_cast<uint64_t>(nst), L & 31);
+        out_cs[lo + kb] = h;
+        if (rec.origin_pointer != STORMCK_NO_ORIGIN) {
+            uint64_t* p = reinterpret_cast<uint64_t*>(arena + rec.origin_pointer);
+            p[0] = h;
+            p[1] = rec.address;
+            p[2] = rec.birth_revision;
+            arena[rec.origin_type] = rec.type;
         }
     }
 }

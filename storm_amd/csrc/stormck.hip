@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
+#include <cstdlib>
 #include <atomic>
 #include <condition_variable>
 #include <cstdio>
@@ -127,6 +129,31 @@ int launch_checksum(const uint8_t* base, uint64_t stride, const uint32_t* lens, 
     HIP_TRY(hipGetLastError());
     return STORMCK_OK;
 }
+
+// Optional phase timing of host-orchestrated calls (STORMCK_TRACE=1 -> stderr).
+struct PhaseTimer {
+    bool on;
+    const char* what;
+    std::chrono::steady_clock::time_point t0, last;
+    std::string log;
+    explicit PhaseTimer(const char* w) : on(std::getenv("STORMCK_TRACE") != nullptr), what(w) {
+        t0 = last = std::chrono::steady_clock::now();
+    }
+    void mark(const char* phase) {
+        if (!on) return;
+        const auto now = std::chrono::steady_clock::now();
+        char buf[96];
+        std::snprintf(buf, sizeof buf, " %s=%.3fms", phase, std::chrono::duration<double, std::milli>(now - last).count());
+        log += buf;
+        last = now;
+    }
+    ~PhaseTimer() {
+        if (!on) return;
+        const auto now = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "[stormck] %s total=%.3fms%s\n", what,
+                     std::chrono::duration<double, std::milli>(now - t0).count(), log.c_str());
+    }
+};
 
 __global__ void k_init_result(uint64_t* r, uint64_t n) {
     if (threadIdx.x == 0) {
@@ -703,21 +730,26 @@ int stormck_commit_device(void* d_arena, stormck_dirty_block* blocks, uint64_t n
     if (n == 0) return STORMCK_OK;
     if (!d_arena || !blocks || !last_allocated_block || !out_checksums) return fail(STORMCK_EINVAL, "null argument");
     if (n > 0xffffffffULL) return fail(STORMCK_EINVAL, "more than 2^32 dirty blocks");
+    PhaseTimer pt("commit");
+    // One pass: validate, and raise every ancestor's height to >= its depth below it
+    // (a walk stops at the first ancestor that is already high enough, so each edge is
+    // walked O(1) times amortised for storm-shaped forests).
+    std::vector<uint32_t> height(n, 0);
+    uint64_t relocating = 0;
+    bool aligned16 = (reinterpret_cast<uintptr_t>(d_arena) & 15) == 0;
     for (uint64_t i = 0; i < n; ++i) {
         const stormck_dirty_block& b = blocks[i];
+        aligned16 &= (b.data_offset & 15) == 0;
         if (b.parent != STORMCK_NO_PARENT && (b.parent < 0 || static_cast<uint64_t>(b.parent) >= n))
             return fail(STORMCK_EINVAL, "parent index out of range");
         if (b.origin_pointer != STORMCK_NO_ORIGIN && ((b.origin_pointer & 7) != 0))
             return fail(STORMCK_EINVAL, "origin_pointer must be 8-byte aligned (Go blocks.Pointer alignment)");
-    }
-    // heights: 0 = no dirty child; walking up each chain raises ancestors to >= depth
-    std::vector<uint32_t> height(n, 0);
-    uint32_t max_h = 0;
-    for (uint64_t i = 0; i < n; ++i) {
+        relocating += b.birth_revision <= revision;
         uint64_t cur = i;
-        uint32_t h = 0;
+        uint32_t h = height[i];
         while (blocks[cur].parent != STORMCK_NO_PARENT) {
             const uint64_t p = static_cast<uint64_t>(blocks[cur].parent);
+            if (p >= n) return fail(STORMCK_EINVAL, "parent index out of range");
             ++h;
             if (height[p] >= h) break;  // already this high, and so are its ancestors
             height[p] = h;
@@ -725,32 +757,44 @@ int stormck_commit_device(void* d_arena, stormck_dirty_block* blocks, uint64_t n
             cur = p;
         }
     }
-    for (uint64_t i = 0; i < n; ++i) max_h = std::max(max_h, height[i]);
-    // children-first commit order: counting sort by height (stable: index order within a level)
+    pt.mark("heights");
+    // children-first commit order: counting sort by height (stable: index order within a
+    // level); skipped when the caller's array is already in that order
+    uint32_t max_h = 0;
+    bool sorted = true;
+    for (uint64_t i = 0; i < n; ++i) {
+        max_h = std::max(max_h, height[i]);
+        if (i && height[i] < height[i - 1]) sorted = false;
+    }
     std::vector<uint64_t> level_start(static_cast<size_t>(max_h) + 2, 0);
     for (uint64_t i = 0; i < n; ++i) level_start[height[i] + 1]++;
     for (uint32_t l = 0; l <= max_h; ++l) level_start[l + 1] += level_start[l];
-    std::vector<uint32_t> order(n);
-    {
+    std::vector<uint32_t> order;
+    if (!sorted) {
+        order.resize(n);
         std::vector<uint64_t> pos(level_start.begin(), level_start.end() - 1);
         for (uint64_t i = 0; i < n; ++i) order[pos[height[i]]++] = static_cast<uint32_t>(i);
     }
+    pt.mark("order");
     // relocation in commit order (cache/cache.go:114-118), in place like commitBlock
     uint64_t last = *last_allocated_block;
-    for (uint64_t k = 0; k < n; ++k) {
-        stormck_dirty_block& b = blocks[order[k]];
-        if (b.birth_revision <= revision) {
-            b.address = ++last;
-            b.birth_revision = revision + 1;
+    if (relocating) {
+        for (uint64_t k = 0; k < n; ++k) {
+            stormck_dirty_block& b = blocks[sorted ? k : order[k]];
+            if (b.birth_revision <= revision) {
+                b.address = ++last;
+                b.birth_revision = revision + 1;
+            }
         }
     }
     *last_allocated_block = last;
+    pt.mark("relocate");
 
     DeviceCtx* c = nullptr;
     rc = get_ctx(&c);
     if (rc) return rc;
     std::lock_guard<std::mutex> g(c->mu);
-    const uint64_t need = n * sizeof(stormck_dirty_block) + n * 4 + n * 8;
+    const uint64_t need = n * sizeof(stormck_dirty_block) + n * 8 + (sorted ? 0 : n * 4);
     if (c->commit_scratch_bytes < need) {
         if (c->commit_scratch) (void)hipFree(c->commit_scratch);
         c->commit_scratch = nullptr;
@@ -760,21 +804,39 @@ int stormck_commit_device(void* d_arena, stormck_dirty_block* blocks, uint64_t n
     }
     auto* d_blocks = static_cast<stormck_dirty_block*>(c->commit_scratch);
     auto* d_cs = reinterpret_cast<uint64_t*>(d_blocks + n);
-    auto* d_order = reinterpret_cast<uint32_t*>(d_cs + n);
+    auto* d_order = sorted ? nullptr : reinterpret_cast<uint32_t*>(d_cs + n);
     hipStream_t st = static_cast<hipStream_t>(stream);
     HIP_TRY(hipMemcpyAsync(d_blocks, blocks, n * sizeof(stormck_dirty_block), hipMemcpyHostToDevice, st));
-    HIP_TRY(hipMemcpyAsync(d_order, order.data(), n * 4, hipMemcpyHostToDevice, st));
+    if (!sorted) HIP_TRY(hipMemcpyAsync(d_order, order.data(), n * 4, hipMemcpyHostToDevice, st));
+    pt.mark("upload_issue");
     for (uint32_t l = 0; l <= max_h; ++l) {
         const uint64_t lo = level_start[l], cnt = level_start[l + 1] - lo;
         if (cnt == 0) continue;
-        dim3 grid;
-        if (!grid_for(cnt * 4, &grid)) return fail(STORMCK_EINVAL, "level too large");
-        hipLaunchKernelGGL(k_commit_level<kU>, grid, dim3(kThreads), 0, st, static_cast<uint8_t*>(d_arena), d_blocks,
-                           d_order + lo, cnt, d_cs);
+        const uint32_t* lvl_order = sorted ? nullptr : d_order + lo;
+        if (aligned16) {
+            // LDS-DMA ring, 8 waves x 128 blocks per workgroup (as the uniform fast path)
+            const uint64_t wgs = (cnt + kGldsBlocks - 1) / kGldsBlocks;
+            if (wgs > 0x7fffffffULL) return fail(STORMCK_EINVAL, "level too large");
+            hipLaunchKernelGGL((k_commit_level_glds<kTileStripes, kAuxNT, kGldsWaves>), dim3(static_cast<unsigned>(wgs)),
+                               dim3(kGldsThreads), 0, st, static_cast<uint8_t*>(d_arena), d_blocks, lvl_order, lo, cnt,
+                               d_cs);
+        } else {
+            dim3 grid;
+            if (!grid_for(cnt * 4, &grid)) return fail(STORMCK_EINVAL, "level too large");
+            hipLaunchKernelGGL(k_commit_level<kU>, grid, dim3(kThreads), 0, st, static_cast<uint8_t*>(d_arena), d_blocks,
+                               lvl_order, lo, cnt, d_cs);
+        }
         HIP_TRY(hipGetLastError());
     }
     HIP_TRY(hipMemcpyAsync(out_checksums, d_cs, n * 8, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
+    pt.mark("device");
+    if (!sorted) {
+        // d_cs is in commit order; put it back in the caller's order
+        std::vector<uint64_t> tmp(out_checksums, out_checksums + n);
+        for (uint64_t k = 0; k < n; ++k) out_checksums[order[k]] = tmp[k];
+        pt.mark("unpermute");
+    }
     return STORMCK_OK;
 }
 

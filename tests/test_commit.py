@@ -94,10 +94,12 @@ def test_device_commit_matches_fixture(dev):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("n,fanout,slot", [(1, 10, 1024), (10, 10, 1024), (11, 10, 1024), (999, 10, 1024),
-                                            (5000, 1200, 32768), (1201, 1200, 32768)])
+                                            (5000, 1200, 32768), (1201, 1200, 32768),
+                                            # 8- but not 16-byte aligned slots: register-quad commit kernel
+                                            (999, 10, 1032), (3000, 1200, 32776)])
 def test_device_commit_random_forests(dev, n, fanout, slot):
     rng = np.random.default_rng(n * 7 + fanout)
-    choices = [72, 256, 536, 728, 1000, slot] if slot == 1024 else [72, 28808, 30000, 31808, 32768, 4097]
+    choices = [72, 256, 536, 728, 1000, 1024] if slot < 2048 else [72, 28808, 30000, 31808, 32768, 4097]
     lens = rng.choice(choices, size=n)
     b, size, last = sc.pointer_forest(n, lens, fanout, slot=slot, revision=9, first_address=100)
     b["birth_revision"][rng.random(len(b)) < 0.4] = 3

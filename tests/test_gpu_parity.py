@@ -436,3 +436,40 @@ def test_read_verify_fd_f2(dev, tmp_path):
         assert np.array_equal(dst2[5], image[addresses[5]])
     finally:
         os.close(fd)
+
+
+def test_quad_paths_verify_and_gather_variants(dev):
+    """Register-quad kernel in every shape: verify with per-block lengths (LENS+VERIFY),
+    gather with offsets and a uniform length (OFFS only), verify through offsets is
+    covered by the commit tests; host verify with per-block lengths."""
+    from oracle import oracle as o
+    from storm_amd import blocks, engine
+    rng = np.random.default_rng(99)
+    n, stride = 4000, 2048
+    host = rng.integers(0, 256, size=(n, stride), dtype=np.uint8)
+    lens = rng.integers(0, stride + 1, size=n).astype(np.uint32)
+    want = o.checksum_batch(host, n, stride, lens=lens)
+    d = _to_dev(host, dev)
+    d_lens = _to_dev(lens.view(np.int32), dev)
+    exp = torch.from_numpy(want.view(np.int64).copy()).to(dev)
+    res = torch.zeros(2, dtype=torch.int64, device=dev)
+    engine.verify_device(d.data_ptr(), stride, n, exp.data_ptr(), res.data_ptr(), 0, d_lens.data_ptr())
+    torch.cuda.synchronize()
+    assert _u64(res).tolist() == [n, 0]
+    exp[3999] ^= 1
+    exp[1234] ^= 1
+    engine.verify_device(d.data_ptr(), stride, n, exp.data_ptr(), res.data_ptr(), 0, d_lens.data_ptr())
+    torch.cuda.synchronize()
+    assert _u64(res).tolist() == [1234, 2]
+    # gather: reversed order, uniform length
+    offs = (np.arange(n, dtype=np.uint64)[::-1] * stride).copy()
+    d_offs = _to_dev(offs.view(np.int64), dev)
+    out = torch.empty(n, dtype=torch.int64, device=dev)
+    engine.checksum_gather_device(d.data_ptr(), d_offs.data_ptr(), n, out.data_ptr(), 777)
+    torch.cuda.synchronize()
+    assert np.array_equal(_u64(out), o.checksum_batch(host, n, stride, 777)[::-1])
+    # host verify with per-block lengths
+    bad = want.copy()
+    bad[77] ^= 1
+    assert blocks.VerifyChecksumBatch(host, n, stride, want, lens=lens) == (n, 0)
+    assert blocks.VerifyChecksumBatch(host, n, stride, bad, lens=lens) == (77, 1)
