@@ -192,7 +192,7 @@ def keytags_workload(a):
            "roofline": {"bound": "hbm", "achieved": round(n * (klen + 8) / (kms * 1e-3) / 1e9, 1),
                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(n * (klen + 8) / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
-                        "kernel": "k_key_tags<false,false>", "avg_launch_ms": round(kms, 4)}}
+                        "kernel": "k_key_tags_lds<nt> (per-wave LDS-DMA double buffer)", "avg_launch_ms": round(kms, 4)}}
     if not a.no_cpu:
         from oracle import oracle as o
         m = 1 << 20

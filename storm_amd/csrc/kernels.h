@@ -689,6 +689,66 @@ __global__ __launch_bounds__(256) void k_key_tags(const uint8_t* __restrict__ ke
     out[i] = finish_fast(h, L, p + 32 * nst, L & 31);
 }
 
+// f4 fast path for fixed-stride keys (stride % 16 == 0, stride <= 256, 16-byte aligned
+// base): each wave owns runs of 64 consecutive keys = one contiguous 64*stride-byte
+// region, streamed HBM -> LDS by LDS-DMA (stride/16 wave-instructions, fully
+// coalesced) into a per-wave double buffer; the next batch is in flight while the
+// lanes hash the current one from LDS (lane l: its key at l*stride). Only whole
+// batches of 64 keys; the caller hashes the remainder with k_key_tags. Waits are per
+// wave (vmcnt + the wave's own LDS), so no workgroup barrier is needed.
+template <int AUX>
+__global__ __launch_bounds__(256) void k_key_tags_lds(const uint8_t* __restrict__ keys, uint32_t stride, uint32_t len,
+                                                       uint64_t batches, uint32_t per_wave,
+                                                       uint64_t* __restrict__ out) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t dyn_lds[];
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint32_t region = 64 * stride;       // bytes per batch
+    [[maybe_unused]] const uint32_t pieces = region / 1024;  // LDS-DMA wave-instructions per batch
+    uint8_t* buf = dyn_lds + wave * 2 * region;
+    const uint64_t wid = static_cast<uint64_t>(blockIdx.x) * 4 + wave;
+    const uint64_t b0 = wid * per_wave;
+    if (b0 >= batches) return;
+    const uint64_t b1 = (b0 + per_wave < batches) ? b0 + per_wave : batches;
+    const uint32_t nst = len >> 5, rem = len & 31;
+#if defined(__HIP_DEVICE_COMPILE__)
+#define STORMCK_KEYS_ISSUE(B, SLOT)                                                                      \
+    do {                                                                                               \
+        const uint8_t* s_ = keys + (B) * region + lane * 16;                                           \
+        uint8_t* d_ = buf + (SLOT) * region;                                                           \
+        for (uint32_t p_ = 0; p_ < pieces; ++p_)                                                       \
+            __builtin_amdgcn_global_load_lds(s_ + p_ * 1024, d_ + p_ * 1024, 16, 0, AUX);              \
+    } while (0)
+#else
+#define STORMCK_KEYS_ISSUE(B, SLOT) do { } while (0)
+#endif
+    STORMCK_KEYS_ISSUE(b0, 0u);
+    for (uint64_t b = b0; b < b1; ++b) {
+        const uint32_t slot = static_cast<uint32_t>(b - b0) & 1;
+        wait_vmcnt<0>();  // batch b landed (this wave's own pieces)
+        if (b + 1 < b1) STORMCK_KEYS_ISSUE(b + 1, slot ^ 1u);
+        const uint8_t* k = buf + slot * region + lane * stride;
+        uint64_t h;
+        if (len >= 32) {
+            uint64_t v1 = kV1, v2 = kV2, v3 = kV3, v4 = kV4;
+            for (uint32_t s = 0; s < nst; ++s) {
+                const u64x2 x = *reinterpret_cast<const u64x2*>(k + 32 * s);
+                const u64x2 y = *reinterpret_cast<const u64x2*>(k + 32 * s + 16);
+                v1 = round(v1, x.x);
+                v2 = round(v2, x.y);
+                v3 = round(v3, y.x);
+                v4 = round(v4, y.y);
+            }
+            h = converge(v1, v2, v3, v4);
+        } else {
+            h = kP5;
+        }
+        out[b * 64 + lane] = finish_fast(h, len, k + 32 * nst, rem);
+        // the slot is refilled two batches later, after this wave's reads retired
+        // (the compiler waits lgkmcnt before the hash consumes them)
+    }
+#undef STORMCK_KEYS_ISSUE
+}
+
 // ---------------------------------------------------------------------------
 // Synthetic block generator: word w of logical block (first + i)
 // = splitmix64(seed ^ ((first + i) << 20 + w)). One 16-byte store per lane,

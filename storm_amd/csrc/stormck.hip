@@ -710,6 +710,25 @@ int stormck_key_tags_device(const void* d_keys, uint64_t stride, const uint64_t*
     if (!grid_for(n, &grid)) return fail(STORMCK_EINVAL, "batch too large for one launch");
     hipStream_t st = static_cast<hipStream_t>(stream);
     const uint8_t* k = static_cast<const uint8_t*>(d_keys);
+    if (!d_offsets && !d_lens && stride >= 16 && stride <= 256 && (stride & 15) == 0 && len <= stride &&
+        (reinterpret_cast<uintptr_t>(k) & 15) == 0 && n >= 64) {
+        // whole batches of 64 keys through the per-wave LDS-DMA double buffer
+        const uint64_t batches = n / 64;
+        constexpr uint32_t kPerWave = 8;
+        const uint64_t waves = (batches + kPerWave - 1) / kPerWave;
+        const uint64_t wgs = (waves + 3) / 4;
+        if (wgs > 0x7fffffffULL) return fail(STORMCK_EINVAL, "batch too large for one launch");
+        const size_t lds_bytes = 4 * 2 * 64 * static_cast<size_t>(stride);
+        hipLaunchKernelGGL(k_key_tags_lds<kAuxNT>, dim3(static_cast<unsigned>(wgs)), dim3(kThreads), lds_bytes, st, k,
+                           static_cast<uint32_t>(stride), len, batches, kPerWave, d_out);
+        HIP_TRY(hipGetLastError());
+        const uint64_t done = batches * 64;
+        if (done == n) return STORMCK_OK;
+        k += done * stride;
+        d_out += done;
+        n -= done;
+        if (!grid_for(n, &grid)) return fail(STORMCK_EINVAL, "batch too large for one launch");
+    }
     if (d_offsets && d_lens)
         hipLaunchKernelGGL((k_key_tags<true, true>), grid, dim3(kThreads), 0, st, k, stride, d_offsets, d_lens, len, n, d_out);
     else if (d_offsets)

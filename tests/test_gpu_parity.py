@@ -402,6 +402,15 @@ def test_key_tags_f4(dev):
     torch.cuda.synchronize()
     assert np.array_equal(_u64(out), want)
     assert np.array_equal(_u64(quad), want)
+    # fixed strides through the LDS-DMA batch path (+ the lane-kernel remainder):
+    # stride 48/64/256, key lengths below the stride, n not a multiple of 64
+    for stride, klen, m in ((48, 48, 64 * 100 + 17), (64, 40, 64 * 9), (256, 256, 64 * 3 + 63), (16, 5, 1000)):
+        k2 = rng.integers(0, 256, size=(m, stride), dtype=np.uint8)
+        d2 = _to_dev(k2, dev)
+        o2 = torch.empty(m, dtype=torch.int64, device=dev)
+        engine.key_tags_device(d2.data_ptr(), m, o2.data_ptr(), stride=stride, length=klen)
+        torch.cuda.synchronize()
+        assert np.array_equal(_u64(o2), o.checksum_batch(k2, m, stride, klen)), (stride, klen, m)
 
 
 def test_read_verify_fd_f2(dev, tmp_path):
