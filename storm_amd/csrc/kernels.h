@@ -7,12 +7,14 @@
 // Why not "one wavefront per block": XXH64 carries four serial accumulator
 // recurrences over a block's stripes (acc = rotl(acc + w*P2, 31) * P1 per 8-byte word),
 // and the recurrence is not associative, so at most FOUR lanes can work on one block.
-// Mappings implemented here:
-//   * quad  : 4 lanes per block (lane j owns accumulator j and loads word j of each
-//             32-byte stripe), 16 blocks per wave64; the 4 accumulators meet through
-//             DPP quad permutes for the merge; lane 0 of the quad does tail+avalanche.
-//   * lane  : 1 lane per block (all four accumulators in one lane), 64 blocks per wave,
-//             dwordx4 loads of whole stripes.
+// Mapping: a quad of lanes per block (lane j owns accumulator j and reads word j of
+// each 32-byte stripe), 16 blocks per wave64; the 4 accumulators meet through DPP quad
+// permutes for the merge; lane 0 of the quad does tail + avalanche. Kernels:
+//   * k_xxh64_glds   : uniform-length batches, stripes staged HBM -> LDS by LDS-DMA
+//   * k_xxh64_quad   : any shape (per-block lengths, offsets, alignment), register loads
+//   * k_commit_level*: f1 commit levels; k_pointer_level / _node: Merkle nodes
+//   * k_key_tags*    : f4, one lane per short key
+// (A lane-per-block mapping was measured and rejected: tools/probe.hip)
 // The per-block sizes (stride / explicit offsets) and lengths (uniform / per-block)
 // cover storm's block types: 72, 28808, 30000, 31808, 32768 bytes.
 #pragma once
@@ -290,9 +292,6 @@ __global__ __launch_bounds__(64 * WAVES) void k_xxh64_glds(const uint8_t* __rest
     }
 }
 
-// ---------------------------------------------------------------------------
-// Lane kernel: 1 lane per block, uniform length, 16-byte aligned blocks
-// (base % 16 == 0, stride % 16 == 0). U stripes (2U dwordx4) per pipelined group.
 // ---------------------------------------------------------------------------
 template <int U, bool NT = false>
 __global__ __launch_bounds__(256) void k_xxh64_lane(const uint8_t* __restrict__ base, uint64_t stride,

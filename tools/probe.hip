@@ -20,6 +20,14 @@
 
 using namespace stormck;
 
+// Rejected alternative kept for the design comparison: one lane per
+// block, all four accumulators in the lane, dwordx4 loads of whole stripes.
+namespace stormck {
+// ---------------------------------------------------------------------------
+// Lane kernel: 1 lane per block, uniform length, 16-byte aligned blocks
+// (base % 16 == 0, stride % 16 == 0). U stripes (2U dwordx4) per pipelined group.
+}  // namespace stormck
+
 // ---- host XXH64 (probe self-check only) ----
 static inline uint64_t hrotl(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
 static inline uint64_t hround(uint64_t a, uint64_t w) { a += w * kP2; a = hrotl(a, 31); return a * kP1; }
