@@ -14,7 +14,8 @@
 //   * k_xxh64_quad   : any shape (per-block lengths, offsets, alignment), register loads
 //   * k_commit_level*: f1 commit levels; k_pointer_level / _node: Merkle nodes
 //   * k_key_tags*    : f4, one lane per short key
-// (A lane-per-block mapping was measured and rejected: tools/probe.hip)
+// (A lane-per-block mapping was measured and rejected: 0.59-0.66 of HBM peak,
+// profiles/r01_probe*.txt)
 // The per-block sizes (stride / explicit offsets) and lengths (uniform / per-block)
 // cover storm's block types: 72, 28808, 30000, 31808, 32768 bytes.
 #pragma once
