@@ -433,10 +433,10 @@ void stormck_shutdown(void) {
 int stormck_checksum_device(const void* d_base, uint64_t stride, const uint32_t* d_lens, uint32_t len, uint64_t n,
                             uint64_t* d_out, void* stream) {
     if (n == 0) return STORMCK_OK;
-    int rc = device_check();
-    if (rc) return rc;
     if (!d_base || !d_out) return fail(STORMCK_EINVAL, "null device pointer");
     if (!d_lens && n > 1 && stride < len) return fail(STORMCK_EINVAL, "stride smaller than len (blocks overlap)");
+    int rc = device_check();
+    if (rc) return rc;
     return launch_checksum(static_cast<const uint8_t*>(d_base), stride, d_lens, len, nullptr, n, d_out, nullptr,
                            nullptr, nullptr, static_cast<hipStream_t>(stream));
 }
@@ -444,25 +444,25 @@ int stormck_checksum_device(const void* d_base, uint64_t stride, const uint32_t*
 int stormck_checksum_gather_device(const void* d_base, const uint64_t* d_offsets, const uint32_t* d_lens,
                                    uint32_t len, uint64_t n, uint64_t* d_out, void* stream) {
     if (n == 0) return STORMCK_OK;
+    if (!d_base || !d_offsets || !d_out) return fail(STORMCK_EINVAL, "null device pointer");
     int rc = device_check();
     if (rc) return rc;
-    if (!d_base || !d_offsets || !d_out) return fail(STORMCK_EINVAL, "null device pointer");
     return launch_checksum(static_cast<const uint8_t*>(d_base), 0, d_lens, len, d_offsets, n, d_out, nullptr,
                            nullptr, nullptr, static_cast<hipStream_t>(stream));
 }
 
 int stormck_verify_device(const void* d_base, uint64_t stride, const uint32_t* d_lens, uint32_t len, uint64_t n,
                           const uint64_t* d_expected, uint64_t* d_result, void* stream) {
+    if (!d_result) return fail(STORMCK_EINVAL, "d_result is null");
+    if (n > 0 && (!d_base || !d_expected)) return fail(STORMCK_EINVAL, "null device pointer");
+    if (!d_lens && n > 1 && stride < len) return fail(STORMCK_EINVAL, "stride smaller than len (blocks overlap)");
     int rc = device_check();
     if (rc) return rc;
-    if (!d_result) return fail(STORMCK_EINVAL, "d_result is null");
     hipStream_t st = static_cast<hipStream_t>(stream);
     // d_result = {n, 0}: "no mismatch" until a block lowers it.
     hipLaunchKernelGGL(k_init_result, dim3(1), dim3(64), 0, st, d_result, n);
     HIP_TRY(hipGetLastError());
     if (n == 0) return STORMCK_OK;
-    if (!d_base || !d_expected) return fail(STORMCK_EINVAL, "null device pointer");
-    if (!d_lens && n > 1 && stride < len) return fail(STORMCK_EINVAL, "stride smaller than len (blocks overlap)");
     return launch_checksum(static_cast<const uint8_t*>(d_base), stride, d_lens, len, nullptr, n, nullptr, d_expected,
                            reinterpret_cast<unsigned long long*>(d_result),
                            reinterpret_cast<unsigned long long*>(d_result + 1), st);
@@ -495,9 +495,9 @@ int stormck_checksum(const void* p, uint64_t n_bytes, uint64_t* out) {
 }
 
 int stormck_host_register(void* p, uint64_t bytes) {
+    if (!p || bytes == 0) return fail(STORMCK_EINVAL, "empty range");
     int rc = device_check();
     if (rc) return rc;
-    if (!p || bytes == 0) return fail(STORMCK_EINVAL, "empty range");
     HIP_TRY(hipHostRegister(p, bytes, hipHostRegisterDefault));
     return STORMCK_OK;
 }
@@ -512,10 +512,10 @@ int stormck_host_unregister(void* p) {
 int stormck_pointer_level_device(const uint64_t* d_child_cs, uint64_t m, uint64_t child_addr_base, uint64_t rev,
                                  uint8_t child_type, uint32_t fanout, uint64_t* d_parent_cs, void* stream) {
     if (m == 0) return STORMCK_OK;
-    int rc = device_check();
-    if (rc) return rc;
     if (!d_child_cs || !d_parent_cs) return fail(STORMCK_EINVAL, "null device pointer");
     if (fanout == 0 || fanout > kMaxFanout) return fail(STORMCK_EINVAL, "fanout out of range");
+    int rc = device_check();
+    if (rc) return rc;
     const uint64_t pm = (m + fanout - 1) / fanout;
     dim3 grid;
     if (!grid_for(pm * 4, &grid)) return fail(STORMCK_EINVAL, "level too large");
@@ -527,10 +527,10 @@ int stormck_pointer_level_device(const uint64_t* d_child_cs, uint64_t m, uint64_
 
 int stormck_pointer_node_device(const stormck_pointer* d_entries, const uint8_t* d_types, uint32_t count,
                                 uint32_t fanout, uint64_t* d_out_cs, void* stream) {
-    int rc = device_check();
-    if (rc) return rc;
     if (!d_out_cs || (count > 0 && (!d_entries || !d_types))) return fail(STORMCK_EINVAL, "null device pointer");
     if (fanout == 0 || fanout > kMaxFanout || count > fanout) return fail(STORMCK_EINVAL, "count/fanout out of range");
+    int rc = device_check();
+    if (rc) return rc;
     static_assert(sizeof(stormck_pointer) == 24, "Pointer is 24 bytes");
     hipLaunchKernelGGL(k_pointer_node, dim3(1), dim3(64), 0, static_cast<hipStream_t>(stream),
                        reinterpret_cast<const uint64_t*>(d_entries), d_types, count, fanout, d_out_cs);
@@ -542,12 +542,12 @@ int stormck_pack_pointer_blocks_device(const uint64_t* d_child_cs, uint64_t m, u
                                        uint8_t child_type, uint32_t fanout, void* d_blocks, uint64_t dst_stride,
                                        void* stream) {
     if (m == 0) return STORMCK_OK;
-    int rc = device_check();
-    if (rc) return rc;
     if (!d_child_cs || !d_blocks) return fail(STORMCK_EINVAL, "null device pointer");
     if (fanout == 0 || fanout > kMaxFanout) return fail(STORMCK_EINVAL, "fanout out of range");
     if (dst_stride < pointer_block_size(fanout) || (dst_stride & 7) || (reinterpret_cast<uintptr_t>(d_blocks) & 7))
         return fail(STORMCK_EINVAL, "dst_stride/d_blocks must be 8-byte aligned and hold a pointer block");
+    int rc = device_check();
+    if (rc) return rc;
     hipLaunchKernelGGL(k_pack_pointer_blocks, dim3(2048), dim3(kThreads), 0, static_cast<hipStream_t>(stream),
                        d_child_cs, m, child_addr_base, rev, child_type, fanout, static_cast<uint8_t*>(d_blocks),
                        dst_stride);
@@ -569,10 +569,13 @@ int stormck_merkle_root_device(const uint64_t* d_leaf_cs, uint64_t n, uint64_t l
                                uint64_t node_addr_base, uint64_t rev, uint32_t fanout, void* d_workspace,
                                uint64_t workspace_bytes, stormck_pointer* d_root, uint8_t* d_root_type,
                                void* stream) {
-    int rc = device_check();
-    if (rc) return rc;
     if (!d_root || !d_root_type) return fail(STORMCK_EINVAL, "null root pointer");
     if (fanout < 2 || fanout > kMaxFanout) return fail(STORMCK_EINVAL, "fanout out of range");
+    if (n > 0 && !d_leaf_cs) return fail(STORMCK_EINVAL, "d_leaf_cs is null");
+    if (n > 0 && (workspace_bytes < stormck_merkle_workspace_bytes(n, fanout) || (n > 1 && !d_workspace)))
+        return fail(STORMCK_EINVAL, "workspace too small (stormck_merkle_workspace_bytes)");
+    int rc = device_check();
+    if (rc) return rc;
     hipStream_t st = static_cast<hipStream_t>(stream);
     uint64_t* root = reinterpret_cast<uint64_t*>(d_root);
     if (n == 0) {
@@ -581,9 +584,6 @@ int stormck_merkle_root_device(const uint64_t* d_leaf_cs, uint64_t n, uint64_t l
         HIP_TRY(hipGetLastError());
         return STORMCK_OK;
     }
-    if (!d_leaf_cs) return fail(STORMCK_EINVAL, "d_leaf_cs is null");
-    if (workspace_bytes < stormck_merkle_workspace_bytes(n, fanout) || (n > 1 && !d_workspace))
-        return fail(STORMCK_EINVAL, "workspace too small (stormck_merkle_workspace_bytes)");
     const uint64_t* cur = d_leaf_cs;
     uint64_t m = n, addr_base = leaf_addr_base, next_addr = node_addr_base;
     uint8_t type = STORMCK_LEAF_BLOCK;
@@ -611,14 +611,14 @@ int stormck_read_verify_fd(int fd, const uint64_t* addresses, const uint32_t* le
     *first_bad = n;
     *n_bad = 0;
     if (n == 0) return STORMCK_OK;
-    int rc = device_check();
-    if (rc) return rc;
     if (fd < 0 || !addresses || !lens || !dst || !expected) return fail(STORMCK_EINVAL, "null argument");
     const bool full = (flags & STORMCK_READ_FULL_BLOCK) != 0;
     for (uint64_t i = 0; i < n; ++i) {
         const uint64_t want = full ? block_size : lens[i];
         if (lens[i] > block_size || want > dst_stride) return fail(STORMCK_EINVAL, "block does not fit its slot");
     }
+    int rc = device_check();
+    if (rc) return rc;
     // Reads (Store.ReadBlock: Seek(address*BlockSize) + Read) run on a reader thread
     // one super-chunk ahead of the GPU verify of the previous super-chunk.
     const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
@@ -703,9 +703,9 @@ int stormck_read_verify_fd(int fd, const uint64_t* addresses, const uint32_t* le
 int stormck_key_tags_device(const void* d_keys, uint64_t stride, const uint64_t* d_offsets, const uint32_t* d_lens,
                             uint32_t len, uint64_t n, uint64_t* d_out, void* stream) {
     if (n == 0) return STORMCK_OK;
+    if (!d_keys || !d_out) return fail(STORMCK_EINVAL, "null device pointer");
     int rc = device_check();
     if (rc) return rc;
-    if (!d_keys || !d_out) return fail(STORMCK_EINVAL, "null device pointer");
     dim3 grid;
     if (!grid_for(n, &grid)) return fail(STORMCK_EINVAL, "batch too large for one launch");
     hipStream_t st = static_cast<hipStream_t>(stream);
@@ -744,8 +744,6 @@ int stormck_key_tags_device(const void* d_keys, uint64_t stride, const uint64_t*
 int stormck_commit_device(void* d_arena, stormck_dirty_block* blocks, uint64_t n, uint64_t revision,
                           uint64_t* last_allocated_block, uint64_t* out_checksums, void* stream) {
     static_assert(sizeof(stormck_dirty_block) == 56, "stormck_dirty_block ABI");
-    int rc = device_check();
-    if (rc) return rc;
     if (n == 0) return STORMCK_OK;
     if (!d_arena || !blocks || !last_allocated_block || !out_checksums) return fail(STORMCK_EINVAL, "null argument");
     if (n > 0xffffffffULL) return fail(STORMCK_EINVAL, "more than 2^32 dirty blocks");
@@ -795,6 +793,8 @@ int stormck_commit_device(void* d_arena, stormck_dirty_block* blocks, uint64_t n
         for (uint64_t i = 0; i < n; ++i) order[pos[height[i]]++] = static_cast<uint32_t>(i);
     }
     pt.mark("order");
+    int rc = device_check();
+    if (rc) return rc;
     // relocation in commit order (cache/cache.go:114-118), in place like commitBlock
     uint64_t last = *last_allocated_block;
     if (relocating) {
@@ -862,10 +862,10 @@ int stormck_commit_device(void* d_arena, stormck_dirty_block* blocks, uint64_t n
 int stormck_fill_synthetic_device(void* d_dst, uint64_t stride, uint64_t n, uint64_t first, uint64_t seed,
                                   void* stream) {
     if (n == 0) return STORMCK_OK;
-    int rc = device_check();
-    if (rc) return rc;
     if (!d_dst || (stride & 15) || stride == 0 || (reinterpret_cast<uintptr_t>(d_dst) & 15))
         return fail(STORMCK_EINVAL, "fill_synthetic needs a 16-byte aligned destination and stride");
+    int rc = device_check();
+    if (rc) return rc;
     hipLaunchKernelGGL(k_fill_synthetic, dim3(8192), dim3(kThreads), 0, static_cast<hipStream_t>(stream),
                        static_cast<uint8_t*>(d_dst), stride, n, first, seed);
     HIP_TRY(hipGetLastError());

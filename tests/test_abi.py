@@ -72,3 +72,52 @@ def test_no_device_fails_loudly():
     with pytest.raises(_lib.NoDeviceError):
         engine.checksum_device(1 << 20, 32, 1, 1 << 21, 32)
     assert "no HIP device" in _lib.last_error() or "gfx950" in _lib.last_error()
+
+
+def test_argument_errors_precede_the_device_check():
+    """Bad arguments are rejected with STORMCK_EINVAL (and a message) before any device
+    work, so these run identically with or without a GPU."""
+    import numpy as np
+    from storm_amd import _lib, commit as sc
+    L = _lib.lib
+    out = ctypes.c_uint64()
+    cases = [
+        ("null out", lambda: L.stormck_checksum(b"abc", 3, None)),
+        ("overlap", lambda: L.stormck_checksum_device(1 << 20, 16, None, 32, 2, 1 << 21, None)),
+        ("null base", lambda: L.stormck_checksum_device(None, 32, None, 32, 2, 1 << 21, None)),
+        ("gather null", lambda: L.stormck_checksum_gather_device(1 << 20, None, None, 32, 2, 1 << 21, None)),
+        ("verify null result", lambda: L.stormck_verify_device(1 << 20, 32, None, 32, 2, 1 << 21, None, None)),
+        ("fanout 0", lambda: L.stormck_pointer_level_device(1 << 20, 5, 0, 1, 2, 0, 1 << 21, None)),
+        ("node count > fanout", lambda: L.stormck_pointer_node_device(1 << 20, 1 << 21, 11, 10, 1 << 22, None)),
+        ("pack stride", lambda: L.stormck_pack_pointer_blocks_device(1 << 20, 5, 0, 1, 2, 10, 1 << 21, 200, None)),
+        ("workspace", lambda: L.stormck_merkle_root_device(1 << 20, 5000, 0, 5000, 1, 10, 1 << 21, 8,
+                                                           1 << 22, (1 << 22) + 24, None)),
+        ("fill stride", lambda: L.stormck_fill_synthetic_device(1 << 20, 24, 4, 0, 1, None)),
+        ("register empty", lambda: L.stormck_host_register(None, 0)),
+        ("key tags null", lambda: L.stormck_key_tags_device(None, 48, None, None, 48, 10, 1 << 20, None)),
+        ("host null base", lambda: L.stormck_checksum_host(None, 32, None, 32, 4, ctypes.addressof(out))),
+        ("read-verify slot", lambda: L.stormck_read_verify_fd(0, (ctypes.c_uint64 * 1)(0), (ctypes.c_uint32 * 1)(100),
+                                                              1, 32768, (ctypes.c_uint8 * 64)(), 64,
+                                                              (ctypes.c_uint64 * 1)(0), 1, ctypes.byref(out),
+                                                              ctypes.byref(out))),
+    ]
+    for name, fn in cases:
+        assert fn() == _lib.EINVAL, name
+        assert _lib.last_error(), name
+    # f1 planning errors: parent out of range, misaligned origin, cycles
+    b, size, last = sc.pointer_forest(25, 100, 10, slot=1024, revision=1)
+    la = ctypes.c_uint64(last)
+    cs = np.zeros(len(b), dtype=np.uint64)
+
+    def commit(bb):
+        return L.stormck_commit_device(1 << 20, bb.ctypes.data, len(bb), 1, ctypes.byref(la), cs.ctypes.data, None)
+    bad = b.copy()
+    bad["parent"][3] = 10 ** 6
+    assert commit(bad) == _lib.EINVAL and "parent" in _lib.last_error()
+    bad = b.copy()
+    bad["origin_pointer"][3] += 4
+    assert commit(bad) == _lib.EINVAL and "aligned" in _lib.last_error()
+    bad = b.copy()
+    bad["parent"][28] = 0  # root -> leaf 0 -> ... -> root
+    assert commit(bad) == _lib.EINVAL and "cycle" in _lib.last_error()
+    assert (b["address"] == np.arange(1, len(b) + 1)).all()  # rejected calls left the records untouched

@@ -482,3 +482,35 @@ def test_quad_paths_verify_and_gather_variants(dev):
     bad[77] ^= 1
     assert blocks.VerifyChecksumBatch(host, n, stride, want, lens=lens) == (n, 0)
     assert blocks.VerifyChecksumBatch(host, n, stride, bad, lens=lens) == (77, 1)
+
+
+def test_device_entry_points_are_graph_capturable(dev):
+    """The device entry points allocate and synchronise nothing, so a batch checksum
+    + Merkle root can be captured into a HIP graph once and replayed on new data
+    (launch-bound small batches: one graph launch instead of several kernels)."""
+    from oracle import oracle as o
+    from storm_amd import engine
+    n, stride = 2048, 32768
+    buf = torch.empty((n, stride), dtype=torch.uint8, device=dev)
+    out = torch.empty(n, dtype=torch.int64, device=dev)
+    ws = torch.empty(engine.merkle_workspace_bytes(n, 1200) // 8 + 1, dtype=torch.int64, device=dev)
+    engine.fill_synthetic_device(buf.data_ptr(), stride, n, 0, 1)
+    s = torch.cuda.Stream(dev)
+    s.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(s):  # warm-up outside capture
+        engine.checksum_tensor(buf, out=out)
+        engine.merkle_root_tensor(out, 0, n, 1, 1200, ws)
+    torch.cuda.current_stream(dev).wait_stream(s)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        engine.checksum_tensor(buf, out=out)
+        root = engine.merkle_root_tensor(out, 0, n, 1, 1200, ws)
+    for seed in (7, 8):
+        engine.fill_synthetic_device(buf.data_ptr(), stride, n, 0, seed)
+        torch.cuda.synchronize()
+        g.replay()
+        torch.cuda.synchronize()
+        want = o.checksum_batch(buf.cpu().numpy(), n, stride, stride)
+        assert np.array_equal(_u64(out), want)
+        assert engine.as_tuple(root) == o.merkle_root(want, 0, n, 1, 1200)
