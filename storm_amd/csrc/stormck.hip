@@ -748,49 +748,90 @@ int stormck_commit_device(void* d_arena, stormck_dirty_block* blocks, uint64_t n
     if (!d_arena || !blocks || !last_allocated_block || !out_checksums) return fail(STORMCK_EINVAL, "null argument");
     if (n > 0xffffffffULL) return fail(STORMCK_EINVAL, "more than 2^32 dirty blocks");
     PhaseTimer pt("commit");
-    // One pass: validate, and raise every ancestor's height to >= its depth below it
-    // (a walk stops at the first ancestor that is already high enough, so each edge is
-    // walked O(1) times amortised for storm-shaped forests).
-    std::vector<uint32_t> height(n, 0);
-    uint64_t relocating = 0;
-    bool aligned16 = (reinterpret_cast<uintptr_t>(d_arena) & 15) == 0;
-    for (uint64_t i = 0; i < n; ++i) {
-        const stormck_dirty_block& b = blocks[i];
-        aligned16 &= (b.data_offset & 15) == 0;
-        if (b.parent != STORMCK_NO_PARENT && (b.parent < 0 || static_cast<uint64_t>(b.parent) >= n))
-            return fail(STORMCK_EINVAL, "parent index out of range");
-        if (b.origin_pointer != STORMCK_NO_ORIGIN && ((b.origin_pointer & 7) != 0))
-            return fail(STORMCK_EINVAL, "origin_pointer must be 8-byte aligned (Go blocks.Pointer alignment)");
-        relocating += b.birth_revision <= revision;
-        uint64_t cur = i;
-        uint32_t h = height[i];
-        while (blocks[cur].parent != STORMCK_NO_PARENT) {
-            const uint64_t p = static_cast<uint64_t>(blocks[cur].parent);
-            if (p >= n) return fail(STORMCK_EINVAL, "parent index out of range");
-            ++h;
-            if (height[p] >= h) break;  // already this high, and so are its ancestors
-            height[p] = h;
-            if (h > n) return fail(STORMCK_EINVAL, "parent links form a cycle");
-            cur = p;
+    // One parallel pass: validate, and raise every ancestor's height to >= its distance
+    // above each block (atomic max; a walk stops at the first ancestor some walk has
+    // already raised high enough, which then carries the raise further up).
+    std::unique_ptr<std::atomic<uint32_t>[]> height(new std::atomic<uint32_t>[n]);
+    for (uint64_t i = 0; i < n; ++i) height[i].store(0, std::memory_order_relaxed);
+    std::atomic<int> bad{0};  // 1 parent range, 2 origin alignment, 3 cycle
+    std::atomic<uint64_t> relocating_n{0};
+    std::atomic<bool> misaligned{(reinterpret_cast<uintptr_t>(d_arena) & 15) != 0};
+    auto walk = [&](uint64_t lo, uint64_t hi) {
+        uint64_t reloc = 0;
+        bool mis = false;
+        for (uint64_t i = lo; i < hi && !bad.load(std::memory_order_relaxed); ++i) {
+            const stormck_dirty_block& b = blocks[i];
+            mis |= (b.data_offset & 15) != 0;
+            if (b.parent != STORMCK_NO_PARENT && (b.parent < 0 || static_cast<uint64_t>(b.parent) >= n)) {
+                bad.store(1);
+                return;
+            }
+            if (b.origin_pointer != STORMCK_NO_ORIGIN && ((b.origin_pointer & 7) != 0)) {
+                bad.store(2);
+                return;
+            }
+            reloc += b.birth_revision <= revision;
+            uint64_t cur = i;
+            uint32_t hh = 0;
+            while (blocks[cur].parent != STORMCK_NO_PARENT) {
+                const uint64_t p = static_cast<uint64_t>(blocks[cur].parent);
+                if (p >= n) {
+                    bad.store(1);
+                    return;
+                }
+                ++hh;
+                if (hh > n) {
+                    bad.store(3);
+                    return;
+                }
+                uint32_t old = height[p].load(std::memory_order_relaxed);
+                while (old < hh && !height[p].compare_exchange_weak(old, hh, std::memory_order_relaxed)) {
+                }
+                if (old >= hh) break;  // another walk holds p at >= hh and carries it upward
+                cur = p;
+            }
+        }
+        relocating_n.fetch_add(reloc, std::memory_order_relaxed);
+        if (mis) misaligned.store(true, std::memory_order_relaxed);
+    };
+    {
+        const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+        const unsigned nt = static_cast<unsigned>(std::min<uint64_t>({16u, hw, n / 65536 + 1}));
+        if (nt <= 1) {
+            walk(0, n);
+        } else {
+            std::vector<std::thread> th;
+            for (unsigned t = 0; t < nt; ++t) th.emplace_back(walk, n * t / nt, n * (t + 1) / nt);
+            for (auto& x : th) x.join();
         }
     }
+    if (bad.load() == 1) return fail(STORMCK_EINVAL, "parent index out of range");
+    if (bad.load() == 2) return fail(STORMCK_EINVAL, "origin_pointer must be 8-byte aligned (Go blocks.Pointer alignment)");
+    if (bad.load() == 3) return fail(STORMCK_EINVAL, "parent links form a cycle");
+    const uint64_t relocating = relocating_n.load();
+    const bool aligned16 = !misaligned.load();
     pt.mark("heights");
     // children-first commit order: counting sort by height (stable: index order within a
     // level); skipped when the caller's array is already in that order
     uint32_t max_h = 0;
     bool sorted = true;
-    for (uint64_t i = 0; i < n; ++i) {
-        max_h = std::max(max_h, height[i]);
-        if (i && height[i] < height[i - 1]) sorted = false;
+    {
+        uint32_t prev = 0;
+        for (uint64_t i = 0; i < n; ++i) {
+            const uint32_t hi = height[i].load(std::memory_order_relaxed);
+            max_h = std::max(max_h, hi);
+            if (hi < prev) sorted = false;
+            prev = hi;
+        }
     }
     std::vector<uint64_t> level_start(static_cast<size_t>(max_h) + 2, 0);
-    for (uint64_t i = 0; i < n; ++i) level_start[height[i] + 1]++;
+    for (uint64_t i = 0; i < n; ++i) level_start[height[i].load(std::memory_order_relaxed) + 1]++;
     for (uint32_t l = 0; l <= max_h; ++l) level_start[l + 1] += level_start[l];
     std::vector<uint32_t> order;
     if (!sorted) {
         order.resize(n);
         std::vector<uint64_t> pos(level_start.begin(), level_start.end() - 1);
-        for (uint64_t i = 0; i < n; ++i) order[pos[height[i]]++] = static_cast<uint32_t>(i);
+        for (uint64_t i = 0; i < n; ++i) order[pos[height[i].load(std::memory_order_relaxed)]++] = static_cast<uint32_t>(i);
     }
     pt.mark("order");
     int rc = device_check();
@@ -825,12 +866,7 @@ int stormck_commit_device(void* d_arena, stormck_dirty_block* blocks, uint64_t n
     auto* d_cs = reinterpret_cast<uint64_t*>(d_blocks + n);
     auto* d_order = sorted ? nullptr : reinterpret_cast<uint32_t*>(d_cs + n);
     hipStream_t st = static_cast<hipStream_t>(stream);
-    HIP_TRY(hipMemcpyAsync(d_blocks, blocks, n * sizeof(stormck_dirty_block), hipMemcpyHostToDevice, st));
-    if (!sorted) HIP_TRY(hipMemcpyAsync(d_order, order.data(), n * 4, hipMemcpyHostToDevice, st));
-    pt.mark("upload_issue");
-    for (uint32_t l = 0; l <= max_h; ++l) {
-        const uint64_t lo = level_start[l], cnt = level_start[l + 1] - lo;
-        if (cnt == 0) continue;
+    auto launch_level = [&](uint64_t lo, uint64_t cnt) -> int {
         const uint32_t* lvl_order = sorted ? nullptr : d_order + lo;
         if (aligned16) {
             // LDS-DMA ring, 8 waves x 128 blocks per workgroup (as the uniform fast path)
@@ -846,6 +882,35 @@ int stormck_commit_device(void* d_arena, stormck_dirty_block* blocks, uint64_t n
                                lvl_order, lo, cnt, d_cs);
         }
         HIP_TRY(hipGetLastError());
+        return STORMCK_OK;
+    };
+    uint32_t first_level = 0;
+    if (sorted) {
+        // Records already children-first: level 0 is records [0, level_start[1]). Upload
+        // and hash it in chunks so the (host-staged) upload of chunk k+1 overlaps the
+        // hashing of chunk k; then upload the rest for the upper levels.
+        const uint64_t l0 = level_start[1];
+        const uint64_t chunk = std::max<uint64_t>(65536, (l0 + 3) / 4);
+        for (uint64_t lo = 0; lo < l0; lo += chunk) {
+            const uint64_t cnt = std::min(chunk, l0 - lo);
+            HIP_TRY(hipMemcpyAsync(d_blocks + lo, blocks + lo, cnt * sizeof(stormck_dirty_block), hipMemcpyHostToDevice, st));
+            rc = launch_level(lo, cnt);
+            if (rc) return rc;
+        }
+        if (n > l0)
+            HIP_TRY(hipMemcpyAsync(d_blocks + l0, blocks + l0, (n - l0) * sizeof(stormck_dirty_block),
+                                   hipMemcpyHostToDevice, st));
+        first_level = 1;
+    } else {
+        HIP_TRY(hipMemcpyAsync(d_blocks, blocks, n * sizeof(stormck_dirty_block), hipMemcpyHostToDevice, st));
+        HIP_TRY(hipMemcpyAsync(d_order, order.data(), n * 4, hipMemcpyHostToDevice, st));
+    }
+    pt.mark("upload_issue");
+    for (uint32_t l = first_level; l <= max_h; ++l) {
+        const uint64_t lo = level_start[l], cnt = level_start[l + 1] - lo;
+        if (cnt == 0) continue;
+        rc = launch_level(lo, cnt);
+        if (rc) return rc;
     }
     HIP_TRY(hipMemcpyAsync(out_checksums, d_cs, n * 8, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
