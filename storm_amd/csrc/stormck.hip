@@ -885,24 +885,34 @@ int stormck_commit_device(void* d_arena, stormck_dirty_block* blocks, uint64_t n
         return STORMCK_OK;
     };
     uint32_t first_level = 0;
+    // Records go up with HIP's pageable staging: the host thread blocks while a chunk
+    // is staged, but the GPU hashes the previous chunk meanwhile. (Staging through the
+    // context's pinned buffers measured no faster: profiles/r01_bench_commit_pinned.txt.)
+    auto upload = [&](uint64_t lo, uint64_t cnt) -> int {
+        HIP_TRY(hipMemcpyAsync(d_blocks + lo, blocks + lo, cnt * sizeof(stormck_dirty_block), hipMemcpyHostToDevice, st));
+        return STORMCK_OK;
+    };
     if (sorted) {
         // Records already children-first: level 0 is records [0, level_start[1]). Upload
-        // and hash it in chunks so the (host-staged) upload of chunk k+1 overlaps the
-        // hashing of chunk k; then upload the rest for the upper levels.
+        // and hash it in chunks so the upload of chunk k+1 overlaps the hashing of chunk
+        // k; then upload the rest for the upper levels.
         const uint64_t l0 = level_start[1];
         const uint64_t chunk = std::max<uint64_t>(65536, (l0 + 3) / 4);
         for (uint64_t lo = 0; lo < l0; lo += chunk) {
             const uint64_t cnt = std::min(chunk, l0 - lo);
-            HIP_TRY(hipMemcpyAsync(d_blocks + lo, blocks + lo, cnt * sizeof(stormck_dirty_block), hipMemcpyHostToDevice, st));
+            rc = upload(lo, cnt);
+            if (rc) return rc;
             rc = launch_level(lo, cnt);
             if (rc) return rc;
         }
-        if (n > l0)
-            HIP_TRY(hipMemcpyAsync(d_blocks + l0, blocks + l0, (n - l0) * sizeof(stormck_dirty_block),
-                                   hipMemcpyHostToDevice, st));
+        if (n > l0) {
+            rc = upload(l0, n - l0);
+            if (rc) return rc;
+        }
         first_level = 1;
     } else {
-        HIP_TRY(hipMemcpyAsync(d_blocks, blocks, n * sizeof(stormck_dirty_block), hipMemcpyHostToDevice, st));
+        rc = upload(0, n);
+        if (rc) return rc;
         HIP_TRY(hipMemcpyAsync(d_order, order.data(), n * 4, hipMemcpyHostToDevice, st));
     }
     pt.mark("upload_issue");
