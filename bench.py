@@ -151,7 +151,7 @@ def commit_workload(a):
                       "hashed_bytes": blocks_bytes},
            "roofline": {"bound": "hbm", "achieved": round(blocks_bytes / (el / a.steps) / 1e9, 1), "peak": HBM_PEAK_GBS,
                         "unit": "GB/s", "frac": round(blocks_bytes / (el / a.steps) / 1e9 / HBM_PEAK_GBS, 4),
-                        "traffic": None, "kernel": "k_commit_level<16> (whole call, host planning included)"},
+                        "traffic": None, "kernel": "k_commit_level_glds<16,nt,8w> (whole call: host planning, record H2D, checksum D2H included)"},
            "root": "0x%016x" % int(cs[-1])}
     if not a.no_cpu:
         res["cpu_baseline"] = cpu_commit_baseline(a.cpu_seconds)

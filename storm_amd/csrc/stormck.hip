@@ -12,9 +12,11 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <functional>
 #include <thread>
 #include <vector>
 
+#include <pthread.h>
 #include <unistd.h>
 
 #include "../../include/stormck.h"
@@ -25,6 +27,79 @@ using namespace stormck;
 namespace {
 
 thread_local std::string g_last_error;
+
+// Fork-join pool for the host-side passes (commit planning, copies into pinned
+// staging). Spawning threads per call cost about 30 us each, which at 16 threads was
+// most of a 1M-record planning pass. Workers spin briefly after a job (the commit
+// issues its passes back to back), then park on a condition variable.
+class ForkJoin {
+  public:
+    static ForkJoin& get() {
+        // never destroyed: workers may be parked at exit. A fork()ed child has none of
+        // the parent's workers, so it drops the instance and builds its own.
+        static std::once_flag once;
+        std::call_once(once, [] { pthread_atfork(nullptr, nullptr, [] { instance_ = nullptr; }); });
+        std::lock_guard<std::mutex> g(make_mu_);
+        if (!instance_) instance_ = new ForkJoin();
+        return *instance_;
+    }
+    unsigned size() const { return nw_ + 1; }
+    // fn(t) for t in [0, parts); parts is clamped to size(); the caller runs t = 0
+    template <class F>
+    void run(unsigned parts, F&& fn) {
+        parts = std::min(parts, size());
+        if (parts <= 1) {
+            fn(0u);
+            return;
+        }
+        std::lock_guard<std::mutex> serial(run_mu_);
+        std::function<void(unsigned)> job = [&](unsigned t) {
+            if (t < parts) fn(t);
+        };
+        job_ = &job;
+        remaining_.store(nw_, std::memory_order_relaxed);
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            gen_.fetch_add(1, std::memory_order_release);
+        }
+        cv_.notify_all();
+        job(0);
+        while (remaining_.load(std::memory_order_acquire) != 0) std::this_thread::yield();
+    }
+
+  private:
+    ForkJoin() {
+        const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+        nw_ = std::min(16u, hw) - 1;
+        for (unsigned i = 0; i < nw_; ++i) std::thread([this, i] { loop(i + 1); }).detach();
+    }
+    void loop(unsigned id) {
+        uint64_t seen = 0;
+        for (;;) {
+            uint64_t g = gen_.load(std::memory_order_acquire);
+            for (int spin = 0; g == seen && spin < 4096; ++spin) {
+                std::this_thread::yield();
+                g = gen_.load(std::memory_order_acquire);
+            }
+            if (g == seen) {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [&] { return gen_.load(std::memory_order_acquire) != seen; });
+                g = gen_.load(std::memory_order_acquire);
+            }
+            seen = g;
+            (*job_)(id);
+            remaining_.fetch_sub(1, std::memory_order_release);
+        }
+    }
+    static inline ForkJoin* instance_ = nullptr;
+    static inline std::mutex make_mu_;
+    unsigned nw_ = 0;
+    std::mutex run_mu_, mu_;
+    std::condition_variable cv_;
+    std::atomic<uint64_t> gen_{0};
+    std::atomic<unsigned> remaining_{0};
+    const std::function<void(unsigned)>* job_ = nullptr;
+};
 
 int fail(int code, const std::string& msg) {
     g_last_error = msg;
@@ -189,6 +264,10 @@ struct DeviceCtx {
     Stage st[kStages];
     void* commit_scratch = nullptr;  // f1: dirty records + checksums + commit order
     uint64_t commit_scratch_bytes = 0;
+    // f1 record uploads: their own stream, so the H2D of chunk k+1 runs while the
+    // caller's stream hashes chunk k; up_ev[s] marks the last DMA out of st[s].pinned
+    hipStream_t copy_stream = nullptr;
+    hipEvent_t up_ev[kStages] = {};
 };
 
 std::mutex g_ctx_mu;
@@ -222,6 +301,11 @@ int ensure_ready(DeviceCtx* c) {
         HIP_TRY(hipMalloc(&s.d_result, 16));
         HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&s.h_result), 16, hipHostMallocDefault));
     }
+    HIP_TRY(hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
+    for (hipEvent_t& e : c->up_ev) {
+        HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        HIP_TRY(hipEventRecord(e, c->copy_stream));  // recorded once, so a wait on it is always valid
+    }
     c->ready = true;
     return STORMCK_OK;
 }
@@ -245,6 +329,15 @@ void release_ctx(DeviceCtx* c) {
         if (s.stream) (void)hipStreamDestroy(s.stream);
         s = Stage();
     }
+    if (c->copy_stream) {
+        (void)hipStreamSynchronize(c->copy_stream);
+        (void)hipStreamDestroy(c->copy_stream);
+        c->copy_stream = nullptr;
+    }
+    for (hipEvent_t& e : c->up_ev) {
+        if (e) (void)hipEventDestroy(e);
+        e = nullptr;
+    }
     c->ready = false;
     if (c->commit_scratch) (void)hipFree(c->commit_scratch);
     c->commit_scratch = nullptr;
@@ -263,20 +356,13 @@ bool is_pinned(const void* p) {
 
 // Parallel memcpy into pinned staging (pageable sources): a single thread cannot
 // feed PCIe Gen5; a few threads can.
-void par_copy(uint8_t* dst, const uint8_t* src, uint64_t bytes) {
-    const uint64_t kMin = 8ULL << 20;
-    unsigned nt = static_cast<unsigned>(std::min<uint64_t>(8, std::max<uint64_t>(1, bytes / kMin)));
-    if (nt <= 1) {
-        std::memcpy(dst, src, bytes);
-        return;
-    }
-    std::vector<std::thread> th;
-    th.reserve(nt);
-    for (unsigned t = 0; t < nt; ++t) {
+void par_copy(uint8_t* dst, const uint8_t* src, uint64_t bytes, uint64_t min_per_thread = 8ULL << 20) {
+    ForkJoin& fj = ForkJoin::get();
+    const unsigned nt = static_cast<unsigned>(std::min<uint64_t>(fj.size(), std::max<uint64_t>(1, bytes / min_per_thread)));
+    fj.run(nt, [&](unsigned t) {
         const uint64_t lo = bytes * t / nt, hi = bytes * (t + 1) / nt;
-        th.emplace_back([=] { std::memcpy(dst + lo, src + lo, hi - lo); });
-    }
-    for (auto& x : th) x.join();
+        std::memcpy(dst + lo, src + lo, hi - lo);
+    });
 }
 
 // Host pipeline shared by checksum_host / verify_host. Blocks are processed in
@@ -748,15 +834,20 @@ int stormck_commit_device(void* d_arena, stormck_dirty_block* blocks, uint64_t n
     if (!d_arena || !blocks || !last_allocated_block || !out_checksums) return fail(STORMCK_EINVAL, "null argument");
     if (n > 0xffffffffULL) return fail(STORMCK_EINVAL, "more than 2^32 dirty blocks");
     PhaseTimer pt("commit");
-    // One parallel pass: validate, and raise every ancestor's height to >= its distance
-    // above each block (atomic max; a walk stops at the first ancestor some walk has
-    // already raised high enough, which then carries the raise further up).
-    std::unique_ptr<std::atomic<uint32_t>[]> height(new std::atomic<uint32_t>[n]);
-    for (uint64_t i = 0; i < n; ++i) height[i].store(0, std::memory_order_relaxed);
+    ForkJoin& fj = ForkJoin::get();
+    const unsigned nt = static_cast<unsigned>(std::min<uint64_t>(fj.size(), n / 16384 + 1));
+    // fn(t, lo, hi) on nt pool threads over contiguous ranges of [0, n)
+    auto par = [&](auto&& fn) { fj.run(nt, [&](unsigned t) { fn(t, n * t / nt, n * (t + 1) / nt); }); };
+    // Pass 1: validate, and raise every ancestor's height to >= its distance above each
+    // block (atomic max; a walk stops at the first ancestor some walk has already raised
+    // high enough, which then carries the raise further up).
+    std::unique_ptr<uint32_t, void (*)(void*)> height_mem(static_cast<uint32_t*>(std::calloc(n, 4)), std::free);
+    if (!height_mem) return fail(STORMCK_ENOMEM, "commit: height array");
+    uint32_t* height = height_mem.get();
     std::atomic<int> bad{0};  // 1 parent range, 2 origin alignment, 3 cycle
     std::atomic<uint64_t> relocating_n{0};
     std::atomic<bool> misaligned{(reinterpret_cast<uintptr_t>(d_arena) & 15) != 0};
-    auto walk = [&](uint64_t lo, uint64_t hi) {
+    par([&](unsigned, uint64_t lo, uint64_t hi) {
         uint64_t reloc = 0;
         bool mis = false;
         for (uint64_t i = lo; i < hi && !bad.load(std::memory_order_relaxed); ++i) {
@@ -784,8 +875,9 @@ int stormck_commit_device(void* d_arena, stormck_dirty_block* blocks, uint64_t n
                     bad.store(3);
                     return;
                 }
-                uint32_t old = height[p].load(std::memory_order_relaxed);
-                while (old < hh && !height[p].compare_exchange_weak(old, hh, std::memory_order_relaxed)) {
+                uint32_t old = __atomic_load_n(&height[p], __ATOMIC_RELAXED);
+                while (old < hh &&
+                       !__atomic_compare_exchange_n(&height[p], &old, hh, true, __ATOMIC_RELAXED, __ATOMIC_RELAXED)) {
                 }
                 if (old >= hh) break;  // another walk holds p at >= hh and carries it upward
                 cur = p;
@@ -793,67 +885,66 @@ int stormck_commit_device(void* d_arena, stormck_dirty_block* blocks, uint64_t n
         }
         relocating_n.fetch_add(reloc, std::memory_order_relaxed);
         if (mis) misaligned.store(true, std::memory_order_relaxed);
-    };
-    {
-        const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-        const unsigned nt = static_cast<unsigned>(std::min<uint64_t>({16u, hw, n / 65536 + 1}));
-        if (nt <= 1) {
-            walk(0, n);
-        } else {
-            std::vector<std::thread> th;
-            for (unsigned t = 0; t < nt; ++t) th.emplace_back(walk, n * t / nt, n * (t + 1) / nt);
-            for (auto& x : th) x.join();
-        }
-    }
+    });
     if (bad.load() == 1) return fail(STORMCK_EINVAL, "parent index out of range");
     if (bad.load() == 2) return fail(STORMCK_EINVAL, "origin_pointer must be 8-byte aligned (Go blocks.Pointer alignment)");
     if (bad.load() == 3) return fail(STORMCK_EINVAL, "parent links form a cycle");
     const uint64_t relocating = relocating_n.load();
     const bool aligned16 = !misaligned.load();
     pt.mark("heights");
-    // children-first commit order: counting sort by height (stable: index order within a
-    // level); skipped when the caller's array is already in that order
+    // Pass 2: per-range height histograms -> level_start, and whether the caller's array
+    // is already children-first. Otherwise a stable counting sort by height gives the
+    // commit order (index order within a level).
+    struct Part {
+        uint32_t max_h = 0;
+        bool sorted = true;
+        std::vector<uint64_t> hist;
+    };
+    std::vector<Part> part(nt);
+    par([&](unsigned t, uint64_t lo, uint64_t hi) {
+        Part& P = part[t];
+        P.hist.assign(8, 0);
+        uint32_t prev = lo ? height[lo - 1] : 0;
+        for (uint64_t i = lo; i < hi; ++i) {
+            const uint32_t hi_ = height[i];
+            P.sorted &= hi_ >= prev;
+            prev = hi_;
+            if (hi_ >= P.hist.size()) P.hist.resize(static_cast<size_t>(hi_) + 1, 0);
+            P.hist[hi_]++;
+            P.max_h = std::max(P.max_h, hi_);
+        }
+    });
     uint32_t max_h = 0;
     bool sorted = true;
-    {
-        uint32_t prev = 0;
-        for (uint64_t i = 0; i < n; ++i) {
-            const uint32_t hi = height[i].load(std::memory_order_relaxed);
-            max_h = std::max(max_h, hi);
-            if (hi < prev) sorted = false;
-            prev = hi;
-        }
+    for (const Part& P : part) {
+        max_h = std::max(max_h, P.max_h);
+        sorted &= P.sorted;
     }
     std::vector<uint64_t> level_start(static_cast<size_t>(max_h) + 2, 0);
-    for (uint64_t i = 0; i < n; ++i) level_start[height[i].load(std::memory_order_relaxed) + 1]++;
+    for (const Part& P : part)
+        for (size_t l = 0; l < P.hist.size(); ++l) level_start[l + 1] += P.hist[l];
     for (uint32_t l = 0; l <= max_h; ++l) level_start[l + 1] += level_start[l];
     std::vector<uint32_t> order;
     if (!sorted) {
         order.resize(n);
-        std::vector<uint64_t> pos(level_start.begin(), level_start.end() - 1);
-        for (uint64_t i = 0; i < n; ++i) order[pos[height[i].load(std::memory_order_relaxed)]++] = static_cast<uint32_t>(i);
+        std::vector<std::vector<uint64_t>> pos(nt, std::vector<uint64_t>(level_start.begin(), level_start.end() - 1));
+        for (unsigned t = 1; t < nt; ++t)
+            for (size_t l = 0; l <= max_h; ++l)
+                pos[t][l] = pos[t - 1][l] + (l < part[t - 1].hist.size() ? part[t - 1].hist[l] : 0);
+        par([&](unsigned t, uint64_t lo, uint64_t hi) {
+            std::vector<uint64_t>& ps = pos[t];
+            for (uint64_t i = lo; i < hi; ++i) order[ps[height[i]]++] = static_cast<uint32_t>(i);
+        });
     }
     pt.mark("order");
-    int rc = device_check();
-    if (rc) return rc;
-    // relocation in commit order (cache/cache.go:114-118), in place like commitBlock
-    uint64_t last = *last_allocated_block;
-    if (relocating) {
-        for (uint64_t k = 0; k < n; ++k) {
-            stormck_dirty_block& b = blocks[sorted ? k : order[k]];
-            if (b.birth_revision <= revision) {
-                b.address = ++last;
-                b.birth_revision = revision + 1;
-            }
-        }
-    }
-    *last_allocated_block = last;
-    pt.mark("relocate");
 
+    // device resources before the records are touched: a failure here leaves them as given
     DeviceCtx* c = nullptr;
-    rc = get_ctx(&c);
+    int rc = get_ctx(&c);
     if (rc) return rc;
     std::lock_guard<std::mutex> g(c->mu);
+    rc = ensure_ready(c);
+    if (rc) return rc;
     const uint64_t need = n * sizeof(stormck_dirty_block) + n * 8 + (sorted ? 0 : n * 4);
     if (c->commit_scratch_bytes < need) {
         if (c->commit_scratch) (void)hipFree(c->commit_scratch);
@@ -862,6 +953,34 @@ int stormck_commit_device(void* d_arena, stormck_dirty_block* blocks, uint64_t n
         HIP_TRY(hipMalloc(&c->commit_scratch, need));
         c->commit_scratch_bytes = need;
     }
+
+    // relocation in commit order (cache/cache.go:114-118), in place like commitBlock:
+    // the k-th relocating block in commit order gets address last + k
+    uint64_t last = *last_allocated_block;
+    if (relocating) {
+        auto at = [&](uint64_t k) -> stormck_dirty_block& { return blocks[sorted ? k : order[k]]; };
+        std::vector<uint64_t> cnt(nt + 1, 0);
+        par([&](unsigned t, uint64_t lo, uint64_t hi) {
+            uint64_t m = 0;
+            for (uint64_t k = lo; k < hi; ++k) m += at(k).birth_revision <= revision;
+            cnt[t + 1] = m;
+        });
+        for (unsigned t = 0; t < nt; ++t) cnt[t + 1] += cnt[t];
+        par([&](unsigned t, uint64_t lo, uint64_t hi) {
+            uint64_t a = last + cnt[t];
+            for (uint64_t k = lo; k < hi; ++k) {
+                stormck_dirty_block& b = at(k);
+                if (b.birth_revision <= revision) {
+                    b.address = ++a;
+                    b.birth_revision = revision + 1;
+                }
+            }
+        });
+        last += relocating;
+    }
+    *last_allocated_block = last;
+    pt.mark("relocate");
+
     auto* d_blocks = static_cast<stormck_dirty_block*>(c->commit_scratch);
     auto* d_cs = reinterpret_cast<uint64_t*>(d_blocks + n);
     auto* d_order = sorted ? nullptr : reinterpret_cast<uint32_t*>(d_cs + n);
@@ -884,36 +1003,53 @@ int stormck_commit_device(void* d_arena, stormck_dirty_block* blocks, uint64_t n
         HIP_TRY(hipGetLastError());
         return STORMCK_OK;
     };
-    uint32_t first_level = 0;
-    // Records go up with HIP's pageable staging: the host thread blocks while a chunk
-    // is staged, but the GPU hashes the previous chunk meanwhile. (Staging through the
-    // context's pinned buffers measured no faster: profiles/r01_bench_commit_pinned.txt.)
-    auto upload = [&](uint64_t lo, uint64_t cnt) -> int {
-        HIP_TRY(hipMemcpyAsync(d_blocks + lo, blocks + lo, cnt * sizeof(stormck_dirty_block), hipMemcpyHostToDevice, st));
+    // Host records go up through the context's two pinned buffers on the copy stream;
+    // the caller's stream waits only for the bytes its next launch reads, so the copy of
+    // chunk k+1 (host memcpy into pinned, then DMA) overlaps the hashing of chunk k.
+    unsigned ring = 0;
+    auto stage_up = [&](void* d_dst, const void* h_src, uint64_t bytes) -> int {
+        const uint8_t* src = static_cast<const uint8_t*>(h_src);
+        uint8_t* dst = static_cast<uint8_t*>(d_dst);
+        hipEvent_t ev = nullptr;
+        while (bytes) {
+            const uint64_t b = std::min<uint64_t>(bytes, kChunkBytes);
+            const unsigned r = ring;
+            ring = (ring + 1) % kStages;
+            HIP_TRY(hipEventSynchronize(c->up_ev[r]));  // the DMA that last read this buffer is done
+            par_copy(c->st[r].pinned, src, b, 1ULL << 20);
+            HIP_TRY(hipMemcpyAsync(dst, c->st[r].pinned, b, hipMemcpyHostToDevice, c->copy_stream));
+            HIP_TRY(hipEventRecord(c->up_ev[r], c->copy_stream));
+            ev = c->up_ev[r];
+            src += b;
+            dst += b;
+            bytes -= b;
+        }
+        if (ev) HIP_TRY(hipStreamWaitEvent(st, ev, 0));
         return STORMCK_OK;
     };
+    uint32_t first_level = 0;
     if (sorted) {
-        // Records already children-first: level 0 is records [0, level_start[1]). Upload
-        // and hash it in chunks so the upload of chunk k+1 overlaps the hashing of chunk
-        // k; then upload the rest for the upper levels.
+        // Records already children-first: level 0 is records [0, level_start[1]); upload
+        // and hash it in chunks, then upload the rest for the upper levels.
         const uint64_t l0 = level_start[1];
-        const uint64_t chunk = std::max<uint64_t>(65536, (l0 + 3) / 4);
+        const uint64_t chunk = std::max<uint64_t>(32768, (l0 + 7) / 8);
         for (uint64_t lo = 0; lo < l0; lo += chunk) {
             const uint64_t cnt = std::min(chunk, l0 - lo);
-            rc = upload(lo, cnt);
+            rc = stage_up(d_blocks + lo, blocks + lo, cnt * sizeof(stormck_dirty_block));
             if (rc) return rc;
             rc = launch_level(lo, cnt);
             if (rc) return rc;
         }
         if (n > l0) {
-            rc = upload(l0, n - l0);
+            rc = stage_up(d_blocks + l0, blocks + l0, (n - l0) * sizeof(stormck_dirty_block));
             if (rc) return rc;
         }
         first_level = 1;
     } else {
-        rc = upload(0, n);
+        rc = stage_up(d_blocks, blocks, n * sizeof(stormck_dirty_block));
         if (rc) return rc;
-        HIP_TRY(hipMemcpyAsync(d_order, order.data(), n * 4, hipMemcpyHostToDevice, st));
+        rc = stage_up(d_order, order.data(), n * 4);
+        if (rc) return rc;
     }
     pt.mark("upload_issue");
     for (uint32_t l = first_level; l <= max_h; ++l) {
@@ -928,7 +1064,9 @@ int stormck_commit_device(void* d_arena, stormck_dirty_block* blocks, uint64_t n
     if (!sorted) {
         // d_cs is in commit order; put it back in the caller's order
         std::vector<uint64_t> tmp(out_checksums, out_checksums + n);
-        for (uint64_t k = 0; k < n; ++k) out_checksums[order[k]] = tmp[k];
+        par([&](unsigned, uint64_t lo, uint64_t hi) {
+            for (uint64_t k = lo; k < hi; ++k) out_checksums[order[k]] = tmp[k];
+        });
         pt.mark("unpermute");
     }
     return STORMCK_OK;

@@ -121,3 +121,27 @@ def test_argument_errors_precede_the_device_check():
     bad["parent"][28] = 0  # root -> leaf 0 -> ... -> root
     assert commit(bad) == _lib.EINVAL and "cycle" in _lib.last_error()
     assert (b["address"] == np.arange(1, len(b) + 1)).all()  # rejected calls left the records untouched
+
+
+@pytest.mark.skipif("_has_gpu()")
+def test_commit_planning_runs_then_fails_loudly_without_device():
+    """The host planning passes (pool threads: heights, histograms, counting sort) run on
+    a 200K-record shuffled forest, then the call stops at the device check with
+    STORMCK_ENODEV and the caller's records are untouched (no relocation applied)."""
+    import numpy as np
+    from storm_amd import _lib, commit as sc
+    b, size, last = sc.pointer_forest(200_000, 1024, 10, slot=1024, revision=5)
+    rng = np.random.default_rng(1)
+    perm = rng.permutation(len(b))
+    inv = np.empty_like(perm)
+    inv[perm] = np.arange(len(b))
+    bp = b[perm].copy()
+    has = bp["parent"] >= 0
+    bp["parent"][has] = inv[bp["parent"][has]]
+    bp["birth_revision"][::3] = 5  # a third would relocate
+    before = bp.copy()
+    la = ctypes.c_uint64(last)
+    cs = np.zeros(len(bp), dtype=np.uint64)
+    rc = _lib.lib.stormck_commit_device(1 << 20, bp.ctypes.data, len(bp), 5, ctypes.byref(la), cs.ctypes.data, None)
+    assert rc == _lib.ENODEV
+    assert np.array_equal(bp, before) and la.value == last
