@@ -12,6 +12,7 @@
 // permutes for the merge; lane 0 of the quad does tail + avalanche. Kernels:
 //   * k_xxh64_glds   : uniform-length batches, stripes staged HBM -> LDS by LDS-DMA
 //   * k_xxh64_quad   : any shape (per-block lengths, offsets, alignment), register loads
+//   * k_xxh64_single : one slice <= 64 KiB read from pinned host memory (latency path)
 //   * k_commit_level*: f1 commit levels; k_pointer_level / _node: Merkle nodes
 //   * k_key_tags*    : f4, one lane per short key
 // (A lane-per-block mapping was measured and rejected: 0.59-0.66 of HBM peak,
@@ -120,6 +121,40 @@ __device__ __forceinline__ uint64_t finish_fast(uint64_t h, uint64_t n, const ui
     return avalanche(h);
 }
 
+// Tail + avalanche for a 16-byte-aligned tail in LDS, read with ds_read_b128 only
+// (at most roundup16(rem) bytes, so never past a 16-byte-padded key). The compiler
+// guards narrower LDS reads behind in-flight LDS-DMA with a full vmcnt(0) wait, which
+// would drain a key kernel's whole prefetch ring at every key's tail.
+__device__ __forceinline__ uint64_t finish_lds16(uint64_t h, uint64_t n, const uint8_t* p, uint32_t rem) {
+    h += n;
+    u64x2 a = {0, 0}, b = {0, 0};
+    if (rem > 0) a = *reinterpret_cast<const u64x2*>(p);
+    if (rem > 16) b = *reinterpret_cast<const u64x2*>(p + 16);
+    const uint64_t w[4] = {a.x, a.y, b.x, b.y};
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+        if (rem >= 8u * (q + 1)) {
+            h ^= round(0, w[q]);
+            h = rotl<27>(h) * kP1 + kP4;
+        }
+    }
+    const uint32_t nw = rem >> 3;
+    uint64_t x = nw == 0 ? w[0] : (nw == 1 ? w[1] : (nw == 2 ? w[2] : w[3]));
+    uint32_t r = rem & 7;
+    if (r >= 4) {
+        h ^= (x & 0xffffffffULL) * kP1;
+        h = rotl<23>(h) * kP2 + kP3;
+        x >>= 32;
+        r -= 4;
+    }
+    for (; r > 0; --r) {
+        h ^= (x & 0xff) * kP5;
+        h = rotl<11>(h) * kP1;
+        x >>= 8;
+    }
+    return avalanche(h);
+}
+
 // ---------------------------------------------------------------------------
 // Quad kernel: 4 lanes per block. Block i starts at base + (OFFS ? offs[i] : i*stride)
 // and is LENS ? lens[i] : len bytes long. 256-thread workgroups = 64 blocks.
@@ -169,6 +204,65 @@ __global__ __launch_bounds__(256) void k_xxh64_quad(const uint8_t* __restrict__ 
 }
 
 // ---------------------------------------------------------------------------
+// Single-slice latency kernel (stormck_checksum = one blocks.Checksum call). One
+// 256-thread workgroup copies the slice from pinned host memory into LDS (every
+// thread issues all of its 16-byte reads before storing any: one PCIe round trip per
+// 64 KiB), quad 0 hashes it from LDS, and lane 0 stores the checksum straight into
+// pinned host memory, so a call is one launch and one stream sync, with no DMA
+// commands. src is 16-byte aligned and readable up to the next 16-byte boundary.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kSingleMax = 64 * 1024;
+
+// K rounds of 16-byte loads per thread, all issued before the first LDS store. Indices
+// past the end clamp to the last word (a duplicate load and an identical store), so
+// there is no per-load branch and no wait between loads.
+template <int K>
+__device__ __forceinline__ void single_stage(const uint4* __restrict__ src, uint4* buf, uint32_t words) {
+    uint4 r[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) r[k] = src[min(threadIdx.x + 256u * k, words - 1)];
+#pragma unroll
+    for (int k = 0; k < K; ++k) buf[min(threadIdx.x + 256u * k, words - 1)] = r[k];
+}
+
+__global__ __launch_bounds__(256) void k_xxh64_single(const uint8_t* __restrict__ src, uint32_t n,
+                                                        uint64_t* __restrict__ out) {
+    __shared__ uint4 buf[kSingleMax / 16];
+    const uint32_t words = (n + 15) / 16;
+    const uint4* s16 = reinterpret_cast<const uint4*>(src);
+    switch ((words + 255) / 256) {
+        case 0: break;
+        case 1: single_stage<1>(s16, buf, words); break;
+        case 2: single_stage<2>(s16, buf, words); break;
+        case 3: single_stage<3>(s16, buf, words); break;
+        case 4: single_stage<4>(s16, buf, words); break;
+        case 5: single_stage<5>(s16, buf, words); break;
+        case 6: single_stage<6>(s16, buf, words); break;
+        case 7: single_stage<7>(s16, buf, words); break;
+        case 8: single_stage<8>(s16, buf, words); break;
+        case 9: single_stage<9>(s16, buf, words); break;
+        case 10: single_stage<10>(s16, buf, words); break;
+        case 11: single_stage<11>(s16, buf, words); break;
+        case 12: single_stage<12>(s16, buf, words); break;
+        case 13: single_stage<13>(s16, buf, words); break;
+        case 14: single_stage<14>(s16, buf, words); break;
+        case 15: single_stage<15>(s16, buf, words); break;
+        default: single_stage<16>(s16, buf, words); break;
+    }
+    __syncthreads();
+    if (threadIdx.x >= 4) return;
+    const uint32_t j = threadIdx.x;
+    const uint8_t* s = reinterpret_cast<const uint8_t*>(buf);
+    const uint32_t nst = n >> 5;
+    const uint64_t acc = quad_stripes_aligned<16>(reinterpret_cast<const uint64_t*>(s) + j, nst, acc_seed(j));
+    const uint64_t v1 = quad_bcast<0>(acc), v2 = quad_bcast<1>(acc), v3 = quad_bcast<2>(acc), v4 = quad_bcast<3>(acc);
+    if (j == 0) {
+        const uint64_t h0 = (n >= 32) ? converge(v1, v2, v3, v4) : kP5;
+        *out = finish_fast(h0, n, s + 32 * nst, n & 31);
+    }
+}
+
+// ---------------------------------------------------------------------------
 // LDS-staged quad kernel ("glds"): uniform length, 16-byte aligned base/stride.
 // A 256-thread workgroup owns 64 consecutive blocks. Tiles of T stripes (32*T bytes)
 // of all 64 blocks stream HBM -> LDS with global_load_lds_dwordx4 (each wave-
@@ -194,6 +288,13 @@ __device__ __forceinline__ void wait_vmcnt() {
 #if defined(__HIP_DEVICE_COMPILE__)
     constexpr int imm = (N & 0xF) | ((N >> 4) << 14) | (0x7 << 4) | (0xF << 8);
     __builtin_amdgcn_s_waitcnt(imm);
+#endif
+}
+
+// Wait for this wave's outstanding LDS reads (lgkmcnt(0)), vmcnt/expcnt untouched.
+__device__ __forceinline__ void wait_lgkm0() {
+#if defined(__HIP_DEVICE_COMPILE__)
+    __builtin_amdgcn_s_waitcnt(0xF | (0x3 << 14) | (0x7 << 4));
 #endif
 }
 
@@ -696,6 +797,84 @@ __global__ __launch_bounds__(256) void k_key_tags(const uint8_t* __restrict__ ke
 // lanes hash the current one from LDS (lane l: its key at l*stride). Only whole
 // batches of 64 keys; the caller hashes the remainder with k_key_tags. Waits are per
 // wave (vmcnt + the wave's own LDS), so no workgroup barrier is needed.
+// f4 ring variant for a compile-time stride of 16*P bytes: each wave owns PW
+// consecutive batches of 64 keys, keeps RING-1 batches in flight through a RING-slot
+// LDS ring, and holds its PW tags in registers until the end, so the loop issues no
+// stores and a counted vmcnt wait ((RING-2)*P LDS-DMA ops younger than the batch being
+// hashed) is exact. A wave with fewer than PW batches (the grid's last) waits vmcnt(0).
+template <int AUX, int P, int RING, int PW>
+__global__ __launch_bounds__(256) void k_key_tags_ring(const uint8_t* __restrict__ keys, uint32_t len, uint64_t batches,
+                                                        uint64_t* __restrict__ out) {
+    static_assert(RING >= 2 && PW >= RING, "ring");
+    constexpr uint32_t kStride = 16 * P, kRegion = 64 * kStride;
+    extern __shared__ __attribute__((aligned(16))) uint8_t dyn_lds[];
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    uint8_t* buf = dyn_lds + wave * RING * kRegion;
+    const uint64_t b0 = (static_cast<uint64_t>(blockIdx.x) * 4 + wave) * PW;
+    if (b0 >= batches) return;
+    const uint32_t nb = static_cast<uint32_t>(batches - b0 < PW ? batches - b0 : PW);
+    const uint32_t nst = len >> 5, rem = len & 31;
+#if defined(__HIP_DEVICE_COMPILE__)
+#define STORMCK_RING_ISSUE(I)                                                                              \
+    do {                                                                                                  \
+        const uint8_t* s_ = keys + (b0 + (I)) * kRegion + lane * 16;                                      \
+        uint8_t* d_ = buf + ((I) % RING) * kRegion;                                                       \
+        _Pragma("unroll") for (int p_ = 0; p_ < P; ++p_)                                                  \
+            __builtin_amdgcn_global_load_lds(s_ + p_ * 1024, d_ + p_ * 1024, 16, 0, AUX);                  \
+    } while (0)
+#else
+#define STORMCK_RING_ISSUE(I) do { } while (0)
+#endif
+    auto hash_slot = [&](uint32_t i) -> uint64_t {
+        const uint8_t* k = buf + (i % RING) * kRegion + lane * kStride;
+        uint64_t hh;
+        if (len >= 32) {
+            uint64_t v1 = kV1, v2 = kV2, v3 = kV3, v4 = kV4;
+            for (uint32_t s = 0; s < nst; ++s) {
+                const u64x2 x = *reinterpret_cast<const u64x2*>(k + 32 * s);
+                const u64x2 y = *reinterpret_cast<const u64x2*>(k + 32 * s + 16);
+                v1 = round(v1, x.x);
+                v2 = round(v2, x.y);
+                v3 = round(v3, y.x);
+                v4 = round(v4, y.y);
+            }
+            hh = converge(v1, v2, v3, v4);
+        } else {
+            hh = kP5;
+        }
+        return finish_lds16(hh, len, k + 32 * nst, rem);
+    };
+    uint64_t h[PW];
+    if (nb == PW) {
+#pragma unroll
+        for (int i = 0; i < RING - 1; ++i) STORMCK_RING_ISSUE(i);
+#pragma unroll
+        for (int i = 0; i < PW; ++i) {
+            // batches i+1 .. min(i+RING-2, PW-1) were issued after batch i
+            constexpr int kYoungest = RING - 2;
+            if (i + kYoungest <= PW - 1) wait_vmcnt<kYoungest * P>();
+            else wait_vmcnt<0>();
+            // slot (i+RING-1) % RING was last read by batch i-1: its LDS reads retire first
+            if (i + RING - 1 < PW) {
+                wait_lgkm0();
+                STORMCK_RING_ISSUE(i + RING - 1);
+            }
+            h[i] = hash_slot(i);
+        }
+    } else {
+        for (uint32_t i = 0; i < nb; ++i) {
+            STORMCK_RING_ISSUE(i);
+            wait_vmcnt<0>();
+            h[0] = hash_slot(i);
+            out[(b0 + i) * 64 + lane] = h[0];
+        }
+        return;
+    }
+#pragma unroll
+    for (int i = 0; i < PW; ++i) out[(b0 + i) * 64 + lane] = h[i];
+#undef STORMCK_RING_ISSUE
+}
+
 template <int AUX>
 __global__ __launch_bounds__(256) void k_key_tags_lds(const uint8_t* __restrict__ keys, uint32_t stride, uint32_t len,
                                                        uint64_t batches, uint32_t per_wave,
@@ -742,7 +921,7 @@ __global__ __launch_bounds__(256) void k_key_tags_lds(const uint8_t* __restrict_
         } else {
             h = kP5;
         }
-        out[b * 64 + lane] = finish_fast(h, len, k + 32 * nst, rem);
+        out[b * 64 + lane] = finish_lds16(h, len, k + 32 * nst, rem);
         // the slot is refilled two batches later, after this wave's reads retired
         // (the compiler waits lgkmcnt before the hash consumes them)
     }

@@ -577,7 +577,24 @@ int stormck_checksum(const void* p, uint64_t n_bytes, uint64_t* out) {
     static const uint8_t empty = 0;
     if (n_bytes == 0) p = &empty;  // XXH64 of an empty slice: nothing is read
     if (!p) return fail(STORMCK_EINVAL, "p is null");
-    return host_pipeline(p, 0, nullptr, static_cast<uint32_t>(n_bytes), 1, out, nullptr, nullptr, nullptr);
+    if (n_bytes > kSingleMax)
+        return host_pipeline(p, 0, nullptr, static_cast<uint32_t>(n_bytes), 1, out, nullptr, nullptr, nullptr);
+    // latency path: memcpy into pinned staging, one kernel that reads it over PCIe and
+    // writes the checksum into pinned memory, one sync
+    DeviceCtx* c = nullptr;
+    int rc = get_ctx(&c);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> g(c->mu);
+    rc = ensure_ready(c);
+    if (rc) return rc;
+    Stage& s = c->st[0];
+    std::memcpy(s.pinned, p, n_bytes);
+    hipLaunchKernelGGL(k_xxh64_single, dim3(1), dim3(256), 0, s.stream, s.pinned, static_cast<uint32_t>(n_bytes),
+                       s.h_out);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(s.stream));
+    *out = s.h_out[0];
+    return STORMCK_OK;
 }
 
 int stormck_host_register(void* p, uint64_t bytes) {

@@ -58,6 +58,23 @@ def test_public_answers_single_call(dev):
         assert blocks.Checksum(s.encode()) == hx(v)
 
 
+def test_single_call_latency_path_lengths(dev):
+    """stormck_checksum (one Go blocks.Checksum call): slices up to 64 KiB go through the
+    one-launch kernel that reads pinned host memory (every staging round count 1..16,
+    clamped last round), longer ones through the host pipeline. Unaligned Python views
+    exercise the host-side copy."""
+    from oracle import oracle as o
+    from storm_amd import blocks
+    rng = np.random.default_rng(5)
+    data = rng.integers(0, 256, size=(1 << 17) + 64, dtype=np.uint8)
+    lengths = list(range(0, 100)) + [72, 255, 256, 4095, 4096, 4097, 28808, 30000, 31808, 32768,
+                                     65535, 65536, 65537, 100000, 1 << 17]
+    for L in lengths:
+        for off in (0, 3):
+            sl = data[off:off + L]  # numpy view: off = 3 hands the library an unaligned pointer
+            assert blocks.Checksum(sl) == o.xxh64(sl), (L, off)
+
+
 # ---------------------------------------------------------------------------
 # c1: 1K synthetic 32 KiB blocks; generator parity
 # ---------------------------------------------------------------------------

@@ -98,8 +98,9 @@ def main():
             res["read_verify_note"] = "parallel pread (16 threads) from page cache on a reader thread, 1 GiB ahead of the pipelined H2D + verify"
         finally:
             os.close(fd)
-    # single-call latency (blocks.Checksum on one buffer: H2D + launch + D2H)
-    for size in (72, BLOCK):
+    # single-call latency (blocks.Checksum on one buffer: <= 64 KiB is one launch that
+    # reads pinned staging over PCIe and writes the checksum to pinned memory)
+    for size in (0, 72, 4096, 30000, BLOCK, 65536):
         one = host[0, :size].copy()
         blocks.Checksum(one)
         k = 2000
@@ -107,6 +108,20 @@ def main():
         for _ in range(k):
             blocks.Checksum(one)
         res[f"single_call_us_{size}B"] = round((time.perf_counter() - t0) / k * 1e6, 2)
+    # the same hash with the block already in HBM, one block per launch, back-to-back
+    # launches timed by events: the serial XXH64 chain of one block on one quad of lanes
+    d1 = torch.from_numpy(host[0].copy()).to(dev)
+    o1 = torch.empty(1, dtype=torch.int64, device=dev)
+    st = torch.cuda.current_stream(dev).cuda_stream
+    for size in (72, BLOCK):
+        engine.checksum_device(d1.data_ptr(), BLOCK, 1, o1.data_ptr(), size, stream=st)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(200):
+            engine.checksum_device(d1.data_ptr(), BLOCK, 1, o1.data_ptr(), size, stream=st)
+        e1.record()
+        torch.cuda.synchronize()
+        res[f"device_one_block_us_{size}B"] = round(e0.elapsed_time(e1) / 200 * 1e3, 2)
     print(json.dumps(res), flush=True)
 
 
