@@ -43,6 +43,9 @@ def parse():
     p.add_argument("--arena", type=int, default=4 << 20, help="resident arena (blocks)")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget (rank 0, N=1)")
     p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--settle", type=float, default=1.0,
+                   help="before the W warmup steps, run untimed steps for at least this many seconds so the "
+                        "GPU clocks settle (short workloads otherwise time a ramping clock)")
     p.add_argument("--workload", default="c3", choices=["c3", "commit", "keytags"],
                    help="c3 = BASELINE metric (default); commit = f1 level-synchronous Cache.Commit of a dirty "
                         "forest; keytags = f4 xxhash.Sum64 of 48-byte keys")
@@ -52,6 +55,15 @@ def parse():
     p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                    help="nccl = RCCL (production); gloo only to rehearse N>1 with ranks sharing a GPU")
     return p.parse_args()
+
+
+def settle(step, seconds: float):
+    """Untimed steps until `seconds` of wall time have passed (GPU clock ramp)."""
+    import torch
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        step()
+        torch.cuda.synchronize()
 
 
 def cpu_baseline(seconds: float):
@@ -132,6 +144,7 @@ def commit_workload(a):
     torch.cuda.synchronize()
     # every block is new in this revision (birth = REV + 1), so commit relocates nothing
     # and the metadata array is reusable across steps unchanged
+    settle(lambda: sc.commit_device(arena.data_ptr(), b0, REV, last), a.settle)
     for _ in range(a.warmup):
         sc.commit_device(arena.data_ptr(), b0, REV, last)
     torch.cuda.synchronize()
@@ -172,6 +185,8 @@ def keytags_workload(a):
     engine.fill_synthetic_device(keys.data_ptr(), 48 * 1024, n * klen // (48 * 1024), 0, 0x53544F524D)
     out = torch.empty(n, dtype=torch.int64, device=dev)
     st = torch.cuda.current_stream(dev).cuda_stream
+    settle(lambda: engine.key_tags_device(keys.data_ptr(), n, out.data_ptr(), stride=klen, length=klen, stream=st),
+           a.settle)
     for _ in range(a.warmup):
         engine.key_tags_device(keys.data_ptr(), n, out.data_ptr(), stride=klen, length=klen, stream=st)
     torch.cuda.synchronize()
@@ -192,7 +207,7 @@ def keytags_workload(a):
            "roofline": {"bound": "hbm", "achieved": round(n * (klen + 8) / (kms * 1e-3) / 1e9, 1),
                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(n * (klen + 8) / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
-                        "kernel": "k_key_tags_lds<nt> (per-wave LDS-DMA double buffer)", "avg_launch_ms": round(kms, 4)}}
+                        "kernel": "k_key_tags_ring<nt,3,4,8> (per-wave 4-slot LDS-DMA ring)", "avg_launch_ms": round(kms, 4)}}
     if not a.no_cpu:
         from oracle import oracle as o
         m = 1 << 20
@@ -267,6 +282,7 @@ def main():
             root, _ = sdist.global_root(root, REV, n_total, lambda t, r, ad: engine.combine_roots_tensor(t, r, ad, FANOUT))
         return root
 
+    settle(lambda: step(False), a.settle)
     for _ in range(a.warmup):
         step(False)
     torch.cuda.synchronize()

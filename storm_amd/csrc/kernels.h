@@ -13,6 +13,7 @@
 //   * k_xxh64_glds   : uniform-length batches, stripes staged HBM -> LDS by LDS-DMA
 //   * k_xxh64_quad   : any shape (per-block lengths, offsets, alignment), register loads
 //   * k_xxh64_single : one slice <= 64 KiB read from pinned host memory (latency path)
+//   * k_xxh64_wide   : small batches, one workgroup per block staged whole into LDS
 //   * k_commit_level*: f1 commit levels; k_pointer_level / _node: Merkle nodes
 //   * k_key_tags*    : f4, one lane per short key
 // (A lane-per-block mapping was measured and rejected: 0.59-0.66 of HBM peak,
@@ -259,6 +260,70 @@ __global__ __launch_bounds__(256) void k_xxh64_single(const uint8_t* __restrict_
     if (j == 0) {
         const uint64_t h0 = (n >= 32) ? converge(v1, v2, v3, v4) : kP5;
         *out = finish_fast(h0, n, s + 32 * nst, n & 31);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Small-batch kernel ("wide"): one 256-thread workgroup per block. The block (its
+// 16-byte-aligned cover, <= 32 KiB) moves HBM -> registers -> LDS in ONE memory round
+// trip (every thread issues all its loads before storing any), then quad 0 hashes it
+// from LDS. Per-block latency = one round trip + the serial XXH64 chain, where the
+// streaming kernels pay a round trip per tile and put 128 blocks on one CU; the host
+// picks it for batches too small to fill the chip (launch_checksum). A block whose
+// cover exceeds 32 KiB (per-block lengths only) is hashed straight from memory.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kWideMax = 32 * 1024;
+
+template <bool LENS, bool OFFS, bool VERIFY>
+__global__ __launch_bounds__(256) void k_xxh64_wide(const uint8_t* __restrict__ base, uint64_t stride,
+                                                      const uint32_t* __restrict__ lens, uint32_t len,
+                                                      const uint64_t* __restrict__ offs, uint64_t n,
+                                                      uint64_t* __restrict__ out,
+                                                      const uint64_t* __restrict__ expected,
+                                                      unsigned long long* __restrict__ first_bad,
+                                                      unsigned long long* __restrict__ n_bad) {
+    __shared__ uint4 buf[kWideMax / 16];
+    const uint64_t blk = blockIdx.x;
+    const uint8_t* src = base + (OFFS ? offs[blk] : blk * stride);
+    const uint32_t L = LENS ? lens[blk] : len;
+    const uint32_t shift = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(src) & 15);
+    const uint32_t words = (shift + L + 15) / 16;
+    const uint8_t* s = src;
+    if (words <= kWideMax / 16) {
+        // a 16-byte window holding a byte of the block lies in that byte's page
+        const uint4* cover = reinterpret_cast<const uint4*>(src - shift);
+        switch ((words + 255) / 256) {
+            case 0: break;
+            case 1: single_stage<1>(cover, buf, words); break;
+            case 2: single_stage<2>(cover, buf, words); break;
+            case 3: single_stage<3>(cover, buf, words); break;
+            case 4: single_stage<4>(cover, buf, words); break;
+            case 5: single_stage<5>(cover, buf, words); break;
+            case 6: single_stage<6>(cover, buf, words); break;
+            case 7: single_stage<7>(cover, buf, words); break;
+            default: single_stage<8>(cover, buf, words); break;
+        }
+        __syncthreads();
+        s = reinterpret_cast<const uint8_t*>(buf) + shift;
+    }
+    if (threadIdx.x >= 4) return;
+    const uint32_t j = threadIdx.x;
+    const uint32_t nst = L >> 5;
+    uint64_t acc = acc_seed(j);
+    if ((shift & 7) == 0) acc = quad_stripes_aligned<16>(reinterpret_cast<const uint64_t*>(s) + j, nst, acc);
+    else acc = quad_stripes_unaligned(s + 8 * j, nst, acc);
+    const uint64_t v1 = quad_bcast<0>(acc), v2 = quad_bcast<1>(acc), v3 = quad_bcast<2>(acc), v4 = quad_bcast<3>(acc);
+    if (j == 0) {
+        const uint64_t h0 = (L >= 32) ? converge(v1, v2, v3, v4) : kP5;
+        const uint64_t h = finish_fast(h0, L, s + 32 * static_cast<uint64_t>(nst), L & 31);
+        if (VERIFY) {
+            if (h != expected[blk]) {
+                atomicMin(first_bad, static_cast<unsigned long long>(blk));
+                atomicAdd(n_bad, 1ULL);
+            }
+        } else {
+            out[blk] = h;
+        }
     }
 }
 

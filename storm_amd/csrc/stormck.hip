@@ -129,6 +129,8 @@ constexpr int kGldsWaves = 8;
 constexpr unsigned kGldsThreads = 64 * kGldsWaves;
 constexpr unsigned kGldsBlocks = 16 * kGldsWaves;
 constexpr int kAuxNT = 2;
+constexpr uint64_t kWideBatch = 128;      // batches up to this many blocks: k_xxh64_wide
+constexpr uint64_t kStreamBatch = 16384;  // uniform batches from this many blocks: k_xxh64_glds
 constexpr unsigned kThreads = 256;
 constexpr uint32_t kMaxFanout = 1u << 16;
 
@@ -166,9 +168,33 @@ int launch_checksum(const uint8_t* base, uint64_t stride, const uint32_t* lens, 
                     uint64_t n, uint64_t* out, const uint64_t* expected, unsigned long long* first_bad,
                     unsigned long long* n_bad, hipStream_t st) {
     const bool verify = expected != nullptr;
-    // Fast path: uniform length, 16-byte aligned blocks at a fixed stride, at least one
-    // LDS tile per block -> LDS-staged kernel (global_load_lds, non-temporal).
-    if (!lens && !offs && (reinterpret_cast<uintptr_t>(base) & 15) == 0 && (stride & 15) == 0 &&
+    // Batch-size dispatch (profiles/r01_probe_small.txt, us per launch at 32 KiB):
+    //  * n <= kWideBatch: one workgroup per block, whole block staged in one round trip
+    //  * n <  kStreamBatch: register quad kernel (64 blocks per workgroup spread the
+    //    batch over the chip; the streaming kernel's 128-block workgroups would occupy
+    //    fewer than half of the CUs)
+    //  * otherwise, uniform length, 16-byte aligned blocks at a fixed stride, at least
+    //    one LDS tile per block: LDS-staged streaming kernel (global_load_lds, nt)
+    if (n <= kWideBatch) {
+#define STORMCK_WIDE(LENS, OFFS, VER)                                                                           \
+    hipLaunchKernelGGL((k_xxh64_wide<LENS, OFFS, VER>), dim3(static_cast<unsigned>(n)), dim3(kThreads), 0, st, base, \
+                       stride, lens, len, offs, n, out, expected, first_bad, n_bad)
+        if (!verify) {
+            if (lens && offs) STORMCK_WIDE(true, true, false);
+            else if (lens) STORMCK_WIDE(true, false, false);
+            else if (offs) STORMCK_WIDE(false, true, false);
+            else STORMCK_WIDE(false, false, false);
+        } else {
+            if (lens && offs) STORMCK_WIDE(true, true, true);
+            else if (lens) STORMCK_WIDE(true, false, true);
+            else if (offs) STORMCK_WIDE(false, true, true);
+            else STORMCK_WIDE(false, false, true);
+        }
+#undef STORMCK_WIDE
+        HIP_TRY(hipGetLastError());
+        return STORMCK_OK;
+    }
+    if (n >= kStreamBatch && !lens && !offs && (reinterpret_cast<uintptr_t>(base) & 15) == 0 && (stride & 15) == 0 &&
         len >= 32u * kTileStripes) {
         const uint64_t wgs = (n + kGldsBlocks - 1) / kGldsBlocks;
         if (wgs > 0x7fffffffULL) return fail(STORMCK_EINVAL, "batch too large for one launch");
@@ -815,15 +841,38 @@ int stormck_key_tags_device(const void* d_keys, uint64_t stride, const uint64_t*
     const uint8_t* k = static_cast<const uint8_t*>(d_keys);
     if (!d_offsets && !d_lens && stride >= 16 && stride <= 256 && (stride & 15) == 0 && len <= stride &&
         (reinterpret_cast<uintptr_t>(k) & 15) == 0 && n >= 64) {
-        // whole batches of 64 keys through the per-wave LDS-DMA double buffer
+        // whole batches of 64 keys through a per-wave LDS-DMA prefetch ring: keys up to
+        // 64 bytes (storm's 48-byte keys) take the 4-slot ring with a compile-time
+        // stride, longer ones the runtime-stride double buffer
         const uint64_t batches = n / 64;
         constexpr uint32_t kPerWave = 8;
+        constexpr int kKeyRing = 4;
         const uint64_t waves = (batches + kPerWave - 1) / kPerWave;
         const uint64_t wgs = (waves + 3) / 4;
         if (wgs > 0x7fffffffULL) return fail(STORMCK_EINVAL, "batch too large for one launch");
-        const size_t lds_bytes = 4 * 2 * 64 * static_cast<size_t>(stride);
-        hipLaunchKernelGGL(k_key_tags_lds<kAuxNT>, dim3(static_cast<unsigned>(wgs)), dim3(kThreads), lds_bytes, st, k,
-                           static_cast<uint32_t>(stride), len, batches, kPerWave, d_out);
+        const dim3 grid_k(static_cast<unsigned>(wgs));
+        const size_t ring_lds = 4 * kKeyRing * 64 * static_cast<size_t>(stride);
+        switch (stride) {
+            case 16:
+                hipLaunchKernelGGL((k_key_tags_ring<kAuxNT, 1, kKeyRing, kPerWave>), grid_k, dim3(kThreads), ring_lds, st,
+                                   k, len, batches, d_out);
+                break;
+            case 32:
+                hipLaunchKernelGGL((k_key_tags_ring<kAuxNT, 2, kKeyRing, kPerWave>), grid_k, dim3(kThreads), ring_lds, st,
+                                   k, len, batches, d_out);
+                break;
+            case 48:
+                hipLaunchKernelGGL((k_key_tags_ring<kAuxNT, 3, kKeyRing, kPerWave>), grid_k, dim3(kThreads), ring_lds, st,
+                                   k, len, batches, d_out);
+                break;
+            case 64:
+                hipLaunchKernelGGL((k_key_tags_ring<kAuxNT, 4, kKeyRing, kPerWave>), grid_k, dim3(kThreads), ring_lds, st,
+                                   k, len, batches, d_out);
+                break;
+            default:
+                hipLaunchKernelGGL(k_key_tags_lds<kAuxNT>, grid_k, dim3(kThreads), 4 * 2 * 64 * static_cast<size_t>(stride),
+                                   st, k, static_cast<uint32_t>(stride), len, batches, kPerWave, d_out);
+        }
         HIP_TRY(hipGetLastError());
         const uint64_t done = batches * 64;
         if (done == n) return STORMCK_OK;
@@ -970,6 +1019,7 @@ int stormck_commit_device(void* d_arena, stormck_dirty_block* blocks, uint64_t n
         HIP_TRY(hipMalloc(&c->commit_scratch, need));
         c->commit_scratch_bytes = need;
     }
+    pt.mark("ctx");
 
     // relocation in commit order (cache/cache.go:114-118), in place like commitBlock:
     // the k-th relocating block in commit order gets address last + k
@@ -1004,7 +1054,7 @@ int stormck_commit_device(void* d_arena, stormck_dirty_block* blocks, uint64_t n
     hipStream_t st = static_cast<hipStream_t>(stream);
     auto launch_level = [&](uint64_t lo, uint64_t cnt) -> int {
         const uint32_t* lvl_order = sorted ? nullptr : d_order + lo;
-        if (aligned16) {
+        if (aligned16 && cnt >= kStreamBatch) {
             // LDS-DMA ring, 8 waves x 128 blocks per workgroup (as the uniform fast path)
             const uint64_t wgs = (cnt + kGldsBlocks - 1) / kGldsBlocks;
             if (wgs > 0x7fffffffULL) return fail(STORMCK_EINVAL, "level too large");

@@ -123,6 +123,32 @@ def test_device_commit_random_forests(dev, n, fanout, slot):
 
 
 @pytest.mark.gpu
+def test_device_commit_streaming_level_mixed_lengths(dev):
+    """A level of >= 16384 blocks takes the LDS-DMA commit kernel: 20000 leaves of mixed
+    storm lengths (workgroups whose blocks run out of stripes at different tiles), a
+    third relocating, shuffled dirty list; vs the oracle's serial commit."""
+    rng = np.random.default_rng(20000)
+    n, slot = 20000, 32768
+    lens = rng.choice([72, 28808, 30000, 31808, 32768, 4097, 512], size=n)
+    b, size, last = sc.pointer_forest(n, lens, 1200, slot=slot, revision=4, first_address=7)
+    b["birth_revision"][::3] = 2
+    arena = np.zeros(size, dtype=np.uint8)
+    arena[slot:slot + n * slot] = rng.integers(0, 256, size=n * slot, dtype=np.uint8)
+    perm = rng.permutation(len(b))
+    inv = np.empty_like(perm)
+    inv[perm] = np.arange(len(b))
+    bp = b[perm].copy()
+    has = bp["parent"] >= 0
+    bp["parent"][has] = inv[bp["parent"][has]]
+    ref_arena, ref_b = arena.copy(), bp.copy()
+    want_cs, want_last = o.commit(ref_arena, ref_b, 4, last)
+    out, cs, last2 = device_commit(arena, bp, 4, last, dev)
+    assert np.array_equal(cs, want_cs)
+    assert np.array_equal(bp["address"], ref_b["address"]) and last2 == want_last
+    assert np.array_equal(out, ref_arena)
+
+
+@pytest.mark.gpu
 @pytest.mark.slow
 def test_device_commit_1m_leaves_properties(dev):
     """1M dirty 32 KiB leaves + 835 pointer blocks (fan-out 1200), all in HBM: after the

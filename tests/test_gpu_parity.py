@@ -121,8 +121,9 @@ def test_synth_vs_oracle_random_lengths(dev):
 
 @pytest.mark.parametrize("length", [512, 513, 520, 1000, 8192, 28808, 30000, 31808, 32768])
 def test_uniform_fast_path_lengths(dev, length):
-    """Uniform-length 16-byte-aligned batches take the LDS-staged kernel: whole tiles,
-    remainder stripes and tails, partial last workgroup (n % 64 != 0)."""
+    """Uniform-length 16-byte-aligned batches of every batch-size class: <= 128 blocks
+    (one workgroup per block), < 16384 (register quad), >= 16384 (LDS-staged streaming
+    kernel: whole tiles, remainder stripes and tails, partial last workgroup)."""
     from oracle import oracle as o
     from storm_amd import engine
     rng = np.random.default_rng(length)
@@ -142,6 +143,22 @@ def test_uniform_fast_path_lengths(dev, length):
     engine.verify_device(d.data_ptr(), stride, 1000, exp.data_ptr(), res.data_ptr(), length)
     torch.cuda.synchronize()
     assert _u64(res).tolist() == [500, 2]
+    # streaming-kernel batch: device-generated blocks, n % 128 != 0, then verify
+    n = 16384 + 65
+    big = torch.empty((n, stride), dtype=torch.uint8, device=dev)
+    engine.fill_synthetic_device(big.data_ptr(), stride, n, length, 0x1234)
+    out = engine.checksum_tensor(big, length=length)
+    torch.cuda.synchronize()
+    want = o.checksum_batch(big.cpu().numpy(), n, stride, length, threads=8)
+    assert np.array_equal(_u64(out), want), (length, n)
+    exp = torch.from_numpy(want.view(np.int64).copy()).to(dev)
+    exp[n - 1] ^= 1
+    exp[16400] ^= 1
+    exp[7] ^= 1
+    res = torch.zeros(2, dtype=torch.int64, device=dev)
+    engine.verify_device(big.data_ptr(), stride, n, exp.data_ptr(), res.data_ptr(), length)
+    torch.cuda.synchronize()
+    assert _u64(res).tolist() == [7, 3]
 
 
 def test_mixed_c5(dev):
@@ -428,6 +445,18 @@ def test_key_tags_f4(dev):
         engine.key_tags_device(d2.data_ptr(), m, o2.data_ptr(), stride=stride, length=klen)
         torch.cuda.synchronize()
         assert np.array_equal(_u64(o2), o.checksum_batch(k2, m, stride, klen)), (stride, klen, m)
+    # compile-time-stride ring (strides 16..64): every key length up to the stride (all
+    # tail shapes of the b128-only LDS tail), full waves of 8 batches, a partial last
+    # wave (3 batches) and a lane-kernel remainder (7 keys)
+    m = 64 * 8 * 5 + 64 * 3 + 7
+    for stride in (16, 32, 48, 64):
+        k2 = rng.integers(0, 256, size=(m, stride), dtype=np.uint8)
+        d2 = _to_dev(k2, dev)
+        o2 = torch.empty(m, dtype=torch.int64, device=dev)
+        for klen in range(0, stride + 1):
+            engine.key_tags_device(d2.data_ptr(), m, o2.data_ptr(), stride=stride, length=klen)
+            torch.cuda.synchronize()
+            assert np.array_equal(_u64(o2), o.checksum_batch(k2, m, stride, klen)), (stride, klen)
 
 
 def test_read_verify_fd_f2(dev, tmp_path):
