@@ -103,6 +103,11 @@ int stormck_checksum(const void* p, uint64_t n_bytes, uint64_t* out);
 /* Page-lock a host range so the host path can DMA from it without staging copies. */
 int stormck_host_register(void* p, uint64_t bytes);
 int stormck_host_unregister(void* p);
+/* Device-visible address of host memory registered with stormck_host_register: the
+ * *_device entry points (stormck_commit_device's arena included) then read and write
+ * it in place over PCIe. This runs f1 on storm's cache.data where it lives, in host
+ * memory (cache/cache.go:36-40), at link rate instead of HBM rate. */
+int stormck_host_device_pointer(void* p, void** d_p);
 
 /* ---- Merkle pointer tree (storm pointer.Block nodes) -----------------------
  * One level: children are entries {cs[i], child_addr_base + i, rev}, all of type

@@ -53,6 +53,7 @@ SIGNATURES = {
     "stormck_checksum": (c_int, [c_void_p, c_uint64, POINTER(c_uint64)]),
     "stormck_host_register": (c_int, [c_void_p, c_uint64]),
     "stormck_host_unregister": (c_int, [c_void_p]),
+    "stormck_host_device_pointer": (c_int, [c_void_p, c_void_p]),
     "stormck_pointer_level_device": (c_int, [c_void_p, c_uint64, c_uint64, c_uint64, c_uint8, c_uint32, c_void_p, c_void_p]),
     "stormck_pointer_node_device": (c_int, [c_void_p, c_void_p, c_uint32, c_uint32, c_void_p, c_void_p]),
     "stormck_pack_pointer_blocks_device": (

@@ -166,3 +166,23 @@ def ReadVerifyBatch(fd: int, addresses, lens, expected, dst, dst_stride: int, bl
     if rc != _lib.EMISMATCH:
         _lib.check(rc)
     return fb.value, nb.value
+
+
+def RegisterHostMemory(buf) -> None:
+    """Page-lock a long-lived host buffer (storm's cache.data, allocated once in
+    cache.New, cache/cache.go:36-40): host batches then DMA straight from it, and
+    HostDevicePointer gives kernels in-place access to it."""
+    a = _as_u8(buf)
+    _lib.check(_lib.lib.stormck_host_register(a.ctypes.data, a.nbytes))
+
+
+def UnregisterHostMemory(buf) -> None:
+    _lib.check(_lib.lib.stormck_host_unregister(_as_u8(buf).ctypes.data))
+
+
+def HostDevicePointer(buf) -> int:
+    """Device address of a registered host buffer (for the *_device entry points,
+    e.g. commit.commit_device on a host-resident arena)."""
+    d = ctypes.c_void_p()
+    _lib.check(_lib.lib.stormck_host_device_pointer(_as_u8(buf).ctypes.data, ctypes.byref(d)))
+    return int(d.value or 0)

@@ -377,7 +377,7 @@ __device__ __forceinline__ void wait_lgkm0() {
 #define STORMCK_GLDS_ISSUE(SRC, DST, T_, NK, ROW_, AUX_) do { } while (0)
 #endif
 
-template <int T, int R, int AUX, bool HASH = true, bool VERIFY = false, int WAVES = 4>
+template <int T, int R, int AUX, bool HASH = true, bool VERIFY = false, int WAVES = 4, bool SYNC = true>
 __global__ __launch_bounds__(64 * WAVES) void k_xxh64_glds(const uint8_t* __restrict__ base, uint64_t stride, uint32_t len,
                                                      uint64_t n, uint64_t* __restrict__ out,
                                                      const uint64_t* __restrict__ expected = nullptr,
@@ -390,6 +390,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_xxh64_glds(const uint8_t* __rest
     constexpr int PER_WAVE = INSTR / WAVES; // ... per wave
     static_assert(INSTR % WAVES == 0, "tile must split evenly over the waves");
     static_assert(R >= 2, "ring needs >= 2 slots");
+    static_assert(SYNC || T % 2 == 0, "without SYNC a wave's pieces must be its own block rows");
     __shared__ __attribute__((aligned(16))) uint8_t lds[R * TILE];
 
     const uint32_t tid = threadIdx.x;
@@ -425,7 +426,11 @@ __global__ __launch_bounds__(64 * WAVES) void k_xxh64_glds(const uint8_t* __rest
         // tile t landed (this wave's pieces), then every wave's pieces
         if (t + R - 2 < ntiles) wait_vmcnt<PER_WAVE * (R - 2)>();
         else wait_vmcnt<0>();
-        __builtin_amdgcn_s_barrier();
+        // A wave's pieces are exactly the rows of its own 16 blocks, so a wave only
+        // reads what it loaded. SYNC keeps the waves in step with a barrier; without
+        // it each wave only retires its own reads of tile t-1 before refilling.
+        if constexpr (SYNC) __builtin_amdgcn_s_barrier();
+        else wait_lgkm0();
         // all waves finished reading tile t-1: refill its slot with tile t+R-1
         if (t + R - 1 < ntiles)
             STORMCK_GLDS_ISSUE(src, lds + ((t + R - 1) % R) * TILE + wave * PER_WAVE * 1024, t + R - 1, PER_WAVE, ROW, AUX);

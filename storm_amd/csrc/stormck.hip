@@ -384,7 +384,9 @@ bool is_pinned(const void* p) {
 // feed PCIe Gen5; a few threads can.
 void par_copy(uint8_t* dst, const uint8_t* src, uint64_t bytes, uint64_t min_per_thread = 8ULL << 20) {
     ForkJoin& fj = ForkJoin::get();
-    const unsigned nt = static_cast<unsigned>(std::min<uint64_t>(fj.size(), std::max<uint64_t>(1, bytes / min_per_thread)));
+    // 8 copy threads saturate host memory bandwidth; more only contend with the HIP
+    // runtime's own threads for the box's cores
+    const unsigned nt = static_cast<unsigned>(std::min<uint64_t>({8, fj.size(), std::max<uint64_t>(1, bytes / min_per_thread)}));
     fj.run(nt, [&](unsigned t) {
         const uint64_t lo = bytes * t / nt, hi = bytes * (t + 1) / nt;
         std::memcpy(dst + lo, src + lo, hi - lo);
@@ -627,7 +629,15 @@ int stormck_host_register(void* p, uint64_t bytes) {
     if (!p || bytes == 0) return fail(STORMCK_EINVAL, "empty range");
     int rc = device_check();
     if (rc) return rc;
-    HIP_TRY(hipHostRegister(p, bytes, hipHostRegisterDefault));
+    HIP_TRY(hipHostRegister(p, bytes, hipHostRegisterMapped));
+    return STORMCK_OK;
+}
+
+int stormck_host_device_pointer(void* p, void** d_p) {
+    if (!p || !d_p) return fail(STORMCK_EINVAL, "null pointer");
+    int rc = device_check();
+    if (rc) return rc;
+    HIP_TRY(hipHostGetDevicePointer(d_p, p, 0));
     return STORMCK_OK;
 }
 

@@ -94,6 +94,7 @@ def test_argument_errors_precede_the_device_check():
                                                            1 << 22, (1 << 22) + 24, None)),
         ("fill stride", lambda: L.stormck_fill_synthetic_device(1 << 20, 24, 4, 0, 1, None)),
         ("register empty", lambda: L.stormck_host_register(None, 0)),
+        ("device pointer null", lambda: L.stormck_host_device_pointer(None, None)),
         ("key tags null", lambda: L.stormck_key_tags_device(None, 48, None, None, 48, 10, 1 << 20, None)),
         ("host null base", lambda: L.stormck_checksum_host(None, 32, None, 32, 4, ctypes.addressof(out))),
         ("read-verify slot", lambda: L.stormck_read_verify_fd(0, (ctypes.c_uint64 * 1)(0), (ctypes.c_uint32 * 1)(100),

@@ -149,6 +149,34 @@ def test_device_commit_streaming_level_mixed_lengths(dev):
 
 
 @pytest.mark.gpu
+def test_commit_on_registered_host_arena(dev):
+    """f1 on storm's cache.data where it lives: a registered host arena, reached in
+    place through stormck_host_device_pointer (kernels read blocks and write origins
+    over PCIe). Same result as the oracle's serial commit, byte for byte."""
+    from storm_amd import blocks as sb
+    rng = np.random.default_rng(77)
+    n, slot = 3000, 32768
+    lens = rng.choice([72, 28808, 30000, 31808, 32768], size=n)
+    b, size, last = sc.pointer_forest(n, lens, 1200, slot=slot, revision=6)
+    b["birth_revision"][::4] = 3
+    arena = np.zeros(size, dtype=np.uint8)
+    arena[slot:slot + n * slot] = rng.integers(0, 256, size=n * slot, dtype=np.uint8)
+    ref_arena, ref_b = arena.copy(), b.copy()
+    want_cs, want_last = o.commit(ref_arena, ref_b, 6, last)
+    sb.RegisterHostMemory(arena)
+    try:
+        d_arena = sb.HostDevicePointer(arena)
+        assert d_arena != 0
+        cs, last2 = sc.commit_device(d_arena, b, 6, last)
+        torch.cuda.synchronize()
+    finally:
+        sb.UnregisterHostMemory(arena)
+    assert np.array_equal(cs, want_cs) and last2 == want_last
+    assert np.array_equal(b["address"], ref_b["address"])
+    assert np.array_equal(arena, ref_arena)
+
+
+@pytest.mark.gpu
 @pytest.mark.slow
 def test_device_commit_1m_leaves_properties(dev):
     """1M dirty 32 KiB leaves + 835 pointer blocks (fan-out 1200), all in HBM: after the

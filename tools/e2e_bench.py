@@ -98,6 +98,32 @@ def main():
             res["read_verify_note"] = "parallel pread (16 threads) from page cache on a reader thread, 1 GiB ahead of the pipelined H2D + verify"
         finally:
             os.close(fd)
+    # f1 commit on a registered HOST arena (storm's cache.data in place, kernels over
+    # PCIe via stormck_host_device_pointer), and the zero-copy device-entry hash rate
+    from storm_amd import commit as sc
+    nl = 32768
+    bf, size, last = sc.pointer_forest(nl, BLOCK, 1200, slot=BLOCK, revision=1)
+    arena = np.zeros(size, dtype=np.uint8)
+    arena[BLOCK:BLOCK + nl * BLOCK] = host[:nl].reshape(-1) if nl <= n else 0
+    blocks.RegisterHostMemory(arena)
+    try:
+        d_arena = blocks.HostDevicePointer(arena)
+        sc.commit_device(d_arena, bf, 1, last)  # warm
+        t, (cs, _) = timed(lambda: sc.commit_device(d_arena, bf, 1, last))
+        res["commit_registered_host_arena_gib_s"] = round(int(bf["length"].sum()) / t / 2**30, 2)
+        res["commit_registered_host_arena_ms"] = round(t * 1e3, 2)
+        o1 = torch.empty(nl, dtype=torch.int64, device=dev)
+
+        def zc():
+            engine.checksum_device(d_arena + BLOCK, BLOCK, nl, o1.data_ptr(), BLOCK)
+            torch.cuda.synchronize()
+
+        t, _ = timed(zc)
+        res["zero_copy_device_entry_gib_s"] = round(nl * BLOCK / t / 2**30, 2)
+        assert np.array_equal(o1.cpu().numpy().view(np.uint64), want[:nl]), "zero-copy hash mismatch"
+        assert np.array_equal(cs[:nl], want[:nl]), "host-arena commit mismatch"
+    finally:
+        blocks.UnregisterHostMemory(arena)
     # single-call latency (blocks.Checksum on one buffer: <= 64 KiB is one launch that
     # reads pinned staging over PCIe and writes the checksum to pinned memory)
     for size in (0, 72, 4096, 30000, BLOCK, 65536):

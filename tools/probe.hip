@@ -151,14 +151,16 @@ int main(int argc, char** argv) {
     std::vector<V> vs;
     vs.push_back({"readpeak nt grid=16384", [&] { hipLaunchKernelGGL(k_readpeak<true>, dim3(16384), dim3(256), 0, 0, (const u64x2*)d, bytes / 16, sink); }, false});
     vs.push_back({"quad U=16", [&] { hipLaunchKernelGGL((k_xxh64_quad<16, false, false, false, false>), gq, dim3(256), 0, 0, d, L, nullptr, (uint32_t)L, nullptr, n, out, nullptr, nullptr, nullptr); }, true});
-#define GV(T, R, AUX) vs.push_back({"glds T=" #T " R=" #R " aux=" #AUX, [&] { hipLaunchKernelGGL((k_xxh64_glds<T, R, AUX>), gg, dim3(256), 0, 0, d, L, (uint32_t)L, n, out, nullptr, nullptr, nullptr); }, true})
-    GV(16, 3, 2); GV(24, 3, 2);
+    // glds<T, R, nt> with W waves per workgroup (16 blocks per wave); S = barrier-synchronised
+    // ring, N = per-wave ring (each wave waits only for its own pieces)
+#define GW(W, T, R, SY)                                                                                       \
+    vs.push_back({std::string("glds " #W "w T=" #T " R=" #R) + (SY ? " sync" : " nosync"), [&] {                              \
+        hipLaunchKernelGGL((k_xxh64_glds<T, R, 2, true, false, W, SY>), dim3((unsigned)((n + 16 * W - 1) / (16 * W))), \
+                           dim3(64 * W), 0, 0, d, L, (uint32_t)L, n, out, nullptr, nullptr, nullptr); }, true})
+    GW(8, 16, 2, true); GW(8, 16, 2, false); GW(8, 20, 2, false); GW(8, 12, 3, false);
+    GW(4, 16, 2, false); GW(4, 16, 4, false); GW(2, 16, 3, false); GW(2, 16, 4, false);
+    GW(1, 16, 2, false); GW(1, 16, 3, false); GW(1, 16, 4, false); GW(1, 32, 2, false);
     const dim3 g8((unsigned)((n + 127) / 128));
-#define GV8(T, R) vs.push_back({"glds8w T=" #T " R=" #R, [&] { hipLaunchKernelGGL((k_xxh64_glds<T, R, 2, true, false, 8>), g8, dim3(512), 0, 0, d, L, (uint32_t)L, n, out, nullptr, nullptr, nullptr); }, true})
-    GV8(16, 2); GV8(12, 3); GV8(20, 2); GV8(10, 3); GV8(14, 2); GV8(18, 2);
-    const dim3 g16((unsigned)((n + 255) / 256));
-#define GV16(T, R) vs.push_back({"glds16w T=" #T " R=" #R, [&] { hipLaunchKernelGGL((k_xxh64_glds<T, R, 2, true, false, 16>), g16, dim3(1024), 0, 0, d, L, (uint32_t)L, n, out, nullptr, nullptr, nullptr); }, true})
-    GV16(8, 2); GV16(6, 3); GV16(10, 2);
     vs.push_back({"glds8w T=16 R=2 noHash", [&] { hipLaunchKernelGGL((k_xxh64_glds<16, 2, 2, false, false, 8>), g8, dim3(512), 0, 0, d, L, (uint32_t)L, n, out, nullptr, nullptr, nullptr); }, false});
     std::vector<std::vector<double>> gbs(vs.size());
     for (int r = 0; r < rounds; ++r) {
