@@ -134,6 +134,55 @@ func RegisterHostMemory(b []byte) error {
 	return nil
 }
 
+// DirtyBlock mirrors stormck_dirty_block (include/stormck.h): one dirty block of
+// Cache.Commit's data phase, its blockMetadata plus its BlockOrigin as byte offsets into
+// the arena (cache.data), and the index of its parent record.
+type DirtyBlock struct {
+	DataOffset    uint64       // offset of the block in the arena
+	OriginPointer uint64       // offset of the parent's blocks.Pointer slot, or NoOrigin
+	OriginType    uint64       // offset of the parent's BlockType byte, or NoOrigin
+	Parent        int64        // index of the parent's record, or NoParent
+	Address       BlockAddress // in: current address; out: after relocation
+	BirthRevision uint64       // in/out, as commitBlock (cache/cache.go:114-118)
+	Length        uint32       // bytes hashed: unsafe.Sizeof of the block's type
+	Type          BlockType
+	_             [3]byte
+}
+
+const (
+	NoOrigin = ^uint64(0)
+	NoParent = int64(-1)
+)
+
+// compile-time check that DirtyBlock has the C layout (56 bytes)
+var _ = [1]struct{}{}[unsafe.Sizeof(DirtyBlock{})-56]
+
+// CommitBatch runs Cache.Commit's data phase (cache/cache.go:87-137, trace.go:274-320)
+// for every dirty block on the GPU, children first, level by level. The arena is
+// storm's cache.data, registered with RegisterHostMemory: kernels read the blocks and
+// store each {checksum, address, birth revision} and type into the parent's origin in
+// place. Relocations are written back into dirty; out[i] is dirty[i]'s checksum.
+func CommitBatch(arena []byte, dirty []DirtyBlock, revision uint64, lastAllocated *BlockAddress, out []Hash) error {
+	if len(dirty) == 0 {
+		return nil
+	}
+	if len(out) < len(dirty) {
+		return errors.New("CommitBatch: out too small")
+	}
+	var dArena unsafe.Pointer
+	if rc := C.stormck_host_device_pointer(bytesPtr(arena), &dArena); rc != C.STORMCK_OK {
+		return stormckError(rc)
+	}
+	la := C.uint64_t(*lastAllocated)
+	rc := C.stormck_commit_device(dArena, (*C.stormck_dirty_block)(unsafe.Pointer(&dirty[0])), C.uint64_t(len(dirty)),
+		C.uint64_t(revision), &la, (*C.uint64_t)(unsafe.Pointer(&out[0])), nil)
+	if rc != C.STORMCK_OK {
+		return stormckError(rc)
+	}
+	*lastAllocated = BlockAddress(la)
+	return nil
+}
+
 // UnregisterHostMemory undoes RegisterHostMemory.
 func UnregisterHostMemory(b []byte) error {
 	if rc := C.stormck_host_unregister(bytesPtr(b)); rc != C.STORMCK_OK {
