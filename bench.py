@@ -46,7 +46,7 @@ def parse():
     p.add_argument("--settle", type=float, default=1.0,
                    help="before the W warmup steps, run untimed steps for at least this many seconds so the "
                         "GPU clocks settle (short workloads otherwise time a ramping clock)")
-    p.add_argument("--workload", default="c3", choices=["c3", "commit", "keytags"],
+    p.add_argument("--workload", default="c3", choices=["c3", "commit", "keytags", "c5"],
                    help="c3 = BASELINE metric (default); commit = f1 level-synchronous Cache.Commit of a dirty "
                         "forest; keytags = f4 xxhash.Sum64 of 48-byte keys")
     p.add_argument("--commit-leaves", type=int, default=1 << 20)
@@ -171,6 +171,75 @@ def commit_workload(a):
     print(json.dumps(res), flush=True)
 
 
+def c5_workload(a):
+    """c5: the mixed batch of one storm commit in keystore/benchmark_test.go (SURVEY §8a
+    a6: ~1200 objectlist leaves of 31808 B + 1 pointer block of 30000 B + the 72 B
+    singularity), device-resident. One step = the batch checksum (per-block lengths)
+    AND the same batch committed as a forest through stormck_commit_device (host
+    planning, H2D of records, 2 level launches, D2H). Latency-bound by nature: one
+    32 KiB block is ~1000 serial XXH64 rounds per accumulator."""
+    import numpy as np
+    import torch
+    from storm_amd import commit as sc
+    from storm_amd import engine
+
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    n_ol = 1200
+    lens = np.array([31808] * n_ol + [30000, 72], dtype=np.uint32)
+    n = len(lens)
+    buf = torch.empty((n, BLOCK), dtype=torch.uint8, device=dev)
+    engine.fill_synthetic_device(buf.data_ptr(), BLOCK, n, 0, 0x53544F524D)
+    d_lens = torch.from_numpy(lens.view(np.int32)).to(dev)
+    out = torch.empty(n, dtype=torch.int64, device=dev)
+    st = torch.cuda.current_stream(dev).cuda_stream
+    # the commit form: 1200 objectlist leaves under one pointer block (fan-out 1200), rooted at the singularity
+    b0, size, last = sc.pointer_forest(n_ol, 31808, FANOUT, slot=BLOCK, revision=REV)
+    arena = torch.zeros(size, dtype=torch.uint8, device=dev)
+    engine.fill_synthetic_device(arena.data_ptr() + BLOCK, BLOCK, n_ol, 0, 0x53544F524D)
+
+    def batch():
+        engine.checksum_device(buf.data_ptr(), BLOCK, n, out.data_ptr(), 0, d_lens.data_ptr(), st)
+
+    settle(batch, a.settle)
+    for _ in range(a.warmup):
+        batch()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        batch()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    settle(lambda: sc.commit_device(arena.data_ptr(), b0, REV, last), a.settle)
+    tc = time.perf_counter()
+    for _ in range(a.steps):
+        cs, _ = sc.commit_device(arena.data_ptr(), b0, REV, last)
+    commit_us = (time.perf_counter() - tc) / a.steps * 1e6
+    hashed = int(lens.sum())
+    res = {"metric": "GiB/s mixed storm commit batch (c5), device-resident", "value": round(hashed * a.steps / el / 2**30, 2),
+           "unit": "GiB/s", "n_gpus": 1, "steps": a.steps, "warmup": a.warmup,
+           "ms_per_step": round(el / a.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
+           "vs_baseline": None, "dtype": "u64", "data": "synthetic",
+           "config": {"workload": "c5: 1200 x 31808 B objectlist + 1 x 30000 B pointer + 1 x 72 B singularity "
+                                  "(keystore/benchmark_test.go commit), per-block lengths", "blocks": n,
+                      "hashed_bytes": hashed},
+           "batch_us": round(el / a.steps * 1e6, 1),
+           "commit_forest_us": round(commit_us, 1),
+           "commit_root": "0x%016x" % int(cs[-1])}
+    if not a.no_cpu:
+        from oracle import oracle as o
+        host = buf.cpu().numpy()
+        reps, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < min(a.cpu_seconds, 5.0):
+            o.checksum_batch(host, n, BLOCK, 0, lens=lens)
+            reps += 1
+        el = time.perf_counter() - t0
+        res["cpu_baseline"] = {"value": round(reps * hashed / el / 2**30, 3), "unit": "GiB/s", "cores": 1, "kind": "port",
+                               "sample": f"the same {n}-block batch hashed {reps}x in {el:.1f} s by oracle/xxh64_oracle.c",
+                               "batch_us": round(el / reps * 1e6, 1)}
+    print(json.dumps(res), flush=True)
+
+
 def keytags_workload(a):
     """f4: one step = xxhash.Sum64 of 64M 48-byte keys resident in HBM (the key shape of
     keystore/benchmark_test.go:27-32), one lane per key (stormck_key_tags_device)."""
@@ -228,6 +297,8 @@ def main():
         return commit_workload(a)
     if a.workload == "keytags":
         return keytags_workload(a)
+    if a.workload == "c5":
+        return c5_workload(a)
     import numpy as np
     import torch
 
@@ -320,6 +391,16 @@ def main():
         if tj.get("arena_blocks") == arena_n and tj.get("kernel") == KERNEL:
             traffic = tj.get("hbm_bytes_per_launch")
 
+    read_peak = None
+    rpath = os.path.join(ROOT, "profiles", "read_peak.json")
+    if os.path.exists(rpath):
+        with open(rpath) as f:
+            rp = json.load(f)
+        # also report against a measured stream-read peak
+        read_peak = {"GB/s": rp["stream_read_GBps"], "frac": round(achieved / rp["stream_read_GBps"], 4),
+                     "kernel": rp["stream_read_kernel"], "grid_stride_read_GB/s": rp["grid_stride_read_GBps"],
+                     "source": rp["source"]}
+
     if rank == 0:
         root_t = engine.as_tuple(root)
         res = {
@@ -333,7 +414,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "kernel": KERNEL, "avg_launch_ms": round(avg_ms, 4),
-                         "algorithmic_bytes_per_launch": int(alg_bytes)},
+                         "algorithmic_bytes_per_launch": int(alg_bytes), "measured_read_peak": read_peak},
             "root": "0x%016x" % root_t[0],
         }
         if world == 1 and not a.no_cpu:
