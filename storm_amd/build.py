@@ -56,12 +56,20 @@ def build_oracle(force: bool = False) -> str:
     return out
 
 
+PROBES = ("probe", "probe_keys", "probe_small")  # tools/<name>.hip: design probes, not product
+
+
 def build_probe(force: bool = False) -> str:
-    out = os.path.join(ROOT, "tools", "probe")
-    srcs = [os.path.join(ROOT, "tools", "probe.hip"), os.path.join(CSRC, "kernels.h"), os.path.join(CSRC, "xxh64_dev.h")]
-    if force or not _newer(out, srcs):
-        subprocess.run([hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-o", out, srcs[0]], check=True)
-    return out
+    """Build the design probes (tools/probe*.hip) next to their sources."""
+    built = []
+    for name in PROBES:
+        out = os.path.join(ROOT, "tools", name)
+        srcs = [os.path.join(ROOT, "tools", name + ".hip"), os.path.join(CSRC, "kernels.h"),
+                os.path.join(CSRC, "xxh64_dev.h")]
+        if force or not _newer(out, srcs):
+            subprocess.run([hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-o", out, srcs[0]], check=True)
+        built.append(out)
+    return " ".join(built)
 
 
 if __name__ == "__main__":

@@ -134,6 +134,14 @@ def test_uniform_fast_path_lengths(dev, length):
         torch.cuda.synchronize()
         want = o.checksum_batch(host, n, stride, length)
         assert np.array_equal(_u64(out), want), (length, n)
+        if n == 65:  # verify through the one-workgroup-per-block kernel
+            exp = torch.from_numpy(want.view(np.int64).copy()).to(dev)
+            exp[64] ^= 1
+            exp[9] ^= 1
+            res = torch.zeros(2, dtype=torch.int64, device=dev)
+            engine.verify_device(_to_dev(host, dev).data_ptr(), stride, n, exp.data_ptr(), res.data_ptr(), length)
+            torch.cuda.synchronize()
+            assert _u64(res).tolist() == [9, 2], length
     # verify through the same path
     d = _to_dev(host, dev)
     exp = torch.from_numpy(want.view(np.int64).copy()).to(dev)
