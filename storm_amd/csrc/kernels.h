@@ -377,7 +377,7 @@ __device__ __forceinline__ void wait_lgkm0() {
 #define STORMCK_GLDS_ISSUE(SRC, DST, T_, NK, ROW_, AUX_) do { } while (0)
 #endif
 
-template <int T, int R, int AUX, bool HASH = true, bool VERIFY = false, int WAVES = 4, bool SYNC = true>
+template <int T, int R, int AUX, bool HASH = true, bool VERIFY = false, int WAVES = 4, bool SYNC = true, bool XCD = false>
 __global__ __launch_bounds__(64 * WAVES) void k_xxh64_glds(const uint8_t* __restrict__ base, uint64_t stride, uint32_t len,
                                                      uint64_t n, uint64_t* __restrict__ out,
                                                      const uint64_t* __restrict__ expected = nullptr,
@@ -395,7 +395,12 @@ __global__ __launch_bounds__(64 * WAVES) void k_xxh64_glds(const uint8_t* __rest
 
     const uint32_t tid = threadIdx.x;
     const uint32_t wave = tid >> 6, lane = tid & 63;
-    const uint64_t blk0 = static_cast<uint64_t>(blockIdx.x) * BPW;
+    uint32_t wg = blockIdx.x;
+    if constexpr (XCD) {
+        // workgroups are dealt round-robin to the 8 XCDs: give XCD x a contiguous range
+        if ((gridDim.x & 7) == 0) wg = (wg & 7) * (gridDim.x >> 3) + (wg >> 3);
+    }
+    const uint64_t blk0 = static_cast<uint64_t>(wg) * BPW;
     const uint32_t nst = len >> 5;
     const uint32_t ntiles = nst / T;
 

@@ -157,9 +157,13 @@ int main(int argc, char** argv) {
     vs.push_back({std::string("glds " #W "w T=" #T " R=" #R) + (SY ? " sync" : " nosync"), [&] {                              \
         hipLaunchKernelGGL((k_xxh64_glds<T, R, 2, true, false, W, SY>), dim3((unsigned)((n + 16 * W - 1) / (16 * W))), \
                            dim3(64 * W), 0, 0, d, L, (uint32_t)L, n, out, nullptr, nullptr, nullptr); }, true})
-    GW(8, 16, 2, true); GW(8, 16, 2, false); GW(8, 20, 2, false); GW(8, 12, 3, false);
-    GW(4, 16, 2, false); GW(4, 16, 4, false); GW(2, 16, 3, false); GW(2, 16, 4, false);
-    GW(1, 16, 2, false); GW(1, 16, 3, false); GW(1, 16, 4, false); GW(1, 32, 2, false);
+    GW(8, 16, 2, true); GW(8, 20, 2, true);
+    // cache-policy bits of the LDS-DMA loads (aux: 1 = sc0, 2 = nt, 16 = sc1) and the XCD remap
+#define GA(AUXV, XC)                                                                                           \
+    vs.push_back({std::string("glds 8w T=16 R=2 aux=" #AUXV) + (XC ? " xcd" : ""), [&] {                       \
+        hipLaunchKernelGGL((k_xxh64_glds<16, 2, AUXV, true, false, 8, true, XC>), dim3((unsigned)((n + 127) / 128)), \
+                           dim3(512), 0, 0, d, L, (uint32_t)L, n, out, nullptr, nullptr, nullptr); }, true})
+    GA(0, false); GA(3, false); GA(18, false); GA(16, false); GA(2, true);
     const dim3 g8((unsigned)((n + 127) / 128));
     vs.push_back({"glds8w T=16 R=2 noHash", [&] { hipLaunchKernelGGL((k_xxh64_glds<16, 2, 2, false, false, 8>), g8, dim3(512), 0, 0, d, L, (uint32_t)L, n, out, nullptr, nullptr, nullptr); }, false});
     std::vector<std::vector<double>> gbs(vs.size());
