@@ -42,13 +42,17 @@ def pointer_block_size(fanout: int) -> int:
 
 
 def commit_device(d_arena: int, blocks: np.ndarray, revision: int, last_allocated: int,
-                  stream: int = 0) -> Tuple[np.ndarray, int]:
+                  stream: int = 0, out: Optional[np.ndarray] = None) -> Tuple[np.ndarray, int]:
     """Commit the dirty forest (updates blocks' address/birth_revision in place).
-    Returns (checksums uint64[n], new last_allocated_block)."""
+    Returns (checksums uint64[n], new last_allocated_block). ``out`` (uint64[n]) may be
+    passed to reuse the checksum array across commits, as a long-lived caller would."""
     if blocks.dtype != DIRTY_DTYPE or not blocks.flags["C_CONTIGUOUS"]:
         raise ValueError("blocks must be a contiguous DIRTY_DTYPE array")
     n = blocks.shape[0]
-    out = np.zeros(n, dtype=np.uint64)
+    if out is None:
+        out = np.zeros(n, dtype=np.uint64)
+    elif out.dtype != np.uint64 or out.shape != (n,) or not out.flags["C_CONTIGUOUS"]:
+        raise ValueError("out must be a contiguous uint64 array of len(blocks)")
     la = ctypes.c_uint64(last_allocated)
     _lib.check(_lib.lib.stormck_commit_device(d_arena, blocks.ctypes.data if n else None, n, revision,
                                               ctypes.byref(la), out.ctypes.data if n else None, stream or None))

@@ -654,28 +654,24 @@ __global__ void k_set_root(const uint64_t* __restrict__ cs, uint64_t addr, uint6
 }
 
 // ---------------------------------------------------------------------------
-// f1: one level of a level-synchronous commit (order[0..cnt) = the caller's indices
-// of this level's blocks). Quad per dirty block: hash the
-// block's bytes (gather by data_offset, per-block length), then lane 0 performs
-// storm's PostCommitFunc (cache/trace.go:274-320): Pointer{cs, address,
-// birth_revision} into the parent's origin slot and the block type into the origin
-// type byte. Origins belong to blocks of later levels (parents), which this launch
-// never reads.
+// f1: one level of a level-synchronous commit. blocks[lo, lo + cnt) are this level's
+// dirty records in commit order (the host lays them out so; they may sit in pinned
+// host memory, read over PCIe). Quad per dirty block: hash the block's bytes (gather
+// by data_offset, per-block length), then lane 0 performs storm's PostCommitFunc
+// (cache/trace.go:274-320): Pointer{cs, address, birth_revision} into the parent's
+// origin slot and the block type into the origin type byte. Origins belong to blocks
+// of later levels (parents), which this launch never reads. out_cs[lo + k] = checksum.
 // ---------------------------------------------------------------------------
 template <int U>
 __global__ __launch_bounds__(256) void k_commit_level(uint8_t* __restrict__ arena,
-                                                       const stormck_dirty_block* __restrict__ blocks,
-                                                       const uint32_t* __restrict__ order, uint64_t lo,
+                                                       const stormck_dirty_block* __restrict__ blocks, uint64_t lo,
                                                        uint64_t cnt, uint64_t* __restrict__ out_cs) {
     const uint64_t gtid = static_cast<uint64_t>(blockIdx.x) * 256 + threadIdx.x;
     const uint64_t k = gtid >> 2;
     const uint32_t j = threadIdx.x & 3;
     const bool live = k < cnt;
     const uint64_t kk = live ? k : cnt - 1;
-    // caller's index of this level's k-th block (identity when the caller's array is
-    // already children-first); checksums are written in commit order (lo + k)
-    const uint64_t idx = order ? order[kk] : lo + kk;
-    const stormck_dirty_block b = blocks[idx];
+    const stormck_dirty_block b = blocks[lo + kk];
     const uint8_t* src = arena + b.data_offset;
     const uint32_t L = b.length;
     const uint32_t nst = L >> 5;
@@ -701,7 +697,9 @@ __global__ __launch_bounds__(256) void k_commit_level(uint8_t* __restrict__ aren
 
 // ---------------------------------------------------------------------------
 // f1 fast path: one commit level through the LDS-DMA ring (the k_xxh64_glds scheme
-// with a ring of 2 tiles) for arenas whose block offsets are 16-byte aligned. Blocks
+// with a ring of 2 tiles) for arenas whose block offsets are 16-byte aligned. The
+// workgroup's 128 records (7 KiB, possibly in host memory) are first copied into LDS
+// with 8-byte loads spread over all threads, so each record crosses the bus once. Blocks
 // of a workgroup may differ in length: block b streams floor(nst_b / T) whole tiles,
 // the workgroup runs the longest block's tile count, and LDS-DMA lanes of blocks that
 // have run out of tiles are switched off (exec mask). With a 2-slot ring every tile
@@ -712,63 +710,63 @@ __global__ __launch_bounds__(256) void k_commit_level(uint8_t* __restrict__ aren
 template <int T, int AUX, int WAVES>
 __global__ __launch_bounds__(64 * WAVES) void k_commit_level_glds(uint8_t* __restrict__ arena,
                                                                    const stormck_dirty_block* __restrict__ blocks,
-                                                                   const uint32_t* __restrict__ order, uint64_t lo,
-                                                                   uint64_t cnt, uint64_t* __restrict__ out_cs) {
+                                                                   uint64_t lo, uint64_t cnt,
+                                                                   uint64_t* __restrict__ out_cs) {
     constexpr int R = 2;
     constexpr int BPW = 16 * WAVES;
     constexpr int ROW = 32 * T;
     constexpr int TILE = BPW * ROW;
     constexpr int INSTR = TILE / 1024;
     constexpr int PER_WAVE = INSTR / WAVES;
+    constexpr int RW = sizeof(stormck_dirty_block) / 8;  // 7 words per record
     static_assert(INSTR % WAVES == 0, "tile must split evenly over the waves");
     __shared__ __attribute__((aligned(16))) uint8_t lds[R * TILE];
+    // the records sit in ring slot 1 until the first tile is issued into it. (A second
+    // __shared__ array makes hipcc guard every ds_read after an LDS-DMA with vmcnt(0),
+    // which serialises the ring: 12% slower, measured.)
+    uint64_t* rec_lds = reinterpret_cast<uint64_t*>(lds + TILE);
+    static_assert(BPW * RW * 8 <= TILE, "records fit in one ring slot");
 
     const uint32_t tid = threadIdx.x;
     const uint32_t wave = tid >> 6, lane = tid & 63;
     const uint64_t k0 = static_cast<uint64_t>(blockIdx.x) * BPW;  // first level-local block of this workgroup
+    const uint32_t nrec = static_cast<uint32_t>(min<uint64_t>(BPW, cnt - k0));
+    {
+        const uint64_t* src = reinterpret_cast<const uint64_t*>(blocks + lo + k0);
+        uint64_t w[(BPW * RW + 64 * WAVES - 1) / (64 * WAVES)];
+#pragma unroll
+        for (int m = 0; m < (BPW * RW + 64 * WAVES - 1) / (64 * WAVES); ++m) {
+            const uint32_t q = tid + m * 64 * WAVES;
+            w[m] = q < nrec * RW ? src[q] : 0;
+        }
+#pragma unroll
+        for (int m = 0; m < (BPW * RW + 64 * WAVES - 1) / (64 * WAVES); ++m) {
+            const uint32_t q = tid + m * 64 * WAVES;
+            if (q < BPW * RW) rec_lds[q] = w[m];
+        }
+    }
+    __syncthreads();
+    const stormck_dirty_block* recs = reinterpret_cast<const stormck_dirty_block*>(rec_lds);
 
-    // per-lane LDS-DMA sources: block of each of this wave's PER_WAVE pieces. Loads are
-    // batched (all indices, then all record fields) and branch-free so they overlap.
+    // per-lane LDS-DMA sources: block of each of this wave's PER_WAVE pieces
     const uint8_t* src[PER_WAVE];
     uint32_t ntl[PER_WAVE];
-    uint64_t ridx[PER_WAVE];
-    uint32_t piece[PER_WAVE];
-    bool plive[PER_WAVE];
 #pragma unroll
     for (int k = 0; k < PER_WAVE; ++k) {
         const uint32_t ii = wave * PER_WAVE + k;
         const uint32_t off = ii * 1024 + lane * 16;
         const uint32_t bb = off / ROW, q = (off % ROW) / 16;
-        piece[k] = (q + glds_rot<T>(bb)) % (2 * T);
-        const uint64_t kk = k0 + bb;
-        plive[k] = kk < cnt;
-        ridx[k] = plive[k] ? kk : cnt - 1;
-    }
-    if (order) {
-#pragma unroll
-        for (int k = 0; k < PER_WAVE; ++k) ridx[k] = order[ridx[k]];
-    } else {
-#pragma unroll
-        for (int k = 0; k < PER_WAVE; ++k) ridx[k] += lo;
-    }
-    uint64_t doff[PER_WAVE];
-    uint32_t dlen[PER_WAVE];
-#pragma unroll
-    for (int k = 0; k < PER_WAVE; ++k) {
-        doff[k] = blocks[ridx[k]].data_offset;
-        dlen[k] = blocks[ridx[k]].length;
-    }
-#pragma unroll
-    for (int k = 0; k < PER_WAVE; ++k) {
-        src[k] = arena + doff[k] + piece[k] * 16;
-        ntl[k] = plive[k] ? (dlen[k] >> 5) / T : 0;
+        const uint32_t piece = (q + glds_rot<T>(bb)) % (2 * T);
+        const bool plive = bb < nrec;
+        const stormck_dirty_block& r = recs[plive ? bb : 0];
+        src[k] = arena + r.data_offset + piece * 16;
+        ntl[k] = plive ? (r.length >> 5) / T : 0;
     }
     // this lane's hash block (quad) and the workgroup's tile count
     const uint32_t b = tid >> 2, j = tid & 3;
     const uint64_t kb = k0 + b;
-    const bool live = kb < cnt;
-    const uint64_t idx = order ? order[live ? kb : cnt - 1] : lo + (live ? kb : cnt - 1);
-    const stormck_dirty_block rec = blocks[idx];
+    const bool live = b < nrec;
+    const stormck_dirty_block rec = recs[live ? b : 0];
     const uint32_t L = rec.length, nst = L >> 5;
     const uint32_t my_tiles = live ? nst / T : 0;
     uint32_t wg_tiles = my_tiles;

@@ -288,12 +288,11 @@ struct DeviceCtx {
     int device = -1;
     bool ready = false;
     Stage st[kStages];
-    void* commit_scratch = nullptr;  // f1: dirty records + checksums + commit order
-    uint64_t commit_scratch_bytes = 0;
-    // f1 record uploads: their own stream, so the H2D of chunk k+1 runs while the
-    // caller's stream hashes chunk k; up_ev[s] marks the last DMA out of st[s].pinned
-    hipStream_t copy_stream = nullptr;
-    hipEvent_t up_ev[kStages] = {};
+    // f1: the dirty records (commit order) and their checksums in coherent pinned host
+    // memory, which the level kernels read and write in place over PCIe (zero-copy)
+    stormck_dirty_block* commit_rec = nullptr;
+    uint64_t* commit_cs = nullptr;
+    uint64_t commit_n = 0;
 };
 
 std::mutex g_ctx_mu;
@@ -327,17 +326,12 @@ int ensure_ready(DeviceCtx* c) {
         HIP_TRY(hipMalloc(&s.d_result, 16));
         HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&s.h_result), 16, hipHostMallocDefault));
     }
-    HIP_TRY(hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
-    for (hipEvent_t& e : c->up_ev) {
-        HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-        HIP_TRY(hipEventRecord(e, c->copy_stream));  // recorded once, so a wait on it is always valid
-    }
     c->ready = true;
     return STORMCK_OK;
 }
 
 void release_ctx(DeviceCtx* c) {
-    if (!c || (!c->ready && !c->commit_scratch)) return;
+    if (!c || (!c->ready && !c->commit_rec)) return;
     int prev = 0;
     (void)hipGetDevice(&prev);
     (void)hipSetDevice(c->device);
@@ -355,19 +349,12 @@ void release_ctx(DeviceCtx* c) {
         if (s.stream) (void)hipStreamDestroy(s.stream);
         s = Stage();
     }
-    if (c->copy_stream) {
-        (void)hipStreamSynchronize(c->copy_stream);
-        (void)hipStreamDestroy(c->copy_stream);
-        c->copy_stream = nullptr;
-    }
-    for (hipEvent_t& e : c->up_ev) {
-        if (e) (void)hipEventDestroy(e);
-        e = nullptr;
-    }
     c->ready = false;
-    if (c->commit_scratch) (void)hipFree(c->commit_scratch);
-    c->commit_scratch = nullptr;
-    c->commit_scratch_bytes = 0;
+    if (c->commit_rec) (void)hipHostFree(c->commit_rec);
+    if (c->commit_cs) (void)hipHostFree(c->commit_cs);
+    c->commit_rec = nullptr;
+    c->commit_cs = nullptr;
+    c->commit_n = 0;
     (void)hipSetDevice(prev);
 }
 
@@ -914,28 +901,31 @@ int stormck_commit_device(void* d_arena, stormck_dirty_block* blocks, uint64_t n
     const unsigned nt = static_cast<unsigned>(std::min<uint64_t>(fj.size(), n / 16384 + 1));
     // fn(t, lo, hi) on nt pool threads over contiguous ranges of [0, n)
     auto par = [&](auto&& fn) { fj.run(nt, [&](unsigned t) { fn(t, n * t / nt, n * (t + 1) / nt); }); };
-    // Pass 1: validate, and raise every ancestor's height to >= its distance above each
-    // block (atomic max; a walk stops at the first ancestor some walk has already raised
-    // high enough, which then carries the raise further up).
+    // Pass 1 (the only pass before the first launch): validate, and raise every
+    // ancestor's height to >= its distance above each block (atomic max; a walk stops at
+    // the first ancestor some walk has already raised high enough, which then carries
+    // the raise further up). The first raise of a block from 0 marks it as an upper
+    // block; their count and smallest index tell whether level 0 (the blocks without
+    // dirty children) is a prefix of the caller's array.
     std::unique_ptr<uint32_t, void (*)(void*)> height_mem(static_cast<uint32_t*>(std::calloc(n, 4)), std::free);
     if (!height_mem) return fail(STORMCK_ENOMEM, "commit: height array");
     uint32_t* height = height_mem.get();
     std::atomic<int> bad{0};  // 1 parent range, 2 origin alignment, 3 cycle
-    std::atomic<uint64_t> relocating_n{0};
+    std::atomic<uint64_t> relocating_n{0}, upper_n{0}, upper_min{n};
     std::atomic<bool> misaligned{(reinterpret_cast<uintptr_t>(d_arena) & 15) != 0};
     par([&](unsigned, uint64_t lo, uint64_t hi) {
-        uint64_t reloc = 0;
+        uint64_t reloc = 0, up = 0, up_min = n;
         bool mis = false;
         for (uint64_t i = lo; i < hi && !bad.load(std::memory_order_relaxed); ++i) {
             const stormck_dirty_block& b = blocks[i];
             mis |= (b.data_offset & 15) != 0;
             if (b.parent != STORMCK_NO_PARENT && (b.parent < 0 || static_cast<uint64_t>(b.parent) >= n)) {
                 bad.store(1);
-                return;
+                break;
             }
             if (b.origin_pointer != STORMCK_NO_ORIGIN && ((b.origin_pointer & 7) != 0)) {
                 bad.store(2);
-                return;
+                break;
             }
             reloc += b.birth_revision <= revision;
             uint64_t cur = i;
@@ -944,75 +934,41 @@ int stormck_commit_device(void* d_arena, stormck_dirty_block* blocks, uint64_t n
                 const uint64_t p = static_cast<uint64_t>(blocks[cur].parent);
                 if (p >= n) {
                     bad.store(1);
-                    return;
+                    break;
                 }
                 ++hh;
                 if (hh > n) {
                     bad.store(3);
-                    return;
+                    break;
                 }
                 uint32_t old = __atomic_load_n(&height[p], __ATOMIC_RELAXED);
                 while (old < hh &&
                        !__atomic_compare_exchange_n(&height[p], &old, hh, true, __ATOMIC_RELAXED, __ATOMIC_RELAXED)) {
                 }
                 if (old >= hh) break;  // another walk holds p at >= hh and carries it upward
+                if (old == 0) {        // this walk raised p first
+                    ++up;
+                    up_min = std::min(up_min, p);
+                }
                 cur = p;
             }
         }
         relocating_n.fetch_add(reloc, std::memory_order_relaxed);
+        upper_n.fetch_add(up, std::memory_order_relaxed);
+        uint64_t m = upper_min.load(std::memory_order_relaxed);
+        while (up_min < m && !upper_min.compare_exchange_weak(m, up_min, std::memory_order_relaxed)) {
+        }
         if (mis) misaligned.store(true, std::memory_order_relaxed);
     });
     if (bad.load() == 1) return fail(STORMCK_EINVAL, "parent index out of range");
     if (bad.load() == 2) return fail(STORMCK_EINVAL, "origin_pointer must be 8-byte aligned (Go blocks.Pointer alignment)");
     if (bad.load() == 3) return fail(STORMCK_EINVAL, "parent links form a cycle");
     const uint64_t relocating = relocating_n.load();
+    const uint64_t nu = upper_n.load(), n0 = n - nu;
+    if (n0 == 0) return fail(STORMCK_EINVAL, "parent links form a cycle");  // every block has a dirty child
+    const bool prefix0 = nu == 0 || upper_min.load() == n0;
     const bool aligned16 = !misaligned.load();
     pt.mark("heights");
-    // Pass 2: per-range height histograms -> level_start, and whether the caller's array
-    // is already children-first. Otherwise a stable counting sort by height gives the
-    // commit order (index order within a level).
-    struct Part {
-        uint32_t max_h = 0;
-        bool sorted = true;
-        std::vector<uint64_t> hist;
-    };
-    std::vector<Part> part(nt);
-    par([&](unsigned t, uint64_t lo, uint64_t hi) {
-        Part& P = part[t];
-        P.hist.assign(8, 0);
-        uint32_t prev = lo ? height[lo - 1] : 0;
-        for (uint64_t i = lo; i < hi; ++i) {
-            const uint32_t hi_ = height[i];
-            P.sorted &= hi_ >= prev;
-            prev = hi_;
-            if (hi_ >= P.hist.size()) P.hist.resize(static_cast<size_t>(hi_) + 1, 0);
-            P.hist[hi_]++;
-            P.max_h = std::max(P.max_h, hi_);
-        }
-    });
-    uint32_t max_h = 0;
-    bool sorted = true;
-    for (const Part& P : part) {
-        max_h = std::max(max_h, P.max_h);
-        sorted &= P.sorted;
-    }
-    std::vector<uint64_t> level_start(static_cast<size_t>(max_h) + 2, 0);
-    for (const Part& P : part)
-        for (size_t l = 0; l < P.hist.size(); ++l) level_start[l + 1] += P.hist[l];
-    for (uint32_t l = 0; l <= max_h; ++l) level_start[l + 1] += level_start[l];
-    std::vector<uint32_t> order;
-    if (!sorted) {
-        order.resize(n);
-        std::vector<std::vector<uint64_t>> pos(nt, std::vector<uint64_t>(level_start.begin(), level_start.end() - 1));
-        for (unsigned t = 1; t < nt; ++t)
-            for (size_t l = 0; l <= max_h; ++l)
-                pos[t][l] = pos[t - 1][l] + (l < part[t - 1].hist.size() ? part[t - 1].hist[l] : 0);
-        par([&](unsigned t, uint64_t lo, uint64_t hi) {
-            std::vector<uint64_t>& ps = pos[t];
-            for (uint64_t i = lo; i < hi; ++i) order[ps[height[i]]++] = static_cast<uint32_t>(i);
-        });
-    }
-    pt.mark("order");
 
     // device resources before the records are touched: a failure here leaves them as given
     DeviceCtx* c = nullptr;
@@ -1021,132 +977,231 @@ int stormck_commit_device(void* d_arena, stormck_dirty_block* blocks, uint64_t n
     std::lock_guard<std::mutex> g(c->mu);
     rc = ensure_ready(c);
     if (rc) return rc;
-    const uint64_t need = n * sizeof(stormck_dirty_block) + n * 8 + (sorted ? 0 : n * 4);
-    if (c->commit_scratch_bytes < need) {
-        if (c->commit_scratch) (void)hipFree(c->commit_scratch);
-        c->commit_scratch = nullptr;
-        c->commit_scratch_bytes = 0;
-        HIP_TRY(hipMalloc(&c->commit_scratch, need));
-        c->commit_scratch_bytes = need;
+    if (c->commit_n < n) {
+        if (c->commit_rec) (void)hipHostFree(c->commit_rec);
+        if (c->commit_cs) (void)hipHostFree(c->commit_cs);
+        c->commit_rec = nullptr;
+        c->commit_cs = nullptr;
+        c->commit_n = 0;
+        HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&c->commit_rec), n * sizeof(stormck_dirty_block),
+                              hipHostMallocCoherent));
+        HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&c->commit_cs), n * 8, hipHostMallocCoherent));
+        c->commit_n = n;
     }
+    stormck_dirty_block* d_blocks = nullptr;
+    uint64_t* d_cs = nullptr;
+    HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(&d_blocks), c->commit_rec, 0));
+    HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(&d_cs), c->commit_cs, 0));
     pt.mark("ctx");
 
-    // relocation in commit order (cache/cache.go:114-118), in place like commitBlock:
-    // the k-th relocating block in commit order gets address last + k
-    uint64_t last = *last_allocated_block;
-    if (relocating) {
-        auto at = [&](uint64_t k) -> stormck_dirty_block& { return blocks[sorted ? k : order[k]]; };
-        std::vector<uint64_t> cnt(nt + 1, 0);
+    // Commit order: level 0 in index order, then the upper levels by height (index order
+    // within a height). `order` (commit position -> caller's index) is materialised only
+    // when it is not the identity. Level 0's part is all the first launch needs; the
+    // upper part is built while level 0 hashes.
+    std::vector<uint32_t> order;
+    std::vector<uint32_t> upper;  // upper blocks in index order (when level 0 is not a prefix)
+    if (!prefix0) {
+        order.resize(n);
+        upper.resize(nu);
+        std::vector<uint64_t> z(nt + 1, 0);
         par([&](unsigned t, uint64_t lo, uint64_t hi) {
             uint64_t m = 0;
-            for (uint64_t k = lo; k < hi; ++k) m += at(k).birth_revision <= revision;
-            cnt[t + 1] = m;
+            for (uint64_t i = lo; i < hi; ++i) m += height[i] == 0;
+            z[t + 1] = m;
         });
-        for (unsigned t = 0; t < nt; ++t) cnt[t + 1] += cnt[t];
+        for (unsigned t = 0; t < nt; ++t) z[t + 1] += z[t];
         par([&](unsigned t, uint64_t lo, uint64_t hi) {
-            uint64_t a = last + cnt[t];
-            for (uint64_t k = lo; k < hi; ++k) {
-                stormck_dirty_block& b = at(k);
-                if (b.birth_revision <= revision) {
-                    b.address = ++a;
-                    b.birth_revision = revision + 1;
-                }
+            uint64_t a = z[t], u = lo - z[t];
+            for (uint64_t i = lo; i < hi; ++i) {
+                if (height[i] == 0) order[a++] = static_cast<uint32_t>(i);
+                else upper[u++] = static_cast<uint32_t>(i);
             }
         });
-        last += relocating;
+        pt.mark("order0");
     }
-    *last_allocated_block = last;
-    pt.mark("relocate");
+    auto idx_at = [&](uint64_t k) -> uint64_t { return order.empty() ? k : order[k]; };
 
-    auto* d_blocks = static_cast<stormck_dirty_block*>(c->commit_scratch);
-    auto* d_cs = reinterpret_cast<uint64_t*>(d_blocks + n);
-    auto* d_order = sorted ? nullptr : reinterpret_cast<uint32_t*>(d_cs + n);
     hipStream_t st = static_cast<hipStream_t>(stream);
     auto launch_level = [&](uint64_t lo, uint64_t cnt) -> int {
-        const uint32_t* lvl_order = sorted ? nullptr : d_order + lo;
         if (aligned16 && cnt >= kStreamBatch) {
             // LDS-DMA ring, 8 waves x 128 blocks per workgroup (as the uniform fast path)
             const uint64_t wgs = (cnt + kGldsBlocks - 1) / kGldsBlocks;
             if (wgs > 0x7fffffffULL) return fail(STORMCK_EINVAL, "level too large");
             hipLaunchKernelGGL((k_commit_level_glds<kTileStripes, kAuxNT, kGldsWaves>), dim3(static_cast<unsigned>(wgs)),
-                               dim3(kGldsThreads), 0, st, static_cast<uint8_t*>(d_arena), d_blocks, lvl_order, lo, cnt,
-                               d_cs);
+                               dim3(kGldsThreads), 0, st, static_cast<uint8_t*>(d_arena), d_blocks, lo, cnt, d_cs);
         } else {
             dim3 grid;
             if (!grid_for(cnt * 4, &grid)) return fail(STORMCK_EINVAL, "level too large");
             hipLaunchKernelGGL(k_commit_level<kU>, grid, dim3(kThreads), 0, st, static_cast<uint8_t*>(d_arena), d_blocks,
-                               lvl_order, lo, cnt, d_cs);
+                               lo, cnt, d_cs);
         }
         HIP_TRY(hipGetLastError());
         return STORMCK_OK;
     };
-    // Host records go up through the context's two pinned buffers on the copy stream;
-    // the caller's stream waits only for the bytes its next launch reads, so the copy of
-    // chunk k+1 (host memcpy into pinned, then DMA) overlaps the hashing of chunk k.
-    unsigned ring = 0;
-    auto stage_up = [&](void* d_dst, const void* h_src, uint64_t bytes) -> int {
-        const uint8_t* src = static_cast<const uint8_t*>(h_src);
-        uint8_t* dst = static_cast<uint8_t*>(d_dst);
-        hipEvent_t ev = nullptr;
-        while (bytes) {
-            const uint64_t b = std::min<uint64_t>(bytes, kChunkBytes);
-            const unsigned r = ring;
-            ring = (ring + 1) % kStages;
-            HIP_TRY(hipEventSynchronize(c->up_ev[r]));  // the DMA that last read this buffer is done
-            par_copy(c->st[r].pinned, src, b, 1ULL << 20);
-            HIP_TRY(hipMemcpyAsync(dst, c->st[r].pinned, b, hipMemcpyHostToDevice, c->copy_stream));
-            HIP_TRY(hipEventRecord(c->up_ev[r], c->copy_stream));
-            ev = c->up_ev[r];
-            src += b;
-            dst += b;
-            bytes -= b;
+    // Records are copied in commit order into the context's coherent pinned buffer,
+    // which the level kernels read over PCIe (56 B per block beside its ~32 KiB of HBM
+    // reads; no DMA command, so nothing queues behind or between the hashing launches).
+    // Relocation (cache/cache.go:114-118: the k-th relocating block in commit order gets
+    // address last + k) is applied to the caller's record as it is copied. Each launch
+    // writes its checksums into pinned memory too; `back` lists the launches, so the
+    // host moves a launch's checksums to the caller's order while later ones run.
+    uint64_t last = *last_allocated_block;
+    auto stage_records = [&](uint64_t a, uint64_t b) {
+        const uint64_t cnt = b - a;
+        stormck_dirty_block* dst = c->commit_rec + a;
+        const unsigned tn = static_cast<unsigned>(std::min<uint64_t>({8, fj.size(), cnt / 8192 + 1}));
+        if (!relocating && order.empty()) {
+            par_copy(reinterpret_cast<uint8_t*>(dst), reinterpret_cast<const uint8_t*>(blocks + a),
+                     cnt * sizeof(stormck_dirty_block), 1ULL << 20);
+            return;
         }
-        if (ev) HIP_TRY(hipStreamWaitEvent(st, ev, 0));
+        std::vector<uint64_t> rc_(tn + 1, 0);
+        if (relocating) {
+            fj.run(tn, [&](unsigned t) {
+                uint64_t m = 0;
+                for (uint64_t k = a + cnt * t / tn, e = a + cnt * (t + 1) / tn; k < e; ++k)
+                    m += blocks[idx_at(k)].birth_revision <= revision;
+                rc_[t + 1] = m;
+            });
+            for (unsigned t = 0; t < tn; ++t) rc_[t + 1] += rc_[t];
+        }
+        fj.run(tn, [&](unsigned t) {
+            uint64_t addr = last + rc_[t];
+            for (uint64_t k = a + cnt * t / tn, e = a + cnt * (t + 1) / tn; k < e; ++k) {
+                stormck_dirty_block& rec = blocks[idx_at(k)];
+                if (relocating && rec.birth_revision <= revision) {
+                    rec.address = ++addr;
+                    rec.birth_revision = revision + 1;
+                }
+                dst[k - a] = rec;
+            }
+        });
+        last += rc_[tn];
+    };
+    struct Back {
+        uint64_t lo, cnt;
+        hipEvent_t hashed;
+    };
+    std::vector<Back> back;
+    auto send_back = [&](uint64_t lo, uint64_t cnt) -> int {
+        back.push_back({lo, cnt, nullptr});
+        HIP_TRY(hipEventCreateWithFlags(&back.back().hashed, hipEventDisableTiming));
+        HIP_TRY(hipEventRecord(back.back().hashed, st));
         return STORMCK_OK;
     };
-    uint32_t first_level = 0;
-    if (sorted) {
-        // Records already children-first: level 0 is records [0, level_start[1]); upload
-        // and hash it in chunks, then upload the rest for the upper levels.
-        const uint64_t l0 = level_start[1];
-        const uint64_t chunk = std::max<uint64_t>(32768, (l0 + 7) / 8);
-        for (uint64_t lo = 0; lo < l0; lo += chunk) {
-            const uint64_t cnt = std::min(chunk, l0 - lo);
-            rc = stage_up(d_blocks + lo, blocks + lo, cnt * sizeof(stormck_dirty_block));
-            if (rc) return rc;
-            rc = launch_level(lo, cnt);
-            if (rc) return rc;
+    auto run = [&]() -> int {
+        // Level 0 in growing chunks: a first chunk of 2 x kStreamBatch blocks (one LDS-DMA
+        // workgroup per CU) starts the device after a small upload; each next chunk is 3x
+        // the previous, small enough that its records (56 B per block over PCIe) arrive
+        // before the previous chunk's blocks (~32 KiB each at HBM rate) are hashed.
+        uint64_t next = 2 * kStreamBatch;
+        for (uint64_t lo = 0; lo < n0;) {
+            uint64_t cnt = std::min(next, n0 - lo);
+            if (n0 - lo - cnt < kStreamBatch) cnt = n0 - lo;  // no runt last chunk
+            stage_records(lo, lo + cnt);
+            int e = launch_level(lo, cnt);
+            if (e) return e;
+            e = send_back(lo, cnt);
+            if (e) return e;
+            lo += cnt;
+            next = cnt * 3;
         }
-        if (n > l0) {
-            rc = stage_up(d_blocks + l0, blocks + l0, (n - l0) * sizeof(stormck_dirty_block));
-            if (rc) return rc;
-        }
-        first_level = 1;
-    } else {
-        rc = stage_up(d_blocks, blocks, n * sizeof(stormck_dirty_block));
-        if (rc) return rc;
-        rc = stage_up(d_order, order.data(), n * 4);
-        if (rc) return rc;
-    }
-    pt.mark("upload_issue");
-    for (uint32_t l = first_level; l <= max_h; ++l) {
-        const uint64_t lo = level_start[l], cnt = level_start[l + 1] - lo;
-        if (cnt == 0) continue;
-        rc = launch_level(lo, cnt);
-        if (rc) return rc;
-    }
-    HIP_TRY(hipMemcpyAsync(out_checksums, d_cs, n * 8, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipStreamSynchronize(st));
-    pt.mark("device");
-    if (!sorted) {
-        // d_cs is in commit order; put it back in the caller's order
-        std::vector<uint64_t> tmp(out_checksums, out_checksums + n);
-        par([&](unsigned, uint64_t lo, uint64_t hi) {
-            for (uint64_t k = lo; k < hi; ++k) out_checksums[order[k]] = tmp[k];
+        pt.mark("level0_issue");
+        if (nu == 0) return STORMCK_OK;
+        // Upper levels, planned while level 0 hashes: a stable counting sort by height of
+        // the upper blocks (index order within a height) unless already in that order.
+        auto uidx = [&](uint64_t u) -> uint32_t { return upper.empty() ? static_cast<uint32_t>(n0 + u) : upper[u]; };
+        const unsigned un = static_cast<unsigned>(std::min<uint64_t>(fj.size(), nu / 16384 + 1));
+        struct Part {
+            uint32_t max_h = 0;
+            bool sorted = true;
+            std::vector<uint64_t> hist;
+        };
+        std::vector<Part> part(un);
+        fj.run(un, [&](unsigned t) {
+            Part& P = part[t];
+            P.hist.assign(8, 0);
+            const uint64_t lo = nu * t / un, hi = nu * (t + 1) / un;
+            uint32_t prev = lo ? height[uidx(lo - 1)] : 0;
+            for (uint64_t u = lo; u < hi; ++u) {
+                const uint32_t h = height[uidx(u)];
+                P.sorted &= h >= prev;
+                prev = h;
+                if (h >= P.hist.size()) P.hist.resize(static_cast<size_t>(h) + 1, 0);
+                P.hist[h]++;
+                P.max_h = std::max(P.max_h, h);
+            }
         });
-        pt.mark("unpermute");
+        uint32_t max_h = 0;
+        bool sorted = true;
+        for (const Part& P : part) {
+            max_h = std::max(max_h, P.max_h);
+            sorted &= P.sorted;
+        }
+        // level_start[h] = commit position of height h's first block (h >= 1)
+        std::vector<uint64_t> level_start(static_cast<size_t>(max_h) + 2, 0);
+        for (const Part& P : part)
+            for (size_t l = 1; l < P.hist.size(); ++l) level_start[l + 1] += P.hist[l];
+        level_start[1] = n0;
+        for (uint32_t l = 1; l <= max_h; ++l) level_start[l + 1] += level_start[l];
+        if (!sorted || !upper.empty()) {
+            if (order.empty()) {
+                order.resize(n);
+                for (uint64_t k = 0; k < n0; ++k) order[k] = static_cast<uint32_t>(k);
+            }
+            if (sorted) {
+                std::memcpy(order.data() + n0, upper.data(), nu * 4);
+            } else {
+                std::vector<std::vector<uint64_t>> pos(un, std::vector<uint64_t>(level_start.begin(), level_start.end() - 1));
+                for (unsigned t = 1; t < un; ++t)
+                    for (size_t l = 1; l <= max_h; ++l)
+                        pos[t][l] = pos[t - 1][l] + (l < part[t - 1].hist.size() ? part[t - 1].hist[l] : 0);
+                fj.run(un, [&](unsigned t) {
+                    std::vector<uint64_t>& ps = pos[t];
+                    for (uint64_t u = nu * t / un, e = nu * (t + 1) / un; u < e; ++u) {
+                        const uint32_t i = uidx(u);
+                        order[ps[height[i]]++] = i;
+                    }
+                });
+            }
+        }
+        pt.mark("order_upper");
+        stage_records(n0, n);
+        int e = STORMCK_OK;
+        for (uint32_t l = 1; l <= max_h; ++l) {
+            const uint64_t lo = level_start[l], cnt = level_start[l + 1] - lo;
+            if (cnt == 0) continue;
+            e = launch_level(lo, cnt);
+            if (e) return e;
+        }
+        return send_back(n0, nu);
+    };
+    rc = run();
+    *last_allocated_block = last;  // the relocations applied to the caller's records so far
+    if (rc == STORMCK_OK) {
+        // checksums to the caller's order, each launch's slice as soon as it is back
+        for (const Back& x : back) {
+            if (hipEventSynchronize(x.hashed) != hipSuccess) {
+                rc = fail(STORMCK_EHIP, "commit: checksum copy-back failed");
+                break;
+            }
+            const unsigned tn = static_cast<unsigned>(std::min<uint64_t>({8, fj.size(), x.cnt / 65536 + 1}));
+            fj.run(tn, [&](unsigned t) {
+                const uint64_t lo = x.lo + x.cnt * t / tn, hi = x.lo + x.cnt * (t + 1) / tn;
+                if (order.empty()) {
+                    std::memcpy(out_checksums + lo, c->commit_cs + lo, (hi - lo) * 8);
+                } else {
+                    for (uint64_t k = lo; k < hi; ++k) out_checksums[order[k]] = c->commit_cs[k];
+                }
+            });
+        }
     }
-    return STORMCK_OK;
+    // nothing of this call may still be in flight when it returns (pinned buffers are reused)
+    const hipError_t s1 = hipStreamSynchronize(st);
+    for (Back& x : back) (void)hipEventDestroy(x.hashed);
+    if (rc == STORMCK_OK && s1 != hipSuccess) rc = fail(STORMCK_EHIP, std::string("commit: ") + hipGetErrorString(s1));
+    pt.mark("device");
+    return rc;
 }
 
 int stormck_fill_synthetic_device(void* d_dst, uint64_t stride, uint64_t n, uint64_t first, uint64_t seed,

@@ -92,12 +92,37 @@ def test_device_commit_matches_fixture(dev):
     assert singularity_step(out, g["revision"], last2) == hx(g["singularity_checksum"])
 
 
+def arrange(b: np.ndarray, how: str, rng) -> np.ndarray:
+    """Permute the dirty list and remap parent indices. "shuffled": parents may precede
+    children; "upper_shuffled": level 0 (the leaves) stays a prefix in index order, the
+    pointer blocks after it are shuffled; "children_first": as built."""
+    n_leaves = int((b["type"] == sc.LEAF).sum())
+    if how == "children_first":
+        return b.copy()
+    if how == "shuffled":
+        perm = rng.permutation(len(b))
+    else:
+        perm = np.concatenate([np.arange(n_leaves), n_leaves + rng.permutation(len(b) - n_leaves)])
+    inv = np.empty_like(perm)
+    inv[perm] = np.arange(len(b))
+    bp = b[perm].copy()
+    has = bp["parent"] >= 0
+    bp["parent"][has] = inv[bp["parent"][has]]
+    return bp
+
+
 @pytest.mark.gpu
+@pytest.mark.parametrize("how", ["shuffled", "upper_shuffled", "children_first"])
 @pytest.mark.parametrize("n,fanout,slot", [(1, 10, 1024), (10, 10, 1024), (11, 10, 1024), (999, 10, 1024),
                                             (5000, 1200, 32768), (1201, 1200, 32768),
                                             # 8- but not 16-byte aligned slots: register-quad commit kernel
-                                            (999, 10, 1032), (3000, 1200, 32776)])
-def test_device_commit_random_forests(dev, n, fanout, slot):
+                                            (999, 10, 1032), (3000, 1200, 32776),
+                                            # level 0 in several growing chunks (32K, 96K, rest)
+                                            (140000, 10, 1024)])
+def test_device_commit_random_forests(dev, n, fanout, slot, how):
+    """The commit must not depend on the caller's order beyond the documented
+    (height, index) rule; the library takes a different route per arrangement (level 0
+    a prefix or not, upper levels in height order or not)."""
     rng = np.random.default_rng(n * 7 + fanout)
     choices = [72, 256, 536, 728, 1000, 1024] if slot < 2048 else [72, 28808, 30000, 31808, 32768, 4097]
     lens = rng.choice(choices, size=n)
@@ -105,14 +130,7 @@ def test_device_commit_random_forests(dev, n, fanout, slot):
     b["birth_revision"][rng.random(len(b)) < 0.4] = 3
     arena = np.zeros(size, dtype=np.uint8)
     arena[slot:slot + n * slot] = rng.integers(0, 256, size=n * slot, dtype=np.uint8)
-    # shuffle the dirty list: the commit must not depend on the caller's order beyond
-    # the documented (height, index) rule, and parents may precede children in it
-    perm = rng.permutation(len(b))
-    inv = np.empty_like(perm)
-    inv[perm] = np.arange(len(b))
-    bp = b[perm].copy()
-    has = bp["parent"] >= 0
-    bp["parent"][has] = inv[bp["parent"][has]]
+    bp = arrange(b, how, rng)
     ref_arena, ref_b = arena.copy(), bp.copy()
     want_cs, want_last = o.commit(ref_arena, ref_b, 9, last)
     out, cs, last2 = device_commit(arena, bp, 9, last, dev)
