@@ -875,10 +875,16 @@ __global__ __launch_bounds__(256) void k_key_tags(const uint8_t* __restrict__ ke
 // LDS ring, and holds its PW tags in registers until the end, so the loop issues no
 // stores and a counted vmcnt wait ((RING-2)*P LDS-DMA ops younger than the batch being
 // hashed) is exact. A wave with fewer than PW batches (the grid's last) waits vmcnt(0).
-template <int AUX, int P, int RING, int PW>
-__global__ __launch_bounds__(256) void k_key_tags_ring(const uint8_t* __restrict__ keys, uint32_t len, uint64_t batches,
-                                                        uint64_t* __restrict__ out) {
+// KLEN > 0: every key is KLEN bytes (a compile-time constant, e.g. storm's 48-byte keys
+// at stride 48), so the stripe count and the tail fold into straight-line code; the
+// kernel is VALU-bound (about 28 64-bit multiplies per 48-byte key) and the generic tail
+// costs about a third of its instructions. KLEN = 0: the runtime `len`.
+template <int AUX, int P, int RING, int PW, int KLEN = 0>
+__global__ __launch_bounds__(256) void k_key_tags_ring(const uint8_t* __restrict__ keys, uint32_t len_rt,
+                                                        uint64_t batches, uint64_t* __restrict__ out) {
     static_assert(RING >= 2 && PW >= RING, "ring");
+    static_assert(KLEN >= 0 && KLEN <= 16 * P, "key length within the stride");
+    const uint32_t len = KLEN > 0 ? static_cast<uint32_t>(KLEN) : len_rt;
     constexpr uint32_t kStride = 16 * P, kRegion = 64 * kStride;
     extern __shared__ __attribute__((aligned(16))) uint8_t dyn_lds[];
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;

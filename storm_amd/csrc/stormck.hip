@@ -840,7 +840,8 @@ int stormck_key_tags_device(const void* d_keys, uint64_t stride, const uint64_t*
         (reinterpret_cast<uintptr_t>(k) & 15) == 0 && n >= 64) {
         // whole batches of 64 keys through a per-wave LDS-DMA prefetch ring: keys up to
         // 64 bytes (storm's 48-byte keys) take the 4-slot ring with a compile-time
-        // stride, longer ones the runtime-stride double buffer
+        // stride (and a compile-time length when keys fill their stride), longer ones the
+        // runtime-stride double buffer
         const uint64_t batches = n / 64;
         constexpr uint32_t kPerWave = 8;
         constexpr int kKeyRing = 4;
@@ -851,20 +852,36 @@ int stormck_key_tags_device(const void* d_keys, uint64_t stride, const uint64_t*
         const size_t ring_lds = 4 * kKeyRing * 64 * static_cast<size_t>(stride);
         switch (stride) {
             case 16:
-                hipLaunchKernelGGL((k_key_tags_ring<kAuxNT, 1, kKeyRing, kPerWave>), grid_k, dim3(kThreads), ring_lds, st,
-                                   k, len, batches, d_out);
+                if (len == 16)
+                    hipLaunchKernelGGL((k_key_tags_ring<kAuxNT, 1, kKeyRing, kPerWave, 16>), grid_k, dim3(kThreads), ring_lds,
+                                       st, k, len, batches, d_out);
+                else
+                    hipLaunchKernelGGL((k_key_tags_ring<kAuxNT, 1, kKeyRing, kPerWave>), grid_k, dim3(kThreads), ring_lds, st,
+                                       k, len, batches, d_out);
                 break;
             case 32:
-                hipLaunchKernelGGL((k_key_tags_ring<kAuxNT, 2, kKeyRing, kPerWave>), grid_k, dim3(kThreads), ring_lds, st,
-                                   k, len, batches, d_out);
+                if (len == 32)
+                    hipLaunchKernelGGL((k_key_tags_ring<kAuxNT, 2, kKeyRing, kPerWave, 32>), grid_k, dim3(kThreads), ring_lds,
+                                       st, k, len, batches, d_out);
+                else
+                    hipLaunchKernelGGL((k_key_tags_ring<kAuxNT, 2, kKeyRing, kPerWave>), grid_k, dim3(kThreads), ring_lds, st,
+                                       k, len, batches, d_out);
                 break;
             case 48:
-                hipLaunchKernelGGL((k_key_tags_ring<kAuxNT, 3, kKeyRing, kPerWave>), grid_k, dim3(kThreads), ring_lds, st,
-                                   k, len, batches, d_out);
+                if (len == 48)
+                    hipLaunchKernelGGL((k_key_tags_ring<kAuxNT, 3, kKeyRing, kPerWave, 48>), grid_k, dim3(kThreads), ring_lds,
+                                       st, k, len, batches, d_out);
+                else
+                    hipLaunchKernelGGL((k_key_tags_ring<kAuxNT, 3, kKeyRing, kPerWave>), grid_k, dim3(kThreads), ring_lds, st,
+                                       k, len, batches, d_out);
                 break;
             case 64:
-                hipLaunchKernelGGL((k_key_tags_ring<kAuxNT, 4, kKeyRing, kPerWave>), grid_k, dim3(kThreads), ring_lds, st,
-                                   k, len, batches, d_out);
+                if (len == 64)
+                    hipLaunchKernelGGL((k_key_tags_ring<kAuxNT, 4, kKeyRing, kPerWave, 64>), grid_k, dim3(kThreads), ring_lds,
+                                       st, k, len, batches, d_out);
+                else
+                    hipLaunchKernelGGL((k_key_tags_ring<kAuxNT, 4, kKeyRing, kPerWave>), grid_k, dim3(kThreads), ring_lds, st,
+                                       k, len, batches, d_out);
                 break;
             default:
                 hipLaunchKernelGGL(k_key_tags_lds<kAuxNT>, grid_k, dim3(kThreads), 4 * 2 * 64 * static_cast<size_t>(stride),
