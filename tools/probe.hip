@@ -28,6 +28,117 @@ namespace stormck {
 // (base % 16 == 0, stride % 16 == 0). U stripes (2U dwordx4) per pipelined group.
 }  // namespace stormck
 
+namespace stormck {
+// ---------------------------------------------------------------------------
+// REJECTED (profiles/r01_probe_persist.txt: 0.884-0.886 vs 0.886 for the one-group-per-
+// workgroup kernel). Persistent form of k_xxh64_glds (R = 2, barrier-synchronised ring): one workgroup per
+// CU walks groups g = blockIdx.x, + gridDim.x, ... of 16*WAVES blocks, and the tile
+// stream runs on across group boundaries, so the first tile of the next group is in
+// flight while the current group's last tile hashes and its blocks finish. The
+// one-group-per-workgroup kernel drains the ring at every group and pays a workgroup
+// launch plus a memory round trip before the next group's first tile lands (1 WG per
+// CU: the 128 KiB ring leaves no room for a second). At any time the resident
+// workgroups cover a contiguous window of groups, as with the hardware's dispatch order.
+// Requires nst / T >= 1 (the host checks).
+// ---------------------------------------------------------------------------
+template <int T, int AUX, bool HASH = true, bool VERIFY = false, int WAVES = 8>
+__global__ __launch_bounds__(64 * WAVES) void k_xxh64_glds_p(const uint8_t* __restrict__ base, uint64_t stride,
+                                                             uint32_t len, uint64_t n, uint64_t* __restrict__ out,
+                                                             const uint64_t* __restrict__ expected = nullptr,
+                                                             unsigned long long* __restrict__ first_bad = nullptr,
+                                                             unsigned long long* __restrict__ n_bad = nullptr) {
+    constexpr int BPW = 16 * WAVES;
+    constexpr int ROW = 32 * T;
+    constexpr int TILE = BPW * ROW;
+    constexpr int INSTR = TILE / 1024;
+    constexpr int PER_WAVE = INSTR / WAVES;
+    static_assert(INSTR % WAVES == 0, "tile must split evenly over the waves");
+    __shared__ __attribute__((aligned(16))) uint8_t lds[2 * TILE];
+
+    const uint32_t tid = threadIdx.x;
+    const uint32_t wave = tid >> 6, lane = tid & 63;
+    const uint64_t ngroups = (n + BPW - 1) / BPW;
+    const uint64_t G = gridDim.x;
+    uint64_t g = blockIdx.x;
+    if (g >= ngroups) return;
+    const uint32_t nst = len >> 5, ntiles = nst / T;
+    const uint64_t total = ((ngroups - g + G - 1) / G) * ntiles;
+
+    // piece geometry, the same in every group: block row and source byte offset
+    uint32_t prow[PER_WAVE], pofs[PER_WAVE];
+#pragma unroll
+    for (int k = 0; k < PER_WAVE; ++k) {
+        const uint32_t off = (wave * PER_WAVE + k) * 1024 + lane * 16;
+        const uint32_t b = off / ROW, q = (off % ROW) / 16;
+        prow[k] = b;
+        pofs[k] = ((q + glds_rot<T>(b)) % (2 * T)) * 16;
+    }
+    const uint8_t* src[PER_WAVE];
+    auto set_src = [&](uint64_t grp) {
+#pragma unroll
+        for (int k = 0; k < PER_WAVE; ++k) {
+            uint64_t gb = grp * BPW + prow[k];
+            if (gb >= n) gb = n - 1;  // shadow the last block; never stored
+            src[k] = base + gb * stride + pofs[k];
+        }
+    };
+
+    const uint32_t b = tid >> 2, j = tid & 3;
+    const uint32_t rot = glds_rot<T>(b);
+    uint64_t acc = acc_seed(j);
+    set_src(g);
+    STORMCK_GLDS_ISSUE(src, lds + wave * PER_WAVE * 1024, 0u, PER_WAVE, ROW, AUX);
+    uint32_t t = 0;
+    for (uint64_t u = 0; u < total; ++u) {
+        wait_vmcnt<0>();
+        __builtin_amdgcn_s_barrier();
+        if (u + 1 < total) {
+            uint32_t tn = t + 1;
+            if (tn == ntiles) {
+                tn = 0;
+                set_src(g + G);
+            }
+            STORMCK_GLDS_ISSUE(src, lds + ((u + 1) & 1) * TILE + wave * PER_WAVE * 1024, tn, PER_WAVE, ROW, AUX);
+        }
+        const uint8_t* row = lds + (u & 1) * TILE + b * ROW + (j & 1) * 8;
+#pragma unroll
+        for (int s = 0; s < T; ++s) {
+            const uint32_t q = (2 * s + (j >> 1) + 2 * T - rot) % (2 * T);
+            const uint64_t w = *reinterpret_cast<const uint64_t*>(row + q * 16);
+            if constexpr (HASH) acc = round(acc, w);
+            else acc ^= w;
+        }
+        if (++t == ntiles) {
+            // this group's blocks are complete: remainder stripes and tail from global
+            // memory (none for 32 KiB blocks), then the checksum
+            const uint64_t gbk = g * BPW + b;
+            const uint64_t gb = gbk < n ? gbk : n - 1;
+            const uint8_t* blk_src = base + gb * stride;
+            for (uint32_t s = ntiles * T; s < nst; ++s)
+                acc = round(acc, reinterpret_cast<const uint64_t*>(blk_src)[4 * s + j]);
+            const uint64_t v1 = quad_bcast<0>(acc), v2 = quad_bcast<1>(acc), v3 = quad_bcast<2>(acc),
+                           v4 = quad_bcast<3>(acc);
+            if (j == 0 && gbk < n) {
+                const uint64_t h0 = converge(v1, v2, v3, v4);
+                const uint64_t h = finish_fast(h0, len, blk_src + 32 * static_cast<uint64_t>(nst), len & 31);
+                if constexpr (VERIFY) {
+                    if (h != expected[gbk]) {
+                        atomicMin(first_bad, static_cast<unsigned long long>(gbk));
+                        atomicAdd(n_bad, 1ULL);
+                    }
+                } else {
+                    out[gbk] = h;
+                }
+            }
+            acc = acc_seed(j);
+            t = 0;
+            g += G;
+        }
+    }
+}
+
+}  // namespace stormck
+
 // ---- host XXH64 (probe self-check only) ----
 static inline uint64_t hrotl(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
 static inline uint64_t hround(uint64_t a, uint64_t w) { a += w * kP2; a = hrotl(a, 31); return a * kP1; }
@@ -157,14 +268,19 @@ int main(int argc, char** argv) {
     vs.push_back({std::string("glds " #W "w T=" #T " R=" #R) + (SY ? " sync" : " nosync"), [&] {                              \
         hipLaunchKernelGGL((k_xxh64_glds<T, R, 2, true, false, W, SY>), dim3((unsigned)((n + 16 * W - 1) / (16 * W))), \
                            dim3(64 * W), 0, 0, d, L, (uint32_t)L, n, out, nullptr, nullptr, nullptr); }, true})
-    GW(8, 16, 2, true); GW(8, 20, 2, true);
+    GW(8, 16, 2, true);
     // cache-policy bits of the LDS-DMA loads (aux: 1 = sc0, 2 = nt, 16 = sc1) and the XCD remap
 #define GA(AUXV, XC)                                                                                           \
     vs.push_back({std::string("glds 8w T=16 R=2 aux=" #AUXV) + (XC ? " xcd" : ""), [&] {                       \
         hipLaunchKernelGGL((k_xxh64_glds<16, 2, AUXV, true, false, 8, true, XC>), dim3((unsigned)((n + 127) / 128)), \
                            dim3(512), 0, 0, d, L, (uint32_t)L, n, out, nullptr, nullptr, nullptr); }, true})
-    GA(0, false); GA(3, false); GA(18, false); GA(16, false); GA(2, true);
+
     const dim3 g8((unsigned)((n + 127) / 128));
+    // persistent form: one workgroup per CU, the tile stream runs across group boundaries
+    const dim3 gp((unsigned)std::min<uint64_t>((n + 127) / 128, (uint64_t)prop.multiProcessorCount));
+    vs.push_back({"persist 8w T=16", [&] { hipLaunchKernelGGL((k_xxh64_glds_p<16, 2, true, false, 8>), gp, dim3(512), 0, 0, d, L, (uint32_t)L, n, out, nullptr, nullptr, nullptr); }, true});
+    vs.push_back({"persist 8w T=20", [&] { hipLaunchKernelGGL((k_xxh64_glds_p<20, 2, true, false, 8>), gp, dim3(512), 0, 0, d, L, (uint32_t)L, n, out, nullptr, nullptr, nullptr); }, true});
+    vs.push_back({"persist 8w T=16 noHash", [&] { hipLaunchKernelGGL((k_xxh64_glds_p<16, 2, false, false, 8>), gp, dim3(512), 0, 0, d, L, (uint32_t)L, n, out, nullptr, nullptr, nullptr); }, false});
     vs.push_back({"glds8w T=16 R=2 noHash", [&] { hipLaunchKernelGGL((k_xxh64_glds<16, 2, 2, false, false, 8>), g8, dim3(512), 0, 0, d, L, (uint32_t)L, n, out, nullptr, nullptr, nullptr); }, false});
     std::vector<std::vector<double>> gbs(vs.size());
     for (int r = 0; r < rounds; ++r) {
