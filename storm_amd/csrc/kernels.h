@@ -584,12 +584,33 @@ struct EntryWords {
 };
 
 // XXH64 of a synthesised node by one quad (lane j = accumulator j). Every lane of
-// the quad returns the hash. size is a multiple of 8 (no 4-/1-byte tail).
-template <class W>
+// the quad returns the hash. size is a multiple of 8 (no 4-/1-byte tail). Words are
+// fetched U stripes ahead (group g+1's child loads in flight while group g hashes):
+// fetched one at a time, each round waited for its load, which made a 1,200-way
+// level of 14K nodes take 240 us instead of the ~30 us serial XXH64 chain.
+template <class W, int U = 16>
 __device__ __forceinline__ uint64_t hash_words_quad(const W& word, uint32_t size, uint32_t j) {
     const uint32_t nst = size >> 5;
     uint64_t acc = acc_seed(j);
-    for (uint32_t s = 0; s < nst; ++s) acc = round(acc, word(4 * s + j));
+    const uint32_t ngroups = nst / U;
+    uint32_t s = 0;
+    if (ngroups > 0) {
+        uint64_t wa[U], wb[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) wa[u] = word(4 * u + j);
+        for (uint32_t g = 1; g < ngroups; ++g) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) wb[u] = word(4 * (g * U + u) + j);
+#pragma unroll
+            for (int u = 0; u < U; ++u) acc = round(acc, wa[u]);
+#pragma unroll
+            for (int u = 0; u < U; ++u) wa[u] = wb[u];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc = round(acc, wa[u]);
+        s = ngroups * U;
+    }
+    for (; s < nst; ++s) acc = round(acc, word(4 * s + j));
     const uint64_t v1 = quad_bcast<0>(acc), v2 = quad_bcast<1>(acc), v3 = quad_bcast<2>(acc), v4 = quad_bcast<3>(acc);
     uint64_t h = (size >= 32) ? converge(v1, v2, v3, v4) : kP5;
     h += size;
@@ -615,13 +636,50 @@ __global__ __launch_bounds__(256) void k_pointer_level(const uint64_t* __restric
     if (j == 0 && pj < pm) parent_cs[pj] = h;
 }
 
-__global__ __launch_bounds__(64) void k_pointer_node(const uint64_t* __restrict__ entries,
-                                                      const uint8_t* __restrict__ types, uint32_t cnt,
-                                                      uint32_t fanout, uint64_t* __restrict__ out_cs) {
-    const uint32_t j = threadIdx.x & 3;
+// Small levels (a handful of nodes, e.g. the top of a shard tree): one workgroup per
+// node. All 256 threads synthesise the node's words into LDS at once, then quad 0
+// hashes from LDS. A quad synthesising its own words issues ~25 instructions per
+// round where hashing alone needs ~11, and a lone wave is issue-bound: 75 us per
+// 30,000 B node against ~26 us for the bare XXH64 chain. Nodes up to kNodeLds bytes.
+constexpr uint32_t kNodeLds = 32768;
+struct LdsWords {
+    const uint64_t* p;
+    __device__ __forceinline__ uint64_t operator()(uint32_t k) const { return p[k]; }
+};
+
+template <class W>
+__device__ __forceinline__ void hash_node_wide(const W& w, uint32_t size, uint64_t* __restrict__ out) {
+    __shared__ uint64_t node[kNodeLds / 8];
+    const uint32_t words = size / 8;
+    for (uint32_t k = threadIdx.x; k < words; k += blockDim.x) node[k] = w(k);
+    __syncthreads();
+    if (threadIdx.x < 4) {
+        const uint64_t h = hash_words_quad(LdsWords{node}, size, threadIdx.x);
+        if (threadIdx.x == 0) *out = h;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_pointer_level_wide(const uint64_t* __restrict__ cs, uint64_t m,
+                                                             uint64_t addr_base, uint64_t rev, uint8_t type,
+                                                             uint32_t fanout, uint64_t* __restrict__ parent_cs) {
+    LevelWords w;
+    w.cs = cs; w.lo = static_cast<uint64_t>(blockIdx.x) * fanout; w.addr_base = addr_base; w.rev = rev;
+    w.fanout = fanout; w.type = type;
+    w.cnt = static_cast<uint32_t>((m - w.lo) < fanout ? (m - w.lo) : fanout);
+    hash_node_wide(w, pointer_block_size(fanout), parent_cs + blockIdx.x);
+}
+
+__global__ __launch_bounds__(256) void k_pointer_node(const uint64_t* __restrict__ entries,
+                                                       const uint8_t* __restrict__ types, uint32_t cnt,
+                                                       uint32_t fanout, uint64_t* __restrict__ out_cs) {
     EntryWords w{entries, types, cnt, fanout};
-    const uint64_t h = hash_words_quad(w, pointer_block_size(fanout), j);
-    if (threadIdx.x == 0) *out_cs = h;
+    const uint32_t size = pointer_block_size(fanout);
+    if (size <= kNodeLds) {
+        hash_node_wide(w, size, out_cs);
+    } else if (threadIdx.x < 4) {
+        const uint64_t h = hash_words_quad(w, size, threadIdx.x);
+        if (threadIdx.x == 0) *out_cs = h;
+    }
 }
 
 __global__ __launch_bounds__(256) void k_pack_pointer_blocks(const uint64_t* __restrict__ cs, uint64_t m,

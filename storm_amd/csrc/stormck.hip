@@ -133,6 +133,10 @@ constexpr uint64_t kWideBatch = 128;      // batches up to this many blocks: k_x
 constexpr uint64_t kStreamBatch = 16384;  // uniform batches from this many blocks: k_xxh64_glds
 constexpr unsigned kThreads = 256;
 constexpr uint32_t kMaxFanout = 1u << 16;
+// Merkle levels of at most this many nodes take one workgroup per node (k_pointer_level_wide):
+// a node is then about one XXH64 chain (~26 us for 30,000 B); larger levels put a quad
+// on each node, 64 nodes per workgroup, to keep every CU busy.
+constexpr uint64_t kWideNodes = 256;
 
 // Cached answer to "is there a usable gfx950 device?" per process.
 int device_check() {
@@ -643,6 +647,14 @@ int stormck_pointer_level_device(const uint64_t* d_child_cs, uint64_t m, uint64_
     int rc = device_check();
     if (rc) return rc;
     const uint64_t pm = (m + fanout - 1) / fanout;
+    if (pm <= kWideNodes && pointer_block_size(fanout) <= kNodeLds) {
+        // a few nodes: one workgroup each, words synthesised into LDS by all its threads
+        hipLaunchKernelGGL(k_pointer_level_wide, dim3(static_cast<unsigned>(pm)), dim3(kThreads), 0,
+                           static_cast<hipStream_t>(stream), d_child_cs, m, child_addr_base, rev, child_type, fanout,
+                           d_parent_cs);
+        HIP_TRY(hipGetLastError());
+        return STORMCK_OK;
+    }
     dim3 grid;
     if (!grid_for(pm * 4, &grid)) return fail(STORMCK_EINVAL, "level too large");
     hipLaunchKernelGGL(k_pointer_level, grid, dim3(kThreads), 0, static_cast<hipStream_t>(stream), d_child_cs, m,
@@ -658,7 +670,7 @@ int stormck_pointer_node_device(const stormck_pointer* d_entries, const uint8_t*
     int rc = device_check();
     if (rc) return rc;
     static_assert(sizeof(stormck_pointer) == 24, "Pointer is 24 bytes");
-    hipLaunchKernelGGL(k_pointer_node, dim3(1), dim3(64), 0, static_cast<hipStream_t>(stream),
+    hipLaunchKernelGGL(k_pointer_node, dim3(1), dim3(kThreads), 0, static_cast<hipStream_t>(stream),
                        reinterpret_cast<const uint64_t*>(d_entries), d_types, count, fanout, d_out_cs);
     HIP_TRY(hipGetLastError());
     return STORMCK_OK;
