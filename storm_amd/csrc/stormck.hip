@@ -439,49 +439,63 @@ int host_pipeline(const void* base, uint64_t stride, const uint32_t* lens, uint3
         return STORMCK_OK;
     };
 
-    uint64_t chunk_idx = 0;
-    for (uint64_t first = 0; first < n; first += per_chunk, ++chunk_idx) {
-        Stage& s = c->st[chunk_idx % kStages];
-        rc = drain(s);
-        if (rc) return rc;
-        const uint64_t cnt = std::min<uint64_t>(per_chunk, n - first);
-        // bytes to move: up to the end of the last block in the chunk
-        const uint64_t last_len = lens ? lens[first + cnt - 1] : len;
-        const uint64_t bytes = (cnt - 1) * stride + last_len;
-        const uint8_t* chunk_src = src + first * stride;
-        if (direct) {
-            HIP_TRY(hipMemcpyAsync(s.d_data, chunk_src, bytes, hipMemcpyHostToDevice, s.stream));
-        } else {
-            par_copy(s.pinned, chunk_src, bytes);
-            HIP_TRY(hipMemcpyAsync(s.d_data, s.pinned, bytes, hipMemcpyHostToDevice, s.stream));
-        }
-        if (lens) HIP_TRY(hipMemcpyAsync(s.d_lens, lens + first, cnt * 4, hipMemcpyHostToDevice, s.stream));
-        if (expected) {
-            HIP_TRY(hipMemcpyAsync(s.d_expected, expected + first, cnt * 8, hipMemcpyHostToDevice, s.stream));
-            const uint64_t init[2] = {cnt, 0};
-            std::memcpy(s.h_result, init, 16);
-            HIP_TRY(hipMemcpyAsync(s.d_result, s.h_result, 16, hipMemcpyHostToDevice, s.stream));
-            rc = launch_checksum(s.d_data, stride, lens ? s.d_lens : nullptr, len, nullptr, cnt, nullptr,
-                                 s.d_expected, reinterpret_cast<unsigned long long*>(s.d_result),
-                                 reinterpret_cast<unsigned long long*>(s.d_result + 1), s.stream);
+    // A call that fails part-way must not leave stages marked busy: the next call's
+    // drain would copy their stale results into that call's output.
+    auto pipeline = [&]() -> int {
+        int rc = STORMCK_OK;
+        uint64_t chunk_idx = 0;
+        for (uint64_t first = 0; first < n; first += per_chunk, ++chunk_idx) {
+            Stage& s = c->st[chunk_idx % kStages];
+            rc = drain(s);
             if (rc) return rc;
-            HIP_TRY(hipMemcpyAsync(s.h_result, s.d_result, 16, hipMemcpyDeviceToHost, s.stream));
-        } else {
-            rc = launch_checksum(s.d_data, stride, lens ? s.d_lens : nullptr, len, nullptr, cnt, s.d_out, nullptr,
-                                 nullptr, nullptr, s.stream);
-            if (rc) return rc;
-            HIP_TRY(hipMemcpyAsync(s.h_out, s.d_out, cnt * 8, hipMemcpyDeviceToHost, s.stream));
+            const uint64_t cnt = std::min<uint64_t>(per_chunk, n - first);
+            // bytes to move: up to the end of the last block in the chunk
+            const uint64_t last_len = lens ? lens[first + cnt - 1] : len;
+            const uint64_t bytes = (cnt - 1) * stride + last_len;
+            const uint8_t* chunk_src = src + first * stride;
+            if (direct) {
+                HIP_TRY(hipMemcpyAsync(s.d_data, chunk_src, bytes, hipMemcpyHostToDevice, s.stream));
+            } else {
+                par_copy(s.pinned, chunk_src, bytes);
+                HIP_TRY(hipMemcpyAsync(s.d_data, s.pinned, bytes, hipMemcpyHostToDevice, s.stream));
+            }
+            if (lens) HIP_TRY(hipMemcpyAsync(s.d_lens, lens + first, cnt * 4, hipMemcpyHostToDevice, s.stream));
+            if (expected) {
+                HIP_TRY(hipMemcpyAsync(s.d_expected, expected + first, cnt * 8, hipMemcpyHostToDevice, s.stream));
+                const uint64_t init[2] = {cnt, 0};
+                std::memcpy(s.h_result, init, 16);
+                HIP_TRY(hipMemcpyAsync(s.d_result, s.h_result, 16, hipMemcpyHostToDevice, s.stream));
+                rc = launch_checksum(s.d_data, stride, lens ? s.d_lens : nullptr, len, nullptr, cnt, nullptr,
+                                     s.d_expected, reinterpret_cast<unsigned long long*>(s.d_result),
+                                     reinterpret_cast<unsigned long long*>(s.d_result + 1), s.stream);
+                if (rc) return rc;
+                HIP_TRY(hipMemcpyAsync(s.h_result, s.d_result, 16, hipMemcpyDeviceToHost, s.stream));
+            } else {
+                rc = launch_checksum(s.d_data, stride, lens ? s.d_lens : nullptr, len, nullptr, cnt, s.d_out, nullptr,
+                                     nullptr, nullptr, s.stream);
+                if (rc) return rc;
+                HIP_TRY(hipMemcpyAsync(s.h_out, s.d_out, cnt * 8, hipMemcpyDeviceToHost, s.stream));
+            }
+            HIP_TRY(hipEventRecord(s.done, s.stream));
+            s.first = first;
+            s.count = cnt;
+            s.busy = true;
+            // a pinned staging buffer may be refilled only after its H2D finished; with two
+            // stages the drain at the top of the next-but-one iteration guarantees that.
         }
-        HIP_TRY(hipEventRecord(s.done, s.stream));
-        s.first = first;
-        s.count = cnt;
-        s.busy = true;
-        // a pinned staging buffer may be refilled only after its H2D finished; with two
-        // stages the drain at the top of the next-but-one iteration guarantees that.
-    }
-    for (Stage& s : c->st) {
-        rc = drain(s);
-        if (rc) return rc;
+        for (Stage& s : c->st) {
+            rc = drain(s);
+            if (rc) return rc;
+        }
+        return STORMCK_OK;
+    };
+    rc = pipeline();
+    if (rc) {
+        for (Stage& s : c->st) {
+            if (s.busy) (void)hipStreamSynchronize(s.stream);
+            s.busy = false;
+        }
+        return rc;
     }
     if (first_bad) *first_bad = fb;
     if (n_bad) *n_bad = nb;
