@@ -412,7 +412,7 @@ def main():
             "metric": METRIC, "value": round(value, 2), "unit": "GiB/s", "n_gpus": world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "u64", "data": "synthetic",
-            "config": {"workload": "c3: 16M x 32 KiB blocks per GPU, XXH64 seed 0 (blocks.Checksum) "
+            "config": {"workload": f"c3: {n_gpu / 2**20:g}M x 32 KiB blocks per GPU, XXH64 seed 0 (blocks.Checksum) "
                                    "+ shard Merkle pointer tree" + (" + RCCL all-gather of shard roots" if distributed else ""),
                        "blocks_per_gpu": n_gpu, "block_bytes": BLOCK, "arena_blocks": arena_n,
                        "passes_per_step": passes, "parallelism": f"dp{world} (contiguous block ranges)"},
