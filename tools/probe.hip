@@ -139,6 +139,39 @@ __global__ __launch_bounds__(64 * WAVES) void k_xxh64_glds_p(const uint8_t* __re
 
 }  // namespace stormck
 
+namespace stormck {
+// REJECTED, the north star's literal mapping: ONE WAVEFRONT PER BLOCK.
+// The wave streams its block through a private 2 x 2 KiB LDS ring with coalesced
+// LDS-DMA (64 lanes x 16 B per instruction), and quad 0 hashes each tile (XXH64's four
+// serial accumulators leave no work for the other 60 lanes). Requires len % 2048 == 0.
+template <int WPB>
+__global__ __launch_bounds__(64 * WPB) void k_xxh64_wave(const uint8_t* __restrict__ base, uint64_t stride,
+                                                         uint32_t len, uint64_t n, uint64_t* __restrict__ out) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[WPB * 2 * 2048];
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint64_t blk = static_cast<uint64_t>(blockIdx.x) * WPB + wave;
+    if (blk >= n) return;
+    const uint8_t* src = base + blk * stride + lane * 16;
+    uint8_t* ring = lds + wave * 2 * 2048;
+    const uint32_t ntiles = len / 2048;
+    const uint8_t* s2[2] = {src, src + 1024};
+    STORMCK_GLDS_ISSUE(s2, ring, 0u, 2, 2048, 2);
+    uint64_t acc = acc_seed(lane & 3);
+    for (uint32_t t = 0; t < ntiles; ++t) {
+        wait_vmcnt<0>();
+        wait_lgkm0();
+        if (t + 1 < ntiles) STORMCK_GLDS_ISSUE(s2, ring + ((t + 1) & 1) * 2048, t + 1, 2, 2048, 2);
+        if (lane < 4) {
+            const uint8_t* tile = ring + (t & 1) * 2048 + lane * 8;
+#pragma unroll 8
+            for (int s = 0; s < 64; ++s) acc = round(acc, *reinterpret_cast<const uint64_t*>(tile + 32 * s));
+        }
+    }
+    const uint64_t v1 = quad_bcast<0>(acc), v2 = quad_bcast<1>(acc), v3 = quad_bcast<2>(acc), v4 = quad_bcast<3>(acc);
+    if (lane == 0) out[blk] = finish_fast(converge(v1, v2, v3, v4), len, base + blk * stride + len, 0);
+}
+}  // namespace stormck
+
 // ---- host XXH64 (probe self-check only) ----
 static inline uint64_t hrotl(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
 static inline uint64_t hround(uint64_t a, uint64_t w) { a += w * kP2; a = hrotl(a, 31); return a * kP1; }
@@ -276,6 +309,8 @@ int main(int argc, char** argv) {
                            dim3(512), 0, 0, d, L, (uint32_t)L, n, out, nullptr, nullptr, nullptr); }, true})
 
     const dim3 g8((unsigned)((n + 127) / 128));
+    vs.push_back({"wave-per-block (4 waves/WG)", [&] { hipLaunchKernelGGL((k_xxh64_wave<4>), dim3((unsigned)((n + 3) / 4)), dim3(256), 0, 0, d, L, (uint32_t)L, n, out); }, true});
+    vs.push_back({"wg-per-block (k_xxh64_wide)", [&] { hipLaunchKernelGGL((k_xxh64_wide<false, false, false>), dim3((unsigned)n), dim3(256), 0, 0, d, L, nullptr, (uint32_t)L, nullptr, n, out, nullptr, nullptr, nullptr); }, true});
     // persistent form: one workgroup per CU, the tile stream runs across group boundaries
     const dim3 gp((unsigned)std::min<uint64_t>((n + 127) / 128, (uint64_t)prop.multiProcessorCount));
     vs.push_back({"persist 8w T=16", [&] { hipLaunchKernelGGL((k_xxh64_glds_p<16, 2, true, false, 8>), gp, dim3(512), 0, 0, d, L, (uint32_t)L, n, out, nullptr, nullptr, nullptr); }, true});
