@@ -31,7 +31,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X spec, /opt/skills/guides/MI355X_MICROARCH.md (ch
 BLOCK = 32768          # blocks.BlockSize, /root/reference/blocks/types.go:4
 FANOUT = 1200          # pointer.PointersPerBlock, /root/reference/blocks/pointer/params.go:6
 REV = 1
-KERNEL = "k_xxh64_glds<16,2,nt,8w>"  # dominant kernel (storm_amd/csrc/kernels.h), as named in profiles/traffic.json
+KERNEL = "k_xxh64_glds_skew<16,nt,8w,4KiB>"  # dominant kernel (storm_amd/csrc/kernels.h), as named in profiles/traffic.json
 
 
 def parse():

@@ -11,6 +11,7 @@
 // each 32-byte stripe), 16 blocks per wave64; the 4 accumulators meet through DPP quad
 // permutes for the merge; lane 0 of the quad does tail + avalanche. Kernels:
 //   * k_xxh64_glds   : uniform-length batches, stripes staged HBM -> LDS by LDS-DMA
+//   * k_xxh64_glds_skew: the same for large batches, persistent, waves' streams 4 KiB apart
 //   * k_xxh64_quad   : any shape (per-block lengths, offsets, alignment), register loads
 //   * k_xxh64_single : one slice <= 64 KiB read from pinned host memory (latency path)
 //   * k_xxh64_wide   : small batches, one workgroup per block staged whole into LDS
@@ -465,6 +466,117 @@ __global__ __launch_bounds__(64 * WAVES) void k_xxh64_glds(const uint8_t* __rest
             }
         } else {
             out[gbk] = h;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Large uniform batches: the same LDS-DMA ring, persistent and with the waves' streams
+// skewed by 4 KiB. One workgroup per CU walks groups g = blockIdx.x, + gridDim.x, ...
+// of 16*WAVES blocks, and the tile stream runs on across group boundaries. Wave v
+// starts its stream v*SKEW tiles late, so at any moment a workgroup reads its blocks
+// at WAVES different offsets, SKEW*32*T bytes apart, instead of all at one offset.
+// Measured (profiles/r01_probe_phase_skew.txt): 4 KiB apart, 0.897 -> 0.912 of peak
+// on a well-placed arena and no change on a badly placed one; 512 B, 1 KiB and 2 KiB
+// apart all lose. The first and last (WAVES-1)*SKEW steps leave some waves idle, so
+// the host uses this kernel only when each workgroup has thousands of steps.
+// A wave only reads the LDS rows it loaded itself (its own 16 blocks: T even), so the
+// skew needs no synchronisation beyond the ring's per-step barrier.
+// ---------------------------------------------------------------------------
+template <int T, int AUX, bool VERIFY, int WAVES, int SKEW>
+__global__ __launch_bounds__(64 * WAVES) void k_xxh64_glds_skew(const uint8_t* __restrict__ base, uint64_t stride,
+                                                                uint32_t len, uint64_t n, uint64_t* __restrict__ out,
+                                                                const uint64_t* __restrict__ expected,
+                                                                unsigned long long* __restrict__ first_bad,
+                                                                unsigned long long* __restrict__ n_bad) {
+    constexpr int BPW = 16 * WAVES;
+    constexpr int ROW = 32 * T;
+    constexpr int TILE = BPW * ROW;
+    constexpr int INSTR = TILE / 1024;
+    constexpr int PER_WAVE = INSTR / WAVES;
+    static_assert(INSTR % WAVES == 0 && T % 2 == 0, "a wave's pieces must be its own block rows");
+    __shared__ __attribute__((aligned(16))) uint8_t lds[2 * TILE];
+
+    const uint32_t tid = threadIdx.x;
+    const uint32_t wave = tid >> 6, lane = tid & 63;
+    const uint64_t ngroups = (n + BPW - 1) / BPW;
+    const uint64_t G = gridDim.x;
+    if (blockIdx.x >= ngroups) return;
+    const uint32_t nst = len >> 5, ntiles = nst / T;
+    const uint64_t total = ((ngroups - blockIdx.x + G - 1) / G) * ntiles;  // this workgroup's tile steps
+    const uint64_t ph = static_cast<uint64_t>(wave) * SKEW;                  // this wave's start delay
+    const uint64_t steps = total + static_cast<uint64_t>(WAVES - 1) * SKEW;   // the same for every wave
+
+    // piece geometry (the same in every group): block row and source byte offset
+    uint32_t prow[PER_WAVE], pofs[PER_WAVE];
+#pragma unroll
+    for (int k = 0; k < PER_WAVE; ++k) {
+        const uint32_t off = (wave * PER_WAVE + k) * 1024 + lane * 16;
+        const uint32_t b = off / ROW, q = (off % ROW) / 16;
+        prow[k] = b;
+        pofs[k] = ((q + glds_rot<T>(b)) % (2 * T)) * 16;
+    }
+    const uint8_t* src[PER_WAVE];
+    uint64_t ig = blockIdx.x, hg = blockIdx.x, ic = 0, hc = 0;  // issue / hash: group, tiles done
+    uint32_t it = 0, ht = 0;                                    // issue / hash: tile within the group
+    auto issue = [&](uint32_t slot) {
+        if (it == 0) {
+#pragma unroll
+            for (int k = 0; k < PER_WAVE; ++k) {
+                uint64_t gb = ig * BPW + prow[k];
+                if (gb >= n) gb = n - 1;  // shadow the last block; never stored
+                src[k] = base + gb * stride + pofs[k];
+            }
+        }
+        STORMCK_GLDS_ISSUE(src, lds + slot * TILE + wave * PER_WAVE * 1024, it, PER_WAVE, ROW, AUX);
+        if (++it == ntiles) {
+            it = 0;
+            ig += G;
+        }
+        ++ic;
+    };
+    const uint32_t b = tid >> 2, j = tid & 3;
+    const uint32_t rot = glds_rot<T>(b);
+    uint64_t acc = acc_seed(j);
+    if (ph == 0 && total > 0) issue(0);
+    for (uint64_t u = 0; u < steps; ++u) {
+        wait_vmcnt<0>();
+        __builtin_amdgcn_s_barrier();
+        if (u + 1 >= ph && ic < total) issue((u + 1) & 1);  // this wave's step u+1 into the other slot
+        if (u >= ph && hc < total) {
+            const uint8_t* row = lds + (u & 1) * TILE + b * ROW + (j & 1) * 8;
+#pragma unroll
+            for (int s = 0; s < T; ++s) {
+                const uint32_t q = (2 * s + (j >> 1) + 2 * T - rot) % (2 * T);
+                acc = round(acc, *reinterpret_cast<const uint64_t*>(row + q * 16));
+            }
+            if (++ht == ntiles) {
+                // the group's blocks are complete: remainder stripes and tail from global
+                // memory (none for 32 KiB blocks), then the checksum
+                const uint64_t gbk = hg * BPW + b;
+                const uint64_t gb = gbk < n ? gbk : n - 1;
+                const uint8_t* blk_src = base + gb * stride;
+                for (uint32_t s = ntiles * T; s < nst; ++s)
+                    acc = round(acc, reinterpret_cast<const uint64_t*>(blk_src)[4 * s + j]);
+                const uint64_t v1 = quad_bcast<0>(acc), v2 = quad_bcast<1>(acc), v3 = quad_bcast<2>(acc),
+                               v4 = quad_bcast<3>(acc);
+                if (j == 0 && gbk < n) {
+                    const uint64_t h = finish_fast(converge(v1, v2, v3, v4), len,
+                                                   blk_src + 32 * static_cast<uint64_t>(nst), len & 31);
+                    if constexpr (VERIFY) {
+                        if (h != expected[gbk]) {
+                            atomicMin(first_bad, static_cast<unsigned long long>(gbk));
+                            atomicAdd(n_bad, 1ULL);
+                        }
+                    } else {
+                        out[gbk] = h;
+                    }
+                }
+                acc = acc_seed(j);
+                ht = 0;
+                hg += G;
+            }
+            ++hc;
         }
     }
 }

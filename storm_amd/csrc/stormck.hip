@@ -138,6 +138,14 @@ constexpr uint32_t kMaxFanout = 1u << 16;
 // on each node, 64 nodes per workgroup, to keep every CU busy.
 constexpr uint64_t kWideNodes = 256;
 
+// Skewed persistent streaming kernel (k_xxh64_glds_skew): wave v starts kSkewTiles*v
+// tiles late, 4 KiB apart at 16-stripe tiles (profiles/r01_probe_phase_skew.txt). Its
+// first and last 7*kSkewTiles steps leave waves idle, so it runs only when every
+// workgroup has at least kSkewMinSteps tile steps (idle share <= 1.6%): for 32 KiB
+// blocks, batches of about 1.8M blocks and up (the bench's 4M-block passes).
+constexpr int kSkewTiles = 8;
+constexpr uint64_t kSkewMinSteps = 3584;
+
 // Cached answer to "is there a usable gfx950 device?" per process.
 int device_check() {
     static std::once_flag once;
@@ -161,6 +169,22 @@ int device_check() {
     return status;
 }
 
+// Compute units of the calling thread's current device (0 if unknown), cached per device.
+uint64_t cu_count() {
+    static std::atomic<int> cache[64] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+    int v = cache[dev].load(std::memory_order_relaxed);
+    if (v == 0) {
+        if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) {
+            (void)hipGetLastError();
+            return 0;
+        }
+        cache[dev].store(v, std::memory_order_relaxed);
+    }
+    return static_cast<uint64_t>(v);
+}
+
 bool grid_for(uint64_t threads, dim3* grid) {
     const uint64_t blocks = (threads + kThreads - 1) / kThreads;
     if (blocks == 0 || blocks > 0x7fffffffULL) return false;
@@ -178,7 +202,8 @@ int launch_checksum(const uint8_t* base, uint64_t stride, const uint32_t* lens, 
     //    batch over the chip; the streaming kernel's 128-block workgroups would occupy
     //    fewer than half of the CUs)
     //  * otherwise, uniform length, 16-byte aligned blocks at a fixed stride, at least
-    //    one LDS tile per block: LDS-staged streaming kernel (global_load_lds, nt)
+    //    one LDS tile per block: LDS-staged streaming kernel (global_load_lds, nt); its
+    //    persistent 4 KiB-skewed form when the batch gives every CU thousands of tiles
     if (n <= kWideBatch) {
 #define STORMCK_WIDE(LENS, OFFS, VER)                                                                           \
     hipLaunchKernelGGL((k_xxh64_wide<LENS, OFFS, VER>), dim3(static_cast<unsigned>(n)), dim3(kThreads), 0, st, base, \
@@ -202,6 +227,20 @@ int launch_checksum(const uint8_t* base, uint64_t stride, const uint32_t* lens, 
         len >= 32u * kTileStripes) {
         const uint64_t wgs = (n + kGldsBlocks - 1) / kGldsBlocks;
         if (wgs > 0x7fffffffULL) return fail(STORMCK_EINVAL, "batch too large for one launch");
+        const uint64_t cus = cu_count();
+        const uint64_t steps_per_wg = (wgs + cus - 1) / cus * ((len / 32) / kTileStripes);
+        if (cus > 0 && wgs >= cus && steps_per_wg >= kSkewMinSteps) {
+            // large batch: persistent workgroups, one per CU, waves' streams 4 KiB apart
+#define STORMCK_SKEW(VER)                                                                                        \
+    hipLaunchKernelGGL((k_xxh64_glds_skew<kTileStripes, kAuxNT, VER, kGldsWaves, kSkewTiles>),                 \
+                       dim3(static_cast<unsigned>(cus)), dim3(kGldsThreads), 0, st, base, stride, len, n, out,  \
+                       expected, first_bad, n_bad)
+            if (verify) STORMCK_SKEW(true);
+            else STORMCK_SKEW(false);
+#undef STORMCK_SKEW
+            HIP_TRY(hipGetLastError());
+            return STORMCK_OK;
+        }
         if (verify)
             hipLaunchKernelGGL((k_xxh64_glds<kTileStripes, kRing, kAuxNT, true, true, kGldsWaves>),
                                dim3(static_cast<unsigned>(wgs)), dim3(kGldsThreads), 0, st, base, stride, len, n, out,

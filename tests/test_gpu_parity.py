@@ -222,6 +222,38 @@ def _digest_check(dev, n_total, arena_blocks):
 
 
 @pytest.mark.slow
+@pytest.mark.parametrize("length", [28808, 32768])
+def test_large_batch_skewed_kernel(dev, length):
+    """Batches that give every CU thousands of tiles take the persistent, 4 KiB-skewed
+    streaming kernel (k_xxh64_glds_skew). 2.3M blocks, not a multiple of the 128-block
+    group, at a storm length with remainder stripes and a tail (28808 B: 56 tiles + 4
+    stripes + 8 B) and at 32 KiB: equal to the per-block-length (quad) path on every
+    block, to the oracle on a random sample, and verify finds planted mismatches."""
+    from oracle import oracle as o
+    from storm_amd import engine
+    n, stride = 2_300_003, 32768
+    arena = torch.empty((n, stride), dtype=torch.uint8, device=dev)
+    engine.fill_synthetic_device(arena.data_ptr(), stride, n, 77, o.SYNTH_SEED)
+    fast = engine.checksum_tensor(arena, length=length)
+    lens = torch.full((n,), length, dtype=torch.int32, device=dev)
+    quad = engine.checksum_tensor(arena, lens=lens)
+    torch.cuda.synchronize()
+    assert torch.equal(fast, quad)
+    rng = np.random.default_rng(length)
+    idx = np.concatenate([rng.integers(0, n, size=60), [0, 127, 128, n - 1]])
+    sample = arena[torch.from_numpy(idx).to(dev)].cpu().numpy()
+    assert np.array_equal(_u64(fast)[idx], o.checksum_batch(sample, len(idx), stride, length))
+    exp = fast.clone()
+    exp[n - 1] ^= 1
+    exp[1_000_000] ^= 1
+    res = torch.zeros(2, dtype=torch.int64, device=dev)
+    engine.verify_device(arena.data_ptr(), stride, n, exp.data_ptr(), res.data_ptr(), length)
+    torch.cuda.synchronize()
+    assert _u64(res).tolist() == [1_000_000, 2]
+    del arena, lens
+
+
+@pytest.mark.slow
 def test_c2_1m_blocks_digest(dev):
     _digest_check(dev, 1 << 20, 1 << 20)
 

@@ -7,7 +7,7 @@ import json
 import os
 import sys
 
-KERNEL = "k_xxh64_glds<16, 2, 2, true, false, 8>"
+KERNEL = "k_xxh64_glds_skew<16, 2, false, 8, 8>"  # rocprofv3 name of the dominant kernel
 
 
 def rows(path):
@@ -24,7 +24,7 @@ def main(d, arena):
     wk = sum(float(r["Counter_Value"]) for r in write) / len(write)
     hbm = fk * 1024 * corr + wk * 1024
     alg = arena * (32768 + 8)
-    out = {"kernel": "k_xxh64_glds<16,2,nt,8w>", "arena_blocks": arena, "fetch_size_kb": fk, "write_size_kb": wk,
+    out = {"kernel": "k_xxh64_glds_skew<16,nt,8w,4KiB>", "arena_blocks": arena, "fetch_size_kb": fk, "write_size_kb": wk,
            "fetch_correction": round(corr, 4), "hbm_bytes_per_launch": int(hbm),
            "algorithmic_bytes_per_launch": alg, "traffic_over_algorithmic": round(hbm / alg, 4),
            "source": os.path.relpath(d, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))}
