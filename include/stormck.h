@@ -203,7 +203,11 @@ typedef struct stormck_dirty_block {
  *    arena[origin_type] = type.
  * Writes out_checksums[i] (host) and updates blocks[i].address / birth_revision.
  * Synchronous on `stream`. Any children-first order is a valid storm commit order
- * (storm's own order follows Go map iteration); this one is deterministic. */
+ * (storm's own order follows Go map iteration); this one is deterministic.
+ * Argument errors (parent range, origin alignment, cycles) and a missing device are
+ * reported before anything is changed. A HIP failure part-way leaves the commit
+ * partly applied, as storm's own loop does on a write error; *last_allocated_block
+ * then still matches the relocations already written into blocks. */
 int stormck_commit_device(void* d_arena, stormck_dirty_block* blocks, uint64_t n, uint64_t revision,
                           uint64_t* last_allocated_block, uint64_t* out_checksums, void* stream);
 

@@ -176,10 +176,11 @@ func CommitBatch(arena []byte, dirty []DirtyBlock, revision uint64, lastAllocate
 	la := C.uint64_t(*lastAllocated)
 	rc := C.stormck_commit_device(dArena, (*C.stormck_dirty_block)(unsafe.Pointer(&dirty[0])), C.uint64_t(len(dirty)),
 		C.uint64_t(revision), &la, (*C.uint64_t)(unsafe.Pointer(&out[0])), nil)
+	// the library reports the relocations it applied to dirty, also on a failure part-way
+	*lastAllocated = BlockAddress(la)
 	if rc != C.STORMCK_OK {
 		return stormckError(rc)
 	}
-	*lastAllocated = BlockAddress(la)
 	return nil
 }
 
