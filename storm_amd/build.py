@@ -56,7 +56,19 @@ def build_oracle(force: bool = False) -> str:
     return out
 
 
-PROBES = ("probe", "probe_keys", "probe_small")  # tools/<name>.hip: design probes, not product
+PROBES = ("probe", "probe_keys", "probe_small", "alloc_probe", "phase_probe")  # tools/<name>.hip: design probes
+READPEAK = os.path.join(ROOT, "tools", "libreadpeak.so")  # bench.py's measured read peak (not product)
+
+
+def build_readpeak(force: bool = False) -> str:
+    """tools/libreadpeak.so: the shipped kernel's data movement without the hash, which
+    bench.py times on its own arena (measurement only)."""
+    srcs = [os.path.join(ROOT, "tools", "readpeak.hip"), os.path.join(CSRC, "kernels.h"),
+            os.path.join(CSRC, "xxh64_dev.h")]
+    if force or not _newer(READPEAK, srcs):
+        subprocess.run([hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-o", READPEAK,
+                        srcs[0]], check=True)
+    return READPEAK
 
 
 def build_probe(force: bool = False) -> str:
@@ -77,4 +89,5 @@ if __name__ == "__main__":
     print(build_lib(force))
     if "--all" in sys.argv:
         print(build_oracle(force))
+        print(build_readpeak(force))
         print(build_probe(force))

@@ -483,7 +483,9 @@ __global__ __launch_bounds__(64 * WAVES) void k_xxh64_glds(const uint8_t* __rest
 // A wave only reads the LDS rows it loaded itself (its own 16 blocks: T even), so the
 // skew needs no synchronisation beyond the ring's per-step barrier.
 // ---------------------------------------------------------------------------
-template <int T, int AUX, bool VERIFY, int WAVES, int SKEW>
+// HASH = false: the same data movement with the hash replaced by xor (the measured
+// read peak bench.py reports beside the kernel, tools/readpeak.hip).
+template <int T, int AUX, bool VERIFY, int WAVES, int SKEW, bool HASH = true>
 __global__ __launch_bounds__(64 * WAVES) void k_xxh64_glds_skew(const uint8_t* __restrict__ base, uint64_t stride,
                                                                 uint32_t len, uint64_t n, uint64_t* __restrict__ out,
                                                                 const uint64_t* __restrict__ expected,
@@ -548,7 +550,9 @@ __global__ __launch_bounds__(64 * WAVES) void k_xxh64_glds_skew(const uint8_t* _
 #pragma unroll
             for (int s = 0; s < T; ++s) {
                 const uint32_t q = (2 * s + (j >> 1) + 2 * T - rot) % (2 * T);
-                acc = round(acc, *reinterpret_cast<const uint64_t*>(row + q * 16));
+                const uint64_t w = *reinterpret_cast<const uint64_t*>(row + q * 16);
+                if constexpr (HASH) acc = round(acc, w);
+                else acc ^= w;
             }
             if (++ht == ntiles) {
                 // the group's blocks are complete: remainder stripes and tail from global

@@ -108,6 +108,45 @@ static std::string TestSingularity() {
     return hex(cs);
 }
 
+// cache/cache_test.go:260-300 (TestNewBlocksProduceConsistentResult): a struct with
+// padding, created twice in randomised memory with the same field values. newBlock
+// zeroes the slot first (cache/cache.go:282-284), so the two images, padding
+// included, and their checksums are identical; without the zeroing they differ.
+struct paddedStruct {
+    uint64_t Field1;
+    uint8_t Field2;
+    uint64_t Field3;
+};
+static_assert(sizeof(paddedStruct) == 24, "Go layout: 7 padding bytes after Field2");
+static void TestNewBlocksProduceConsistentResult() {
+    uint8_t slot1[sizeof(paddedStruct)], slot2[sizeof(paddedStruct)];
+    uint64_t x = 0x243F6A8885A308D3ULL;
+    for (size_t i = 0; i < sizeof slot1; ++i) {  // randomizeCache
+        x ^= x << 13; x ^= x >> 7; x ^= x << 17;
+        slot1[i] = static_cast<uint8_t>(x);
+        slot2[i] = static_cast<uint8_t>(x >> 8);
+    }
+    auto fill = [](uint8_t* slot, bool zero) {
+        if (zero) std::memset(slot, 0, sizeof(paddedStruct));  // newBlock
+        paddedStruct v;
+        std::memcpy(&v, slot, sizeof v);
+        v.Field1 = 1;
+        v.Field2 = 0x02;
+        v.Field3 = 3;
+        std::memcpy(slot, &v, sizeof v);
+    };
+    fill(slot1, true);
+    fill(slot2, true);
+    EXPECT(std::memcmp(slot1, slot2, sizeof slot1) == 0);
+    EXPECT(Checksum(slot1, sizeof slot1) == Checksum(slot2, sizeof slot2));
+    uint8_t dirty1[sizeof slot1], dirty2[sizeof slot2];
+    std::memset(dirty1, 0xAB, sizeof dirty1);
+    std::memset(dirty2, 0xCD, sizeof dirty2);
+    fill(dirty1, false);
+    fill(dirty2, false);
+    EXPECT(Checksum(dirty1, sizeof dirty1) != Checksum(dirty2, sizeof dirty2));  // padding is hashed
+}
+
 // blocks.Checksum on "abc" and the empty slice (public XXH64 answers)
 static void TestKnownAnswers() {
     EXPECT(Checksum("abc", 3) == 0x44BC2CF5AD770999ULL);
@@ -148,6 +187,7 @@ int main() {
     std::string sing = TestSingularity();
     TestKnownAnswers();
     TestBatch();
+    TestNewBlocksProduceConsistentResult();
     std::printf("{\"pointer_block_test_sequence\": %s, \"blob_test_block\": %s, \"singularity\": %s, "
                 "\"zero\": {\"prod\": {\"pointer\": %s, \"objectlist\": %s, \"spacelist\": %s, \"blob\": %s, "
                 "\"singularity\": %s}, \"test\": {\"pointer\": %s, \"objectlist\": %s, \"spacelist\": %s}}, "
