@@ -7,6 +7,7 @@ from them, and per-shard roots gathered over RCCL. Submodules:
 * ``blocks``   — Go ``blocks`` API mirror (Checksum, BlockChecksum, VerifyChecksum, batches)
 * ``layouts``  — storm block structs (pointer, blob, objectlist, spacelist, singularity)
 * ``engine``   — device-resident entry points (raw pointers / torch tensors)
+* ``commit``   — f1: level-synchronous Cache.Commit of a dirty forest (stormck_commit_device)
 * ``dist``     — shard planning and the root all-gather
 * ``build``    — in-tree hipcc build of libstormck.so
 """
