@@ -47,6 +47,58 @@ static uint64_t host_xxh64(const uint8_t* p, uint64_t n) {
     return h;
 }
 
+namespace stormck {
+// CANDIDATE: workgroup-synchronised, persistent LDS-DMA ring for fixed-stride keys (the
+// streaming checksum kernel's scheme applied to keys). A tile is WAVES x BW batches of
+// 64 keys, contiguous in memory (BW * 3 KiB per wave at 48-byte keys); each wave loads
+// and hashes its own batches; tile t+1 is in flight while tile t hashes; one barrier per
+// tile so every tile leaves as one burst. Workgroups walk tiles blockIdx.x + k*gridDim.x.
+template <int P, int BW, int WAVES, int KLEN>
+__global__ __launch_bounds__(64 * WAVES) void k_key_tags_wg(const uint8_t* __restrict__ keys, uint64_t batches,
+                                                            uint64_t* __restrict__ out) {
+    constexpr uint32_t kStride = 16 * P, kRegion = 64 * kStride;   // one batch
+    constexpr uint32_t kWaveBytes = BW * kRegion, kTile = WAVES * kWaveBytes;
+    __shared__ __attribute__((aligned(16))) uint8_t lds[2 * kTile];
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint64_t bpt = static_cast<uint64_t>(WAVES) * BW;        // batches per tile
+    const uint64_t ntile = batches / bpt;                          // whole tiles only (host handles the rest)
+    const uint64_t G = gridDim.x;
+    if (blockIdx.x >= ntile) return;
+    const uint64_t steps = (ntile - blockIdx.x + G - 1) / G;
+    auto issue = [&](uint64_t tile, uint32_t slot) {
+        const uint8_t* s_ = keys + (tile * bpt + static_cast<uint64_t>(wave) * BW) * kRegion + lane * 16;
+        uint8_t* d_ = lds + slot * kTile + wave * kWaveBytes;
+#pragma unroll
+        for (int p_ = 0; p_ < static_cast<int>(BW * P); ++p_)
+            __builtin_amdgcn_global_load_lds(s_ + p_ * 1024, d_ + p_ * 1024, 16, 0, 2);
+    };
+    issue(blockIdx.x, 0);
+    for (uint64_t u = 0; u < steps; ++u) {
+        wait_vmcnt<0>();
+        __builtin_amdgcn_s_barrier();
+        const uint64_t tile = blockIdx.x + u * G;
+        if (u + 1 < steps) issue(tile + G, (u + 1) & 1);
+#pragma unroll
+        for (int bb = 0; bb < BW; ++bb) {
+            const uint8_t* k = lds + (u & 1) * kTile + wave * kWaveBytes + bb * kRegion + lane * kStride;
+            uint64_t v1 = kV1, v2 = kV2, v3 = kV3, v4 = kV4;
+#pragma unroll
+            for (uint32_t s = 0; s < KLEN / 32; ++s) {
+                const u64x2 x = *reinterpret_cast<const u64x2*>(k + 32 * s);
+                const u64x2 y = *reinterpret_cast<const u64x2*>(k + 32 * s + 16);
+                v1 = round(v1, x.x);
+                v2 = round(v2, x.y);
+                v3 = round(v3, y.x);
+                v4 = round(v4, y.y);
+            }
+            const uint64_t h = finish_lds16(KLEN >= 32 ? converge(v1, v2, v3, v4) : kP5, KLEN, k + 32 * (KLEN / 32),
+                                            KLEN & 31);
+            out[(tile * bpt + static_cast<uint64_t>(wave) * BW + bb) * 64 + lane] = h;
+        }
+    }
+}
+}  // namespace stormck
+
 struct Timer {
     hipEvent_t a, b;
     Timer() { CK(hipEventCreate(&a)); CK(hipEventCreate(&b)); }
@@ -88,7 +140,13 @@ int main(int argc, char** argv) {
         const uint64_t waves = (batches + PW - 1) / PW;                                                    \
         hipLaunchKernelGGL((k_key_tags_ring<2, 3, RING, PW>), dim3((unsigned)((waves + 3) / 4)), dim3(256), \
                            4 * RING * 64 * klen, 0, keys, klen, batches, out); }})
-    RV(2, 8); RV(3, 8); RV(3, 16); RV(4, 8); RV(4, 16); RV(5, 16); RV(6, 16);
+    RV(4, 8);
+    hipDeviceProp_t prop; CK(hipGetDeviceProperties(&prop, 0));
+    const unsigned cus = (unsigned)prop.multiProcessorCount;
+#define WG(BW, MULT)                                                                                        \
+    vs.push_back({"wg ring BW=" #BW " grid=" #MULT "xCU", [&] {                                            \
+        hipLaunchKernelGGL((k_key_tags_wg<3, BW, 8, 48>), dim3(cus * MULT), dim3(512), 0, 0, keys, batches, out); }})
+    WG(1, 1); WG(2, 1); WG(3, 1); WG(1, 2); WG(1, 3);
     std::vector<std::vector<double>> gks(vs.size());
     for (int r = 0; r < rounds; ++r)
         for (size_t v = 0; v < vs.size(); ++v) {
