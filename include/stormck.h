@@ -106,7 +106,8 @@ int stormck_host_unregister(void* p);
 /* Device-visible address of host memory registered with stormck_host_register: the
  * *_device entry points (stormck_commit_device's arena included) then read and write
  * it in place over PCIe. This runs f1 on storm's cache.data where it lives, in host
- * memory (cache/cache.go:36-40), at link rate instead of HBM rate. */
+ * memory (cache/cache.go:36-40), at link rate instead of HBM rate. Block rows must be
+ * 256-byte aligned for that (a 16-byte offset costs about a quarter of the rate). */
 int stormck_host_device_pointer(void* p, void** d_p);
 
 /* ---- Merkle pointer tree (storm pointer.Block nodes) -----------------------

@@ -24,6 +24,17 @@ sys.path.insert(0, ROOT)
 BLOCK = 32768
 
 
+def aligned_empty(nbytes: int, align: int = 1 << 21):
+    """uint8 array whose data starts on an `align` boundary. Kernels reading host memory
+    in place need 256-byte aligned rows to run at the PCIe link rate (38 GiB/s at
+    +16 B vs 51 GiB/s aligned, profiles/r01_probe_host_gather.txt); numpy only aligns
+    to 16 B. storm's cache.data, a large Go allocation, is page-aligned."""
+    import numpy as np
+    raw = np.empty(nbytes + align, dtype=np.uint8)
+    off = (-raw.ctypes.data) % align
+    return raw[off:off + nbytes]
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gib", type=float, default=8.0)
@@ -40,7 +51,7 @@ def main():
     engine.fill_synthetic_device(d.data_ptr(), BLOCK, n, 0, 0x53544F524D)
     ref = engine.checksum_tensor(d)
     torch.cuda.synchronize()
-    host = np.empty((n, BLOCK), dtype=np.uint8)
+    host = aligned_empty(n * BLOCK).reshape(n, BLOCK)
     torch.from_numpy(host).copy_(d)
     want = ref.cpu().numpy().view(np.uint64)
     del d
@@ -103,7 +114,8 @@ def main():
     from storm_amd import commit as sc
     nl = 32768
     bf, size, last = sc.pointer_forest(nl, BLOCK, 1200, slot=BLOCK, revision=1)
-    arena = np.zeros(size, dtype=np.uint8)
+    arena = aligned_empty(size)
+    arena[:] = 0
     arena[BLOCK:BLOCK + nl * BLOCK] = host[:nl].reshape(-1) if nl <= n else 0
     blocks.RegisterHostMemory(arena)
     try:

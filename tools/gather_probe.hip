@@ -10,6 +10,7 @@
 #include <numeric>
 #include <random>
 #include <vector>
+#include <sys/mman.h>
 #include "../storm_amd/csrc/kernels.h"
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { fprintf(stderr, "HIP %s at %s:%d\n", hipGetErrorString(e), __FILE__, __LINE__); exit(1);} } while (0)
@@ -60,6 +61,68 @@ int main(int argc, char** argv) {
     rate("quad gather kernel reading host in place", [&] {
         hipLaunchKernelGGL((k_xxh64_quad<16, false, true, false>), dim3((unsigned)((n * 4 + 255) / 256)), dim3(256), 0, st,
                            dhost, 0, nullptr, (uint32_t)L, offs, n, out, nullptr, nullptr, nullptr); });
+    // contiguous blocks read in place by each streaming kernel (the device entry point on a
+    // registered host arena picks by batch size; which kernel reads PCIe best?)
+    rate("glds streaming kernel, contiguous host blocks", [&] {
+        hipLaunchKernelGGL((k_xxh64_glds<16, 2, 2, true, false, 8>), dim3((unsigned)((n + 127) / 128)), dim3(512), 0, st,
+                           dhost, L, (uint32_t)L, n, out, nullptr, nullptr, nullptr); });
+    rate("quad kernel, contiguous host blocks", [&] {
+        hipLaunchKernelGGL((k_xxh64_quad<16, false, false, false>), dim3((unsigned)((n * 4 + 255) / 256)), dim3(256), 0, st,
+                           dhost, L, nullptr, (uint32_t)L, nullptr, n, out, nullptr, nullptr, nullptr); });
+    rate("glds streaming kernel, contiguous, default policy", [&] {
+        hipLaunchKernelGGL((k_xxh64_glds<16, 2, 0, true, false, 8>), dim3((unsigned)((n + 127) / 128)), dim3(512), 0, st,
+                           dhost, L, (uint32_t)L, n, out, nullptr, nullptr, nullptr); });
+    // the same kernels on malloc'd memory page-locked with hipHostRegister (how a Go
+    // caller's cache.data would be pinned) instead of hipHostMalloc
+    uint8_t* reg = static_cast<uint8_t*>(aligned_alloc(1 << 21, n * L));
+    for (uint64_t i = 0; i < n * L; i += 4096) reg[i] = static_cast<uint8_t>(i >> 12);
+    CK(hipHostRegister(reg, n * L, hipHostRegisterMapped));
+    uint8_t* dreg = nullptr;
+    CK(hipHostGetDevicePointer(reinterpret_cast<void**>(&dreg), reg, 0));
+    rate("registered malloc: contiguous DMA", [&] { CK(hipMemcpyAsync(d, reg, n * L, hipMemcpyHostToDevice, st)); });
+    rate("registered malloc: glds streaming kernel", [&] {
+        hipLaunchKernelGGL((k_xxh64_glds<16, 2, 2, true, false, 8>), dim3((unsigned)((n + 127) / 128)), dim3(512), 0, st,
+                           dreg, L, (uint32_t)L, n, out, nullptr, nullptr, nullptr); });
+    rate("registered malloc: quad kernel", [&] {
+        hipLaunchKernelGGL((k_xxh64_quad<16, false, false, false>), dim3((unsigned)((n * 4 + 255) / 256)), dim3(256), 0, st,
+                           dreg, L, nullptr, (uint32_t)L, nullptr, n, out, nullptr, nullptr, nullptr); });
+    CK(hipHostUnregister(reg));
+    free(reg);
+    // base alignment: the same registered buffer read from +16 and +64 bytes (a 16-byte
+    // aligned allocation, as numpy's, vs a cache-line aligned one, as Go's large objects)
+    {
+        uint8_t* r3 = static_cast<uint8_t*>(aligned_alloc(1 << 21, n * L + 4096));
+        for (uint64_t i = 0; i < n * L + 4096; i += 4096) r3[i] = 1;
+        CK(hipHostRegister(r3, n * L + 4096, hipHostRegisterMapped));
+        uint8_t* dr3 = nullptr;
+        CK(hipHostGetDevicePointer(reinterpret_cast<void**>(&dr3), r3, 0));
+        for (uint64_t shift : {16ULL, 64ULL, 256ULL}) {
+            char name[80];
+            snprintf(name, sizeof name, "glds streaming kernel, base %% 4096 = %llu", (unsigned long long)shift);
+            rate(name, [&] {
+                hipLaunchKernelGGL((k_xxh64_glds<16, 2, 2, true, false, 8>), dim3((unsigned)((n + 127) / 128)), dim3(512), 0,
+                                   st, dr3 + shift, L, (uint32_t)L, n, out, nullptr, nullptr, nullptr); });
+        }
+        CK(hipHostUnregister(r3));
+        free(r3);
+    }
+    // the same with transparent huge pages refused (4 KiB pages, as most heaps get)
+    for (int huge = 0; huge < 2; ++huge) {
+        uint8_t* r2 = static_cast<uint8_t*>(aligned_alloc(1 << 21, n * L));
+        madvise(r2, n * L, huge ? MADV_HUGEPAGE : MADV_NOHUGEPAGE);
+        for (uint64_t i = 0; i < n * L; i += 4096) r2[i] = static_cast<uint8_t>(i >> 12);
+        CK(hipHostRegister(r2, n * L, hipHostRegisterMapped));
+        uint8_t* dr2 = nullptr;
+        CK(hipHostGetDevicePointer(reinterpret_cast<void**>(&dr2), r2, 0));
+        rate(huge ? "MADV_HUGEPAGE: glds streaming kernel" : "MADV_NOHUGEPAGE: glds streaming kernel", [&] {
+            hipLaunchKernelGGL((k_xxh64_glds<16, 2, 2, true, false, 8>), dim3((unsigned)((n + 127) / 128)), dim3(512), 0,
+                               st, dr2, L, (uint32_t)L, n, out, nullptr, nullptr, nullptr); });
+        rate(huge ? "MADV_HUGEPAGE: quad gather, scattered" : "MADV_NOHUGEPAGE: quad gather, scattered", [&] {
+            hipLaunchKernelGGL((k_xxh64_quad<16, false, false, false>), dim3((unsigned)((n * 4 + 255) / 256)), dim3(256), 0,
+                               st, dr2, L, nullptr, (uint32_t)L, nullptr, n, out, nullptr, nullptr, nullptr); });
+        CK(hipHostUnregister(r2));
+        free(r2);
+    }
     printf("done\n");
     return 0;
 }
