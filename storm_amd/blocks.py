@@ -171,8 +171,14 @@ def ReadVerifyBatch(fd: int, addresses, lens, expected, dst, dst_stride: int, bl
 def RegisterHostMemory(buf) -> None:
     """Page-lock a long-lived host buffer (storm's cache.data, allocated once in
     cache.New, cache/cache.go:36-40): host batches then DMA straight from it, and
-    HostDevicePointer gives kernels in-place access to it."""
+    HostDevicePointer gives kernels in-place access to it. Kernels reading it in place
+    run at the PCIe link rate only from 256-byte aligned rows; a
+    misaligned buffer works, more slowly, and draws a warning."""
     a = _as_u8(buf)
+    if a.ctypes.data % 256:
+        import warnings
+        warnings.warn(f"host buffer at {a.ctypes.data:#x} is not 256-byte aligned: in-place device reads of it "
+                      "run at about 70% of the PCIe link rate", RuntimeWarning, stacklevel=2)
     _lib.check(_lib.lib.stormck_host_register(a.ctypes.data, a.nbytes))
 
 
