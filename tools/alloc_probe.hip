@@ -2,6 +2,7 @@
 // Bench runs in separate processes differ by ~2% while every process is steady
 // (DESIGN.md §5). One process: several 128 GiB arenas from hipMalloc and
 // hipExtMallocWithFlags(hipDeviceMallocContiguous), each filled and timed.
+// Times the shipped large-batch kernel (k_xxh64_glds_skew, 256 workgroups).
 // Usage: alloc_probe [GiB=128] [reps=5]
 #include <hip/hip_runtime.h>
 #include <stdio.h>
@@ -22,7 +23,7 @@ static double time_arena(uint8_t* d, uint64_t n, uint64_t* out, int reps) {
     std::vector<float> ms;
     for (int r = 0; r < reps + 1; ++r) {
         CK(hipEventRecord(a, 0));
-        hipLaunchKernelGGL((k_xxh64_glds<16, 2, 2, true, false, 8>), dim3((unsigned)((n + 127) / 128)), dim3(512), 0, 0,
+        hipLaunchKernelGGL((k_xxh64_glds_skew<16, 2, false, 8, 8>), dim3(256), dim3(512), 0, 0,
                            d, L, (uint32_t)L, n, out, nullptr, nullptr, nullptr);
         CK(hipEventRecord(b, 0)); CK(hipEventSynchronize(b));
         float t; CK(hipEventElapsedTime(&t, a, b));
@@ -56,6 +57,18 @@ int main(int argc, char** argv) {
     } else {
         printf("contiguous allocation of %.0f GiB failed: %s\n", gib, hipGetErrorString(e));
         (void)hipGetLastError();
+    }
+    // memory types: fine-grained and uncached device memory (MTYPE) instead of the default
+    for (unsigned flags : {static_cast<unsigned>(hipDeviceMallocFinegrained), static_cast<unsigned>(hipDeviceMallocUncached)}) {
+        uint8_t* F = nullptr;
+        hipError_t ef = hipExtMallocWithFlags((void**)&F, bytes, flags);
+        if (ef == hipSuccess) {
+            report(flags == hipDeviceMallocFinegrained ? "hipExtMallocWithFlags fine-grained" : "hipExtMallocWithFlags uncached", F);
+            CK(hipFree(F));
+        } else {
+            printf("flags %u allocation failed: %s\n", flags, hipGetErrorString(ef));
+            (void)hipGetLastError();
+        }
     }
     // eight small allocations in a row, then a big one after them
     std::vector<uint8_t*> small(8);
