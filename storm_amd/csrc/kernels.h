@@ -275,6 +275,37 @@ __global__ __launch_bounds__(256) void k_xxh64_single(const uint8_t* __restrict_
 // ---------------------------------------------------------------------------
 constexpr uint32_t kWideMax = 32 * 1024;
 
+// Quad 0's part of k_xxh64_wide. Inlined once per branch, so the words are read with
+// ds_read from the staged copy and with global loads otherwise: through one generic
+// pointer both would be flat loads, which the compiler can only wait for all at once
+// (s_waitcnt vmcnt(0) lgkmcnt(0) per group, no prefetch overlap).
+template <bool VERIFY>
+__device__ __forceinline__ void wide_hash(const uint8_t* s, uint32_t L, uint64_t blk, uint64_t* __restrict__ out,
+                                          const uint64_t* __restrict__ expected,
+                                          unsigned long long* __restrict__ first_bad,
+                                          unsigned long long* __restrict__ n_bad) {
+    const uint32_t j = threadIdx.x;
+    const uint32_t nst = L >> 5;
+    uint64_t acc = acc_seed(j);
+    if ((reinterpret_cast<uintptr_t>(s) & 7) == 0)
+        acc = quad_stripes_aligned<16>(reinterpret_cast<const uint64_t*>(s) + j, nst, acc);
+    else
+        acc = quad_stripes_unaligned(s + 8 * j, nst, acc);
+    const uint64_t v1 = quad_bcast<0>(acc), v2 = quad_bcast<1>(acc), v3 = quad_bcast<2>(acc), v4 = quad_bcast<3>(acc);
+    if (j == 0) {
+        const uint64_t h0 = (L >= 32) ? converge(v1, v2, v3, v4) : kP5;
+        const uint64_t h = finish_fast(h0, L, s + 32 * static_cast<uint64_t>(nst), L & 31);
+        if (VERIFY) {
+            if (h != expected[blk]) {
+                atomicMin(first_bad, static_cast<unsigned long long>(blk));
+                atomicAdd(n_bad, 1ULL);
+            }
+        } else {
+            out[blk] = h;
+        }
+    }
+}
+
 template <bool LENS, bool OFFS, bool VERIFY>
 __global__ __launch_bounds__(256) void k_xxh64_wide(const uint8_t* __restrict__ base, uint64_t stride,
                                                       const uint32_t* __restrict__ lens, uint32_t len,
@@ -289,7 +320,6 @@ __global__ __launch_bounds__(256) void k_xxh64_wide(const uint8_t* __restrict__ 
     const uint32_t L = LENS ? lens[blk] : len;
     const uint32_t shift = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(src) & 15);
     const uint32_t words = (shift + L + 15) / 16;
-    const uint8_t* s = src;
     if (words <= kWideMax / 16) {
         // a 16-byte window holding a byte of the block lies in that byte's page
         const uint4* cover = reinterpret_cast<const uint4*>(src - shift);
@@ -305,27 +335,12 @@ __global__ __launch_bounds__(256) void k_xxh64_wide(const uint8_t* __restrict__ 
             default: single_stage<8>(cover, buf, words); break;
         }
         __syncthreads();
-        s = reinterpret_cast<const uint8_t*>(buf) + shift;
+        if (threadIdx.x >= 4) return;
+        wide_hash<VERIFY>(reinterpret_cast<const uint8_t*>(buf) + shift, L, blk, out, expected, first_bad, n_bad);
+        return;
     }
     if (threadIdx.x >= 4) return;
-    const uint32_t j = threadIdx.x;
-    const uint32_t nst = L >> 5;
-    uint64_t acc = acc_seed(j);
-    if ((shift & 7) == 0) acc = quad_stripes_aligned<16>(reinterpret_cast<const uint64_t*>(s) + j, nst, acc);
-    else acc = quad_stripes_unaligned(s + 8 * j, nst, acc);
-    const uint64_t v1 = quad_bcast<0>(acc), v2 = quad_bcast<1>(acc), v3 = quad_bcast<2>(acc), v4 = quad_bcast<3>(acc);
-    if (j == 0) {
-        const uint64_t h0 = (L >= 32) ? converge(v1, v2, v3, v4) : kP5;
-        const uint64_t h = finish_fast(h0, L, s + 32 * static_cast<uint64_t>(nst), L & 31);
-        if (VERIFY) {
-            if (h != expected[blk]) {
-                atomicMin(first_bad, static_cast<unsigned long long>(blk));
-                atomicAdd(n_bad, 1ULL);
-            }
-        } else {
-            out[blk] = h;
-        }
-    }
+    wide_hash<VERIFY>(src, L, blk, out, expected, first_bad, n_bad);
 }
 
 // ---------------------------------------------------------------------------
