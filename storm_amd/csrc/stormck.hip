@@ -130,7 +130,15 @@ constexpr unsigned kGldsThreads = 64 * kGldsWaves;
 constexpr unsigned kGldsBlocks = 16 * kGldsWaves;
 constexpr int kAuxNT = 2;
 constexpr uint64_t kWideBatch = 128;      // batches up to this many blocks: k_xxh64_wide
-constexpr uint64_t kStreamBatch = 16384;  // uniform batches from this many blocks: k_xxh64_glds
+constexpr uint64_t kStreamBatch = 16384;  // f1 commit levels from this many blocks: k_commit_level_glds
+// Uniform batches take the LDS-staged kernel from kMidBatch blocks. Below kBigBatch its
+// workgroups are 2 waves (32 blocks, 16 KiB of ring) rather than 8 (128 blocks, 128 KiB):
+// 16,384 blocks in 8-wave workgroups fill only 128 of the 256 CUs
+// (profiles/r01_chain/mid_sweep.txt: 16,384 blocks in 84 us instead of 110; 12,288 in 67
+// instead of the register quad's 76).
+constexpr uint64_t kMidBatch = 10240;
+constexpr uint64_t kBigBatch = 24576;
+constexpr int kMidWaves = 2;
 constexpr unsigned kThreads = 256;
 constexpr uint32_t kMaxFanout = 1u << 16;
 // Merkle levels of at most this many nodes take one workgroup per node (k_pointer_level_wide):
@@ -198,12 +206,13 @@ int launch_checksum(const uint8_t* base, uint64_t stride, const uint32_t* lens, 
     const bool verify = expected != nullptr;
     // Batch-size dispatch (profiles/r01_probe_small.txt, us per launch at 32 KiB):
     //  * n <= kWideBatch: one workgroup per block, whole block staged in one round trip
-    //  * n <  kStreamBatch: register quad kernel (64 blocks per workgroup spread the
+    //  * n <  kMidBatch: register quad kernel (64 blocks per workgroup spread the
     //    batch over the chip; the streaming kernel's 128-block workgroups would occupy
     //    fewer than half of the CUs)
     //  * otherwise, uniform length, 16-byte aligned blocks at a fixed stride, at least
-    //    one LDS tile per block: LDS-staged streaming kernel (global_load_lds, nt); its
-    //    persistent 4 KiB-skewed form when the batch gives every CU thousands of tiles
+    //    one LDS tile per block: LDS-staged streaming kernel (global_load_lds, nt), in
+    //    2-wave workgroups below kBigBatch; its persistent 4 KiB-skewed form when the
+    //    batch gives every CU thousands of tiles
     if (n <= kWideBatch) {
 #define STORMCK_WIDE(LENS, OFFS, VER)                                                                           \
     hipLaunchKernelGGL((k_xxh64_wide<LENS, OFFS, VER>), dim3(static_cast<unsigned>(n)), dim3(kThreads), 0, st, base, \
@@ -223,8 +232,19 @@ int launch_checksum(const uint8_t* base, uint64_t stride, const uint32_t* lens, 
         HIP_TRY(hipGetLastError());
         return STORMCK_OK;
     }
-    if (n >= kStreamBatch && !lens && !offs && (reinterpret_cast<uintptr_t>(base) & 15) == 0 && (stride & 15) == 0 &&
+    if (n >= kMidBatch && !lens && !offs && (reinterpret_cast<uintptr_t>(base) & 15) == 0 && (stride & 15) == 0 &&
         len >= 32u * kTileStripes) {
+        if (n < kBigBatch) {
+            const dim3 grid(static_cast<unsigned>((n + 16 * kMidWaves - 1) / (16 * kMidWaves)));
+            if (verify)
+                hipLaunchKernelGGL((k_xxh64_glds<kTileStripes, kRing, kAuxNT, true, true, kMidWaves, false>), grid,
+                                   dim3(64 * kMidWaves), 0, st, base, stride, len, n, out, expected, first_bad, n_bad);
+            else
+                hipLaunchKernelGGL((k_xxh64_glds<kTileStripes, kRing, kAuxNT, true, false, kMidWaves, false>), grid,
+                                   dim3(64 * kMidWaves), 0, st, base, stride, len, n, out, expected, first_bad, n_bad);
+            HIP_TRY(hipGetLastError());
+            return STORMCK_OK;
+        }
         const uint64_t wgs = (n + kGldsBlocks - 1) / kGldsBlocks;
         if (wgs > 0x7fffffffULL) return fail(STORMCK_EINVAL, "batch too large for one launch");
         const uint64_t cus = cu_count();

@@ -122,8 +122,9 @@ def test_synth_vs_oracle_random_lengths(dev):
 @pytest.mark.parametrize("length", [512, 513, 520, 1000, 8192, 28808, 30000, 31808, 32768])
 def test_uniform_fast_path_lengths(dev, length):
     """Uniform-length 16-byte-aligned batches of every batch-size class: <= 128 blocks
-    (one workgroup per block), < 16384 (register quad), >= 16384 (LDS-staged streaming
-    kernel: whole tiles, remainder stripes and tails, partial last workgroup)."""
+    (one workgroup per block), < 10240 (register quad), >= 10240 (LDS-staged streaming
+    kernel in 2- then 8-wave workgroups: whole tiles, remainder stripes and tails,
+    partial last workgroup)."""
     from oracle import oracle as o
     from storm_amd import engine
     rng = np.random.default_rng(length)
@@ -151,22 +152,25 @@ def test_uniform_fast_path_lengths(dev, length):
     engine.verify_device(d.data_ptr(), stride, 1000, exp.data_ptr(), res.data_ptr(), length)
     torch.cuda.synchronize()
     assert _u64(res).tolist() == [500, 2]
-    # streaming-kernel batch: device-generated blocks, n % 128 != 0, then verify
-    n = 16384 + 65
-    big = torch.empty((n, stride), dtype=torch.uint8, device=dev)
-    engine.fill_synthetic_device(big.data_ptr(), stride, n, length, 0x1234)
-    out = engine.checksum_tensor(big, length=length)
-    torch.cuda.synchronize()
-    want = o.checksum_batch(big.cpu().numpy(), n, stride, length, threads=8)
-    assert np.array_equal(_u64(out), want), (length, n)
-    exp = torch.from_numpy(want.view(np.int64).copy()).to(dev)
-    exp[n - 1] ^= 1
-    exp[16400] ^= 1
-    exp[7] ^= 1
-    res = torch.zeros(2, dtype=torch.int64, device=dev)
-    engine.verify_device(big.data_ptr(), stride, n, exp.data_ptr(), res.data_ptr(), length)
-    torch.cuda.synchronize()
-    assert _u64(res).tolist() == [7, 3]
+    # streaming-kernel batches: device-generated blocks, partial last workgroups, then
+    # verify. 10,257 takes the 2-wave workgroups (kMidBatch..kBigBatch), 24,641 the
+    # 8-wave ones.
+    for n in (10240 + 17, 24576 + 65):
+        big = torch.empty((n, stride), dtype=torch.uint8, device=dev)
+        engine.fill_synthetic_device(big.data_ptr(), stride, n, length, 0x1234)
+        out = engine.checksum_tensor(big, length=length)
+        torch.cuda.synchronize()
+        want = o.checksum_batch(big.cpu().numpy(), n, stride, length, threads=8)
+        assert np.array_equal(_u64(out), want), (length, n)
+        exp = torch.from_numpy(want.view(np.int64).copy()).to(dev)
+        exp[n - 1] ^= 1
+        exp[10000] ^= 1
+        exp[7] ^= 1
+        res = torch.zeros(2, dtype=torch.int64, device=dev)
+        engine.verify_device(big.data_ptr(), stride, n, exp.data_ptr(), res.data_ptr(), length)
+        torch.cuda.synchronize()
+        assert _u64(res).tolist() == [7, 3], (length, n)
+        del big
 
 
 def test_mixed_c5(dev):

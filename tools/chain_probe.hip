@@ -13,6 +13,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <functional>
+#include <string>
 #include <utility>
 #include <vector>
 
@@ -260,8 +261,73 @@ __global__ __launch_bounds__(256) void k_bound(const uint8_t* __restrict__ base,
     if (blk_raw < n && j == 0) out[blk] = acc;
 }
 
+// Mid-size batches (8K..128K blocks of 32 KiB): workgroup size of the LDS-DMA streaming
+// kernel. 8 waves x 16 blocks put 128 blocks and 128 KiB of LDS ring on one CU, so a
+// 16K-block batch occupies only 128 of 256 CUs.
+static int mid_sweep(int reps) {
+    const uint64_t L = 32768, NMAX = 131072;
+    uint8_t* d; CK(hipMalloc(&d, NMAX * L));
+    uint64_t* out; CK(hipMalloc(&out, NMAX * 8));
+    hipLaunchKernelGGL(k_fill_synthetic, dim3(8192), dim3(256), 0, 0, d, L, NMAX, 0ULL, 0x53544f524dULL);
+    CK(hipDeviceSynchronize());
+    const uint64_t K = 256;
+    std::vector<uint8_t> hb(L);
+    std::vector<uint64_t> ref(K), got(K);
+    std::vector<uint64_t> idx(K);
+    for (uint64_t i = 0; i < K; ++i) idx[i] = (i * 2654435761ULL) % 8192;
+    for (uint64_t i = 0; i < K; ++i) { CK(hipMemcpy(hb.data(), d + idx[i] * L, L, hipMemcpyDeviceToHost)); ref[i] = host_xxh64(hb.data(), L); }
+    hipEvent_t a, b; CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
+    auto timeit = [&](const std::function<void()>& f) {
+        CK(hipEventRecord(a, 0));
+        for (int r = 0; r < reps; ++r) f();
+        CK(hipEventRecord(b, 0)); CK(hipEventSynchronize(b));
+        float ms; CK(hipEventElapsedTime(&ms, a, b));
+        return ms * 1e3 / reps;
+    };
+    int bad_total = 0;
+    printf("%7s %9s %9s %9s %9s %9s %9s   (us per launch; GB/s of the best in the last column)\n", "n", "quad", "glds8w",
+           "glds4w", "glds2w", "glds1w", "glds1w-R4");
+    for (uint64_t n : {8192ULL, 12288ULL, 16384ULL, 24576ULL, 32768ULL, 49152ULL, 65536ULL, 131072ULL}) {
+        const unsigned gq = (unsigned)((n * 4 + 255) / 256);
+        auto G = [&](unsigned bpw) { return dim3((unsigned)((n + bpw - 1) / bpw)); };
+        std::vector<std::pair<const char*, std::function<void()>>> fs = {
+            {"quad", [&] { hipLaunchKernelGGL((k_xxh64_quad<16, false, false, false>), dim3(gq), dim3(256), 0, 0, d, L, nullptr, (uint32_t)L, nullptr, n, out, nullptr, nullptr, nullptr); }},
+            {"glds8w", [&] { hipLaunchKernelGGL((k_xxh64_glds<16, 2, 2, true, false, 8>), G(128), dim3(512), 0, 0, d, L, (uint32_t)L, n, out, nullptr, nullptr, nullptr); }},
+            {"glds4w", [&] { hipLaunchKernelGGL((k_xxh64_glds<16, 2, 2, true, false, 4, false>), G(64), dim3(256), 0, 0, d, L, (uint32_t)L, n, out, nullptr, nullptr, nullptr); }},
+            {"glds2w", [&] { hipLaunchKernelGGL((k_xxh64_glds<16, 2, 2, true, false, 2, false>), G(32), dim3(128), 0, 0, d, L, (uint32_t)L, n, out, nullptr, nullptr, nullptr); }},
+            {"glds1w", [&] { hipLaunchKernelGGL((k_xxh64_glds<16, 2, 2, true, false, 1, false>), G(16), dim3(64), 0, 0, d, L, (uint32_t)L, n, out, nullptr, nullptr, nullptr); }},
+            {"glds1w-R4", [&] { hipLaunchKernelGGL((k_xxh64_glds<16, 4, 2, true, false, 1, false>), G(16), dim3(64), 0, 0, d, L, (uint32_t)L, n, out, nullptr, nullptr, nullptr); }},
+        };
+        for (auto& f : fs) f.second();
+        CK(hipDeviceSynchronize());
+        std::vector<double> t(fs.size(), 1e30);
+        for (int round = 0; round < 5; ++round)
+            for (size_t i = 0; i < fs.size(); ++i) t[i] = std::min(t[i], timeit(fs[i].second));
+        for (auto& f : fs) {
+            CK(hipMemset(out, 0, NMAX * 8));
+            f.second();
+            CK(hipDeviceSynchronize());
+            uint64_t bad = 0;
+            for (uint64_t i = 0; i < K; ++i) {
+                if (idx[i] >= n) continue;
+                uint64_t g; CK(hipMemcpy(&g, out + idx[i], 8, hipMemcpyDeviceToHost));
+                bad += g != ref[i];
+            }
+            if (bad) { printf("  !! %s n=%llu: %llu mismatches\n", f.first, (unsigned long long)n, (unsigned long long)bad); ++bad_total; }
+        }
+        double best = 1e30;
+        printf("%7llu", (unsigned long long)n);
+        for (size_t i = 0; i < fs.size(); ++i) { printf(" %9.2f", t[i]); best = std::min(best, t[i]); }
+        printf("   %7.0f GB/s\n", n * (L + 8) / (best * 1e-6) / 1e9);
+        fflush(stdout);
+    }
+    printf(bad_total ? "MISMATCH\n" : "all bit-exact\n");
+    return bad_total ? 1 : 0;
+}
+
 int main(int argc, char** argv) {
     const int reps = argc > 1 ? atoi(argv[1]) : 50;
+    if (argc > 2 && std::string(argv[2]) == "mid") return mid_sweep(reps);
     const uint64_t L = 32768, NMAX = 16384;
     uint8_t* d; CK(hipMalloc(&d, NMAX * L));
     uint64_t* out; CK(hipMalloc(&out, NMAX * 8));
@@ -301,14 +367,17 @@ int main(int argc, char** argv) {
             CK(hipDeviceSynchronize());
         }
     }
-    printf("%6s %9s %9s %9s %9s %9s | %9s %9s %9s %9s   (us per launch, best of 5 alternating rounds of %d launches)\n",
-           "n", "classic", "d16x4", "d16x3", "valu", "loads", "mix-cls", "mix16x4", "mix16x3", "mix8x6", reps);
+    printf("%6s %9s %9s %9s %9s %9s %9s %9s %9s | %9s %9s %9s %9s   (us per launch, best of 5 alternating rounds of %d launches)\n",
+           "n", "classic", "d16x4", "d16x3", "g1w16x2", "g1w16x4", "g1w8x6", "valu", "loads", "mix-cls", "mix16x4", "mix16x3", "mix8x6", reps);
     for (uint64_t n : {1ULL, 16ULL, 64ULL, 256ULL, 1202ULL, 2048ULL, 4096ULL, 8192ULL, 16384ULL}) {
         const dim3 g((unsigned)((n * 4 + 255) / 256));
 #define KU(NAME, KERN) {NAME, [&] { hipLaunchKernelGGL(KERN, g, dim3(256), 0, 0, d, L, nullptr, (uint32_t)L, n, out); }}
 #define KM(NAME, KERN) {NAME, [&] { hipLaunchKernelGGL(KERN, g, dim3(256), 0, 0, d, L, dl, 0u, n, out); }}
         std::vector<std::pair<const char*, std::function<void()>>> fs = {
             KU("classic", (k_quad<false, false>)), KU("d16x4", (k_deep<16, 4, false>)), KU("d16x3", (k_deep<16, 3, false>)),
+            {"g1w16x2", [&] { hipLaunchKernelGGL((k_xxh64_glds<16, 2, 2, true, false, 1, false>), dim3((unsigned)((n + 15) / 16)), dim3(64), 0, 0, d, L, (uint32_t)L, n, out, nullptr, nullptr, nullptr); }},
+            {"g1w16x4", [&] { hipLaunchKernelGGL((k_xxh64_glds<16, 4, 2, true, false, 1, false>), dim3((unsigned)((n + 15) / 16)), dim3(64), 0, 0, d, L, (uint32_t)L, n, out, nullptr, nullptr, nullptr); }},
+            {"g1w8x6", [&] { hipLaunchKernelGGL((k_xxh64_glds<8, 6, 2, true, false, 1, false>), dim3((unsigned)((n + 15) / 16)), dim3(64), 0, 0, d, L, (uint32_t)L, n, out, nullptr, nullptr, nullptr); }},
             {"valu-only", [&] { hipLaunchKernelGGL(k_bound<1>, g, dim3(256), 0, 0, d, L, (uint32_t)L, n, out); }},
             {"loads-only", [&] { hipLaunchKernelGGL(k_bound<2>, g, dim3(256), 0, 0, d, L, (uint32_t)L, n, out); }},
             KM("mix classic", (k_quad<false, true>)), KM("mix d16x4", (k_deep<16, 4, true>)),
@@ -319,9 +388,9 @@ int main(int argc, char** argv) {
         std::vector<double> t(fs.size(), 1e30);
         for (int round = 0; round < 5; ++round)
             for (size_t i = 0; i < fs.size(); ++i) t[i] = std::min(t[i], timeit(fs[i].second));
-        for (size_t i = 0; i < fs.size(); ++i) { fs[i].second(); if (i == 3 || i == 4) continue; check(fs[i].first, n, i < 5 ? ref_u : ref_m); }
+        for (size_t i = 0; i < fs.size(); ++i) { fs[i].second(); if (i == 6 || i == 7) continue; check(fs[i].first, n, i < 8 ? ref_u : ref_m); }
         printf("%6llu", (unsigned long long)n);
-        for (size_t i = 0; i < fs.size(); ++i) printf(i == 5 ? " | %9.2f" : " %9.2f", t[i]);
+        for (size_t i = 0; i < fs.size(); ++i) printf(i == 8 ? " | %9.2f" : " %9.2f", t[i]);
         printf("\n");
         fflush(stdout);
     }
