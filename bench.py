@@ -57,13 +57,28 @@ def parse():
     return p.parse_args()
 
 
-def settle(step, seconds: float):
-    """Untimed steps until `seconds` of wall time have passed (GPU clock ramp)."""
+def settle(step, seconds: float, group_dev=None):
+    """Untimed steps until `seconds` of wall time have passed (GPU clock ramp).
+
+    With a process group (`group_dev` = the tensor device for it) every rank runs the
+    same number of steps: a step holds a collective (the root all-gather), so a count
+    taken from each rank's own clock would leave one rank waiting in a collective the
+    others never enter. The ranks continue while any of them is still short of
+    `seconds` (MAX all-reduce of a flag)."""
     import torch
     t0 = time.perf_counter()
-    while time.perf_counter() - t0 < seconds:
+    while True:
+        more = time.perf_counter() - t0 < seconds
+        if group_dev is not None:
+            import torch.distributed as dist
+            f = torch.tensor([1 if more else 0], dtype=torch.int32, device=group_dev)
+            dist.all_reduce(f, op=dist.ReduceOp.MAX)
+            more = bool(f.item())
+        if not more:
+            return
         step()
-        torch.cuda.synchronize()
+        if torch.cuda.is_available():  # (the CPU gloo test of this loop has no device)
+            torch.cuda.synchronize()
 
 
 def measured_read_peak(arena, arena_n: int, stream, achieved: float):
@@ -389,7 +404,7 @@ def main():
             root, _ = sdist.global_root(root, REV, n_total, lambda t, r, ad: engine.combine_roots_tensor(t, r, ad, FANOUT))
         return root
 
-    settle(lambda: step(False), a.settle)
+    settle(lambda: step(False), a.settle, dev if distributed else None)
     for _ in range(a.warmup):
         step(False)
     torch.cuda.synchronize()

@@ -114,3 +114,58 @@ def test_gloo_world8_matches_fixture():
     for rank, groot, tab in res:
         assert list(groot) == want
         assert [list(t[:3]) for t in tab] == [[hx(v) for v in row[:3]] for row in g["shard_roots"]]
+
+
+def _settle_worker(rank, world, port, q):
+    import time
+
+    import torch
+    import torch.distributed as dist
+
+    import bench
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        count = [0]
+
+        def step():  # like bench.py's c3 step: local work of rank-dependent length, then a collective
+            time.sleep(0.01 * (1 + 4 * rank))
+            t = torch.zeros(1)
+            out = [torch.zeros(1) for _ in range(world)]
+            dist.all_gather(out, t)
+            count[0] += 1
+
+        time.sleep(0.25 * rank)  # uneven setup before the loop, as arena fills and inits are
+        bench.settle(step, 0.3, torch.device("cpu"))
+        dist.barrier()  # a rank left inside a collective would never reach this
+        q.put((rank, count[0]))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(150)
+def test_bench_settle_runs_the_same_step_count_on_every_rank():
+    """bench.py's clock-settle loop holds a collective per step: a count taken from each
+    rank's own clock deadlocks the faster rank in a collective the slower one never
+    enters. The ranks must agree on the count."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_settle_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    try:
+        res = dict(q.get(timeout=60) for _ in range(2))
+    finally:
+        for p in procs:
+            if p.is_alive():
+                p.join(timeout=5)
+            if p.is_alive():
+                p.kill()
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[0] == res[1] and res[0] >= 1
