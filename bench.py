@@ -447,6 +447,9 @@ def main():
     # HBM, so a peak from another process or box would not compare.
     read_peak = measured_read_peak(arena, arena_n, stream, achieved)
 
+    gather = ""
+    if distributed:
+        gather = " + RCCL all-gather of shard roots" if a.dist_backend == "nccl" else " + gloo all-gather of shard roots (rehearsal)"
     if rank == 0:
         root_t = engine.as_tuple(root)
         res = {
@@ -454,7 +457,7 @@ def main():
             "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "u64", "data": "synthetic",
             "config": {"workload": f"c3: {n_gpu / 2**20:g}M x 32 KiB blocks per GPU, XXH64 seed 0 (blocks.Checksum) "
-                                   "+ shard Merkle pointer tree" + (" + RCCL all-gather of shard roots" if distributed else ""),
+                                   "+ shard Merkle pointer tree" + gather,
                        "blocks_per_gpu": n_gpu, "block_bytes": BLOCK, "arena_blocks": arena_n,
                        "passes_per_step": passes, "parallelism": f"dp{world} (contiguous block ranges)"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
