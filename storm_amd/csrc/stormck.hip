@@ -1196,7 +1196,14 @@ int stormck_commit_device(void* d_arena, stormck_dirty_block* blocks, uint64_t n
         // workgroup per CU) starts the device after a small upload; each next chunk is 3x
         // the previous, small enough that its records (56 B per block over PCIe) arrive
         // before the previous chunk's blocks (~32 KiB each at HBM rate) are hashed.
-        uint64_t next = 2 * kStreamBatch;
+        uint64_t next = 2 * kStreamBatch, growth = 3;
+        if (const char* e = std::getenv("STORMCK_COMMIT_CHUNKS")) {  // tuning probe: "first,growth"
+            unsigned long long f = 0, gr = 0;
+            if (std::sscanf(e, "%llu,%llu", &f, &gr) == 2 && f >= 1 && gr >= 1) {
+                next = f;
+                growth = gr;
+            }
+        }
         for (uint64_t lo = 0; lo < n0;) {
             uint64_t cnt = std::min(next, n0 - lo);
             if (n0 - lo - cnt < kStreamBatch) cnt = n0 - lo;  // no runt last chunk
@@ -1206,7 +1213,7 @@ int stormck_commit_device(void* d_arena, stormck_dirty_block* blocks, uint64_t n
             e = send_back(lo, cnt);
             if (e) return e;
             lo += cnt;
-            next = cnt * 3;
+            next = cnt * growth;
         }
         pt.mark("level0_issue");
         if (nu == 0) return STORMCK_OK;
