@@ -7,7 +7,7 @@ import json
 import os
 import sys
 
-KERNEL = "k_xxh64_glds_skew<16, 2, false, 8, 8>"  # rocprofv3 name of the dominant kernel
+KERNEL = "k_xxh64_glds_skew<16, 2, false, 8, 8, true>"  # rocprofv3 name of the dominant kernel
 
 
 def rows(path):
