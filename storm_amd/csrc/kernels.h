@@ -52,8 +52,10 @@ __device__ __forceinline__ T ldg(const T* p) {
 // Stripe loop of one accumulator over nst stripes, 8-byte-aligned source.
 // p points at word j of stripe 0; word j of stripe s is p[4*s].
 // Software-pipelined in groups of U loads: group g+1 is in flight while group g hashes.
-template <int U, bool NT = false>
+// PM: the words are premultiplied by P2 (round_pm).
+template <int U, bool NT = false, bool PM = false>
 __device__ __forceinline__ uint64_t quad_stripes_aligned(const uint64_t* __restrict__ p, uint32_t nst, uint64_t acc) {
+    auto rnd = [](uint64_t a, uint64_t w) { return PM ? round_pm(a, w) : round(a, w); };
     const uint32_t ngroups = nst / U;
     uint32_t s = 0;
     if (ngroups > 0) {
@@ -66,28 +68,28 @@ __device__ __forceinline__ uint64_t quad_stripes_aligned(const uint64_t* __restr
 #pragma unroll
             for (int u = 0; u < U; ++u) wb[u] = ldg<NT>(q + 4 * u);
 #pragma unroll
-            for (int u = 0; u < U; ++u) acc = round(acc, wa[u]);
+            for (int u = 0; u < U; ++u) acc = rnd(acc, wa[u]);
             q += 4 * U;
 #pragma unroll
             for (int u = 0; u < U; ++u) wa[u] = ldg<NT>(q + 4 * u);
 #pragma unroll
-            for (int u = 0; u < U; ++u) acc = round(acc, wb[u]);
+            for (int u = 0; u < U; ++u) acc = rnd(acc, wb[u]);
         }
         if (g < ngroups) {
             const uint64_t* q = p + 4 * U * g;
 #pragma unroll
             for (int u = 0; u < U; ++u) wb[u] = ldg<NT>(q + 4 * u);
 #pragma unroll
-            for (int u = 0; u < U; ++u) acc = round(acc, wa[u]);
+            for (int u = 0; u < U; ++u) acc = rnd(acc, wa[u]);
 #pragma unroll
-            for (int u = 0; u < U; ++u) acc = round(acc, wb[u]);
+            for (int u = 0; u < U; ++u) acc = rnd(acc, wb[u]);
         } else {
 #pragma unroll
-            for (int u = 0; u < U; ++u) acc = round(acc, wa[u]);
+            for (int u = 0; u < U; ++u) acc = rnd(acc, wa[u]);
         }
         s = ngroups * U;
     }
-    for (; s < nst; ++s) acc = round(acc, p[4 * s]);
+    for (; s < nst; ++s) acc = rnd(acc, p[4 * s]);
     return acc;
 }
 
@@ -227,36 +229,72 @@ __device__ __forceinline__ void single_stage(const uint4* __restrict__ src, uint
     for (int k = 0; k < K; ++k) buf[min(threadIdx.x + 256u * k, words - 1)] = r[k];
 }
 
+// single_stage, with the block's stripe words premultiplied by P2 on their way into LDS
+// (round_pm). The block starts `shift8` 8-byte words into the staged cover (0 or 1:
+// only 8-byte-aligned starts take this path) and its first `nw` words are stripe words.
+template <int K>
+__device__ __forceinline__ void single_stage_pm(const uint4* __restrict__ src, uint4* buf, uint32_t words,
+                                                uint32_t shift8, uint32_t nw) {
+    uint4 r[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) r[k] = src[min(threadIdx.x + 256u * k, words - 1)];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const uint32_t idx = min(threadIdx.x + 256u * k, words - 1);
+        uint64_t a = (static_cast<uint64_t>(r[k].y) << 32) | r[k].x;
+        uint64_t b = (static_cast<uint64_t>(r[k].w) << 32) | r[k].z;
+        const uint32_t wa = 2 * idx - shift8;  // block word index of a (wraps below 0)
+        if (wa < nw) a *= kP2;
+        if (wa + 1 < nw) b *= kP2;
+        buf[idx] = make_uint4(static_cast<uint32_t>(a), static_cast<uint32_t>(a >> 32), static_cast<uint32_t>(b),
+                              static_cast<uint32_t>(b >> 32));
+    }
+}
+
+template <int KMAX>
+__device__ __forceinline__ void stage_pm_switch(const uint4* __restrict__ src, uint4* buf, uint32_t words,
+                                                uint32_t shift8, uint32_t nw) {
+    switch ((words + 255) / 256) {
+        case 0: break;
+        case 1: single_stage_pm<1>(src, buf, words, shift8, nw); break;
+        case 2: single_stage_pm<2>(src, buf, words, shift8, nw); break;
+        case 3: single_stage_pm<3>(src, buf, words, shift8, nw); break;
+        case 4: single_stage_pm<4>(src, buf, words, shift8, nw); break;
+        case 5: single_stage_pm<5>(src, buf, words, shift8, nw); break;
+        case 6: single_stage_pm<6>(src, buf, words, shift8, nw); break;
+        case 7: single_stage_pm<7>(src, buf, words, shift8, nw); break;
+        case 8: single_stage_pm<8>(src, buf, words, shift8, nw); break;
+        default:
+            if constexpr (KMAX > 8) {
+                switch ((words + 255) / 256) {
+                    case 9: single_stage_pm<9>(src, buf, words, shift8, nw); break;
+                    case 10: single_stage_pm<10>(src, buf, words, shift8, nw); break;
+                    case 11: single_stage_pm<11>(src, buf, words, shift8, nw); break;
+                    case 12: single_stage_pm<12>(src, buf, words, shift8, nw); break;
+                    case 13: single_stage_pm<13>(src, buf, words, shift8, nw); break;
+                    case 14: single_stage_pm<14>(src, buf, words, shift8, nw); break;
+                    case 15: single_stage_pm<15>(src, buf, words, shift8, nw); break;
+                    default: single_stage_pm<16>(src, buf, words, shift8, nw); break;
+                }
+            } else {
+                single_stage_pm<8>(src, buf, words, shift8, nw);
+            }
+            break;
+    }
+}
+
 __global__ __launch_bounds__(256) void k_xxh64_single(const uint8_t* __restrict__ src, uint32_t n,
                                                         uint64_t* __restrict__ out) {
     __shared__ uint4 buf[kSingleMax / 16];
     const uint32_t words = (n + 15) / 16;
     const uint4* s16 = reinterpret_cast<const uint4*>(src);
-    switch ((words + 255) / 256) {
-        case 0: break;
-        case 1: single_stage<1>(s16, buf, words); break;
-        case 2: single_stage<2>(s16, buf, words); break;
-        case 3: single_stage<3>(s16, buf, words); break;
-        case 4: single_stage<4>(s16, buf, words); break;
-        case 5: single_stage<5>(s16, buf, words); break;
-        case 6: single_stage<6>(s16, buf, words); break;
-        case 7: single_stage<7>(s16, buf, words); break;
-        case 8: single_stage<8>(s16, buf, words); break;
-        case 9: single_stage<9>(s16, buf, words); break;
-        case 10: single_stage<10>(s16, buf, words); break;
-        case 11: single_stage<11>(s16, buf, words); break;
-        case 12: single_stage<12>(s16, buf, words); break;
-        case 13: single_stage<13>(s16, buf, words); break;
-        case 14: single_stage<14>(s16, buf, words); break;
-        case 15: single_stage<15>(s16, buf, words); break;
-        default: single_stage<16>(s16, buf, words); break;
-    }
+    const uint32_t nst = n >> 5;
+    stage_pm_switch<16>(s16, buf, words, 0, 4 * nst);
     __syncthreads();
     if (threadIdx.x >= 4) return;
     const uint32_t j = threadIdx.x;
     const uint8_t* s = reinterpret_cast<const uint8_t*>(buf);
-    const uint32_t nst = n >> 5;
-    const uint64_t acc = quad_stripes_aligned<16>(reinterpret_cast<const uint64_t*>(s) + j, nst, acc_seed(j));
+    const uint64_t acc = quad_stripes_aligned<16, false, true>(reinterpret_cast<const uint64_t*>(s) + j, nst, acc_seed(j));
     const uint64_t v1 = quad_bcast<0>(acc), v2 = quad_bcast<1>(acc), v3 = quad_bcast<2>(acc), v4 = quad_bcast<3>(acc);
     if (j == 0) {
         const uint64_t h0 = (n >= 32) ? converge(v1, v2, v3, v4) : kP5;
@@ -279,7 +317,7 @@ constexpr uint32_t kWideMax = 32 * 1024;
 // ds_read from the staged copy and with global loads otherwise: through one generic
 // pointer both would be flat loads, which the compiler can only wait for all at once
 // (s_waitcnt vmcnt(0) lgkmcnt(0) per group, no prefetch overlap).
-template <bool VERIFY>
+template <bool VERIFY, bool PM = false>
 __device__ __forceinline__ void wide_hash(const uint8_t* s, uint32_t L, uint64_t blk, uint64_t* __restrict__ out,
                                           const uint64_t* __restrict__ expected,
                                           unsigned long long* __restrict__ first_bad,
@@ -287,10 +325,13 @@ __device__ __forceinline__ void wide_hash(const uint8_t* s, uint32_t L, uint64_t
     const uint32_t j = threadIdx.x;
     const uint32_t nst = L >> 5;
     uint64_t acc = acc_seed(j);
-    if ((reinterpret_cast<uintptr_t>(s) & 7) == 0)
+    if constexpr (PM) {  // staged with premultiplied stripe words, 8-byte aligned
+        acc = quad_stripes_aligned<16, false, true>(reinterpret_cast<const uint64_t*>(s) + j, nst, acc);
+    } else if ((reinterpret_cast<uintptr_t>(s) & 7) == 0) {
         acc = quad_stripes_aligned<16>(reinterpret_cast<const uint64_t*>(s) + j, nst, acc);
-    else
+    } else {
         acc = quad_stripes_unaligned(s + 8 * j, nst, acc);
+    }
     const uint64_t v1 = quad_bcast<0>(acc), v2 = quad_bcast<1>(acc), v3 = quad_bcast<2>(acc), v4 = quad_bcast<3>(acc);
     if (j == 0) {
         const uint64_t h0 = (L >= 32) ? converge(v1, v2, v3, v4) : kP5;
@@ -323,6 +364,14 @@ __global__ __launch_bounds__(256) void k_xxh64_wide(const uint8_t* __restrict__ 
     if (words <= kWideMax / 16) {
         // a 16-byte window holding a byte of the block lies in that byte's page
         const uint4* cover = reinterpret_cast<const uint4*>(src - shift);
+        if ((shift & 7) == 0) {  // 8-byte-aligned start: stripe words premultiplied on the way in
+            stage_pm_switch<8>(cover, buf, words, shift / 8, 4 * (L >> 5));
+            __syncthreads();
+            if (threadIdx.x >= 4) return;
+            wide_hash<VERIFY, true>(reinterpret_cast<const uint8_t*>(buf) + shift, L, blk, out, expected, first_bad,
+                                    n_bad);
+            return;
+        }
         switch ((words + 255) / 256) {
             case 0: break;
             case 1: single_stage<1>(cover, buf, words); break;
@@ -719,8 +768,10 @@ struct EntryWords {
 // fetched U stripes ahead (group g+1's child loads in flight while group g hashes):
 // fetched one at a time, each round waited for its load, which made a 1,200-way
 // level of 14K nodes take 240 us instead of the ~30 us serial XXH64 chain.
-template <class W, int U = 16>
+// PM: stripe words (k < 4 * nst) come premultiplied by P2; the tail words do not.
+template <class W, int U = 16, bool PM = false>
 __device__ __forceinline__ uint64_t hash_words_quad(const W& word, uint32_t size, uint32_t j) {
+    auto rnd = [](uint64_t a, uint64_t w) { return PM ? round_pm(a, w) : round(a, w); };
     const uint32_t nst = size >> 5;
     uint64_t acc = acc_seed(j);
     const uint32_t ngroups = nst / U;
@@ -733,15 +784,15 @@ __device__ __forceinline__ uint64_t hash_words_quad(const W& word, uint32_t size
 #pragma unroll
             for (int u = 0; u < U; ++u) wb[u] = word(4 * (g * U + u) + j);
 #pragma unroll
-            for (int u = 0; u < U; ++u) acc = round(acc, wa[u]);
+            for (int u = 0; u < U; ++u) acc = rnd(acc, wa[u]);
 #pragma unroll
             for (int u = 0; u < U; ++u) wa[u] = wb[u];
         }
 #pragma unroll
-        for (int u = 0; u < U; ++u) acc = round(acc, wa[u]);
+        for (int u = 0; u < U; ++u) acc = rnd(acc, wa[u]);
         s = ngroups * U;
     }
-    for (; s < nst; ++s) acc = round(acc, word(4 * s + j));
+    for (; s < nst; ++s) acc = rnd(acc, word(4 * s + j));
     const uint64_t v1 = quad_bcast<0>(acc), v2 = quad_bcast<1>(acc), v3 = quad_bcast<2>(acc), v4 = quad_bcast<3>(acc);
     uint64_t h = (size >= 32) ? converge(v1, v2, v3, v4) : kP5;
     h += size;
@@ -781,11 +832,11 @@ struct LdsWords {
 template <class W>
 __device__ __forceinline__ void hash_node_wide(const W& w, uint32_t size, uint64_t* __restrict__ out) {
     __shared__ uint64_t node[kNodeLds / 8];
-    const uint32_t words = size / 8;
-    for (uint32_t k = threadIdx.x; k < words; k += blockDim.x) node[k] = w(k);
+    const uint32_t words = size / 8, nw = 4 * (size >> 5);
+    for (uint32_t k = threadIdx.x; k < words; k += blockDim.x) node[k] = k < nw ? w(k) * kP2 : w(k);
     __syncthreads();
     if (threadIdx.x < 4) {
-        const uint64_t h = hash_words_quad(LdsWords{node}, size, threadIdx.x);
+        const uint64_t h = hash_words_quad<LdsWords, 16, true>(LdsWords{node}, size, threadIdx.x);
         if (threadIdx.x == 0) *out = h;
     }
 }

@@ -44,6 +44,16 @@ __device__ __forceinline__ uint64_t round(uint64_t acc, uint64_t w) {
     return acc * kP1;
 }
 
+// round() on a word already multiplied by P2 (pw = w * P2). The latency kernels stage a
+// block in LDS and have all 256 threads premultiply its stripe words there, so the one
+// quad that walks the serial chain issues the add, the rotate and the P1 multiply only:
+// a lone wave is issue-bound, and the P2 multiply is 4 of its ~11 instructions a round.
+__device__ __forceinline__ uint64_t round_pm(uint64_t acc, uint64_t pw) {
+    acc += pw;
+    acc = rotl<31>(acc);
+    return acc * kP1;
+}
+
 __device__ __forceinline__ uint64_t merge(uint64_t h, uint64_t v) {
     h ^= round(0, v);
     return h * kP1 + kP4;

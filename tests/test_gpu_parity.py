@@ -119,6 +119,52 @@ def test_synth_vs_oracle_random_lengths(dev):
     assert np.array_equal(_u64(out2), want2)
 
 
+@pytest.mark.parametrize("n", [1, 7, 128])
+def test_wide_path_premultiplied_staging(dev, n):
+    """Batches of <= 128 blocks take k_xxh64_wide: blocks whose start is 8-byte aligned
+    (shift 0 or 8 within their 16-byte cover) are staged with their stripe words
+    premultiplied by P2; other starts, and covers over 32 KiB, take the plain path.
+    Random starts 0..56 mod 16 and lengths up to 32 KiB (incl. 32760 at shift 8, the
+    largest premultiplied stage), checksum and verify, vs the C oracle."""
+    from oracle import oracle as o
+    from storm_amd import engine
+    rng = np.random.default_rng(100 + n)
+    stride = 32768 + 64
+    host = rng.integers(0, 256, size=n * stride, dtype=np.uint8)
+    lens = rng.integers(0, 32769, size=n).astype(np.uint32)
+    shifts = rng.integers(0, 57, size=n).astype(np.uint64)
+    if n >= 7:
+        lens[:7] = [0, 31, 32, 33, 32760, 32768, 4096]
+        shifts[:7] = [8, 8, 0, 8, 8, 0, 24]
+    offs = np.arange(n, dtype=np.uint64) * stride + shifts
+    want = np.array([o.xxh64(host[int(offs[i]):int(offs[i]) + int(lens[i])]) for i in range(n)], dtype=np.uint64)
+    d = _to_dev(host, dev)
+    d_offs = _to_dev(offs.view(np.int64), dev)
+    d_lens = _to_dev(lens.view(np.int32), dev)
+    out = torch.empty(n, dtype=torch.int64, device=dev)
+    engine.checksum_gather_device(d.data_ptr(), d_offs.data_ptr(), n, out.data_ptr(), 0, d_lens.data_ptr())
+    torch.cuda.synchronize()
+    assert np.array_equal(_u64(out), want)
+    # uniform length on an 8-byte (not 16-byte) aligned base: every block at shift 8
+    out2 = torch.empty(n, dtype=torch.int64, device=dev)
+    engine.checksum_device(d.data_ptr() + 8, stride, n, out2.data_ptr(), 30000)
+    torch.cuda.synchronize()
+    want2 = o.checksum_batch(host[8:], n, stride, 30000)
+    assert np.array_equal(_u64(out2), want2)
+    # verify through the same kernel (VERIFY=true)
+    res = torch.zeros(2, dtype=torch.int64, device=dev)
+    exp = _to_dev(want2.view(np.int64), dev)
+    engine.verify_device(d.data_ptr() + 8, stride, n, exp.data_ptr(), res.data_ptr(), 30000)
+    torch.cuda.synchronize()
+    assert _u64(res).tolist() == [n, 0]
+    bad = want2.copy()
+    bad[n - 1] ^= 1
+    engine.verify_device(d.data_ptr() + 8, stride, n, _to_dev(bad.view(np.int64), dev).data_ptr(), res.data_ptr(),
+                         30000)
+    torch.cuda.synchronize()
+    assert _u64(res).tolist() == [n - 1, 1]
+
+
 @pytest.mark.parametrize("length", [512, 513, 520, 1000, 8192, 28808, 30000, 31808, 32768])
 def test_uniform_fast_path_lengths(dev, length):
     """Uniform-length 16-byte-aligned batches of every batch-size class: <= 128 blocks
