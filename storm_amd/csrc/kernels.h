@@ -902,6 +902,54 @@ __global__ void k_set_root(const uint64_t* __restrict__ cs, uint64_t addr, uint6
 // origin slot and the block type into the origin type byte. Origins belong to blocks
 // of later levels (parents), which this launch never reads. out_cs[lo + k] = checksum.
 // ---------------------------------------------------------------------------
+// Small f1 levels (the pointer blocks above the leaves, the root, a short commit): one
+// workgroup per dirty block, as k_xxh64_wide. The block is staged into LDS in one round
+// trip with its stripe words premultiplied by P2 (8-byte-aligned starts; others and
+// blocks over 32 KiB hash from memory), then quad 0 walks the chain and lane 0 performs
+// the PostCommitFunc store, as k_commit_level.
+__global__ __launch_bounds__(256) void k_commit_level_wide(uint8_t* __restrict__ arena,
+                                                            const stormck_dirty_block* __restrict__ blocks,
+                                                            uint64_t lo, uint64_t* __restrict__ out_cs) {
+    __shared__ uint4 buf[kWideMax / 16];
+    const uint64_t k = lo + blockIdx.x;
+    const stormck_dirty_block b = blocks[k];
+    const uint8_t* src = arena + b.data_offset;
+    const uint32_t L = b.length;
+    const uint32_t nst = L >> 5;
+    const uint32_t shift = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(src) & 15);
+    const uint32_t words = (shift + L + 15) / 16;
+    const uint32_t j = threadIdx.x;
+    uint64_t acc = acc_seed(j & 3);
+    const uint8_t* s;
+    if ((shift & 7) == 0 && words <= kWideMax / 16) {  // uniform over the workgroup
+        stage_pm_switch<8>(reinterpret_cast<const uint4*>(src - shift), buf, words, shift / 8, 4 * nst);
+        __syncthreads();
+        if (j >= 4) return;
+        s = reinterpret_cast<const uint8_t*>(buf) + shift;
+        acc = quad_stripes_aligned<16, false, true>(reinterpret_cast<const uint64_t*>(s) + j, nst, acc);
+    } else {
+        if (j >= 4) return;
+        s = src;
+        if ((reinterpret_cast<uintptr_t>(s) & 7) == 0)
+            acc = quad_stripes_aligned<16>(reinterpret_cast<const uint64_t*>(s) + j, nst, acc);
+        else
+            acc = quad_stripes_unaligned(s + 8 * j, nst, acc);
+    }
+    const uint64_t v1 = quad_bcast<0>(acc), v2 = quad_bcast<1>(acc), v3 = quad_bcast<2>(acc), v4 = quad_bcast<3>(acc);
+    if (j == 0) {
+        const uint64_t h0 = (L >= 32) ? converge(v1, v2, v3, v4) : kP5;
+        const uint64_t h = finish_fast(h0, L, s + 32 * static_cast<uint64_t>(nst), L & 31);
+        out_cs[k] = h;
+        if (b.origin_pointer != STORMCK_NO_ORIGIN) {
+            uint64_t* p = reinterpret_cast<uint64_t*>(arena + b.origin_pointer);
+            p[0] = h;
+            p[1] = b.address;
+            p[2] = b.birth_revision;
+            arena[b.origin_type] = b.type;
+        }
+    }
+}
+
 template <int U>
 __global__ __launch_bounds__(256) void k_commit_level(uint8_t* __restrict__ arena,
                                                        const stormck_dirty_block* __restrict__ blocks, uint64_t lo,

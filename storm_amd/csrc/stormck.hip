@@ -130,6 +130,7 @@ constexpr unsigned kGldsThreads = 64 * kGldsWaves;
 constexpr unsigned kGldsBlocks = 16 * kGldsWaves;
 constexpr int kAuxNT = 2;
 constexpr uint64_t kWideBatch = 128;      // batches up to this many blocks: k_xxh64_wide
+constexpr uint64_t kCommitWide = 256;     // f1 levels up to this many blocks: k_commit_level_wide
 constexpr uint64_t kStreamBatch = 16384;  // f1 commit levels from this many blocks: k_commit_level_glds
 // Uniform batches take the LDS-staged kernel from kMidBatch blocks. Below kBigBatch its
 // workgroups are 2 waves (32 blocks, 16 KiB of ring) rather than 8 (128 blocks, 128 KiB):
@@ -1124,6 +1125,8 @@ int stormck_commit_device(void* d_arena, stormck_dirty_block* blocks, uint64_t n
     auto idx_at = [&](uint64_t k) -> uint64_t { return order.empty() ? k : order[k]; };
 
     hipStream_t st = static_cast<hipStream_t>(stream);
+    uint64_t commit_wide = kCommitWide;
+    if (const char* e = std::getenv("STORMCK_COMMIT_WIDE")) commit_wide = std::strtoull(e, nullptr, 10);  // probe knob
     auto launch_level = [&](uint64_t lo, uint64_t cnt) -> int {
         if (aligned16 && cnt >= kStreamBatch) {
             // LDS-DMA ring, 8 waves x 128 blocks per workgroup (as the uniform fast path)
@@ -1131,6 +1134,10 @@ int stormck_commit_device(void* d_arena, stormck_dirty_block* blocks, uint64_t n
             if (wgs > 0x7fffffffULL) return fail(STORMCK_EINVAL, "level too large");
             hipLaunchKernelGGL((k_commit_level_glds<kTileStripes, kAuxNT, kGldsWaves>), dim3(static_cast<unsigned>(wgs)),
                                dim3(kGldsThreads), 0, st, static_cast<uint8_t*>(d_arena), d_blocks, lo, cnt, d_cs);
+        } else if (cnt <= commit_wide) {
+            // one workgroup per block, premultiplied staging: the chain wave is alone on its SIMD
+            hipLaunchKernelGGL(k_commit_level_wide, dim3(static_cast<unsigned>(cnt)), dim3(kThreads), 0, st,
+                               static_cast<uint8_t*>(d_arena), d_blocks, lo, d_cs);
         } else {
             dim3 grid;
             if (!grid_for(cnt * 4, &grid)) return fail(STORMCK_EINVAL, "level too large");
