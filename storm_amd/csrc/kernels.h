@@ -393,6 +393,124 @@ __global__ __launch_bounds__(256) void k_xxh64_wide(const uint8_t* __restrict__ 
 }
 
 // ---------------------------------------------------------------------------
+// Batches that fit one workgroup per CU at BPW blocks each ("wide multi"): a 256-thread
+// workgroup stages BPW blocks (covers <= 32 KiB, 8-byte-aligned starts) into LDS in one
+// memory round trip, stripe words premultiplied by P2, then wave 0's lanes 4b..4b+3
+// walk block b's chain. The chain wave is issue-bound, so BPW blocks cost about what
+// one costs; at BPW = 5 a storm commit batch (~1,200 blocks) is one workgroup per CU.
+// Blocks that cannot be staged (other starts, larger covers) hash from memory in the
+// same lanes.
+// ---------------------------------------------------------------------------
+template <bool LENS, bool OFFS, bool VERIFY, int BPW>
+__global__ __launch_bounds__(256) void k_xxh64_wide_multi(const uint8_t* __restrict__ base, uint64_t stride,
+                                                            const uint32_t* __restrict__ lens, uint32_t len,
+                                                            const uint64_t* __restrict__ offs, uint64_t n,
+                                                            uint64_t* __restrict__ out,
+                                                            const uint64_t* __restrict__ expected,
+                                                            unsigned long long* __restrict__ first_bad,
+                                                            unsigned long long* __restrict__ n_bad) {
+    // Block slots are kPieces 16-byte pieces apart: 2034 = 2 (mod 16), so slot b starts
+    // 32 * b bytes into the 256-byte bank period and the chain's ds_read_b64 of the BPW
+    // blocks (4 lanes x 8 B each) hit distinct banks (a 32 KiB stride would put them all
+    // on the same 8 banks). 5 slots of 32,544 B fit the CU's 160 KiB.
+    constexpr uint32_t kPieces = 2034;
+    static_assert(BPW * kPieces * 16 <= 160 * 1024, "LDS");
+    __shared__ uint4 buf[BPW * kPieces];
+    const uint64_t first = static_cast<uint64_t>(blockIdx.x) * BPW;
+    const uint4* cover[BPW];
+    uint32_t words[BPW], shift8[BPW], nw[BPW];
+#pragma unroll
+    for (int b = 0; b < BPW; ++b) {
+        const uint64_t blk = first + b;
+        words[b] = 0;
+        cover[b] = nullptr;
+        shift8[b] = 0;
+        nw[b] = 0;
+        if (blk < n) {
+            const uint8_t* src = base + (OFFS ? offs[blk] : blk * stride);
+            const uint32_t L = LENS ? lens[blk] : len;
+            const uint32_t shift = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(src) & 15);
+            const uint32_t w = (shift + L + 15) / 16;
+            if ((shift & 7) == 0 && w <= kPieces) {
+                words[b] = w;
+                cover[b] = reinterpret_cast<const uint4*>(src - shift);
+                shift8[b] = shift / 8;
+                nw[b] = 4 * (L >> 5);
+            }
+        }
+    }
+    // every thread issues all of its loads (<= 8 pieces per block) before storing any.
+    // The loads are unconditional (index clamped, blocks that are not staged read a
+    // staged block's cover): a load under a branch gets its own vmcnt(0) wait, which
+    // would make the 8 * BPW loads 8 * BPW round trips.
+    const uint4* safe = nullptr;
+#pragma unroll
+    for (int b = 0; b < BPW; ++b)
+        if (!safe && words[b]) safe = cover[b];
+    if (safe) {  // uniform over the workgroup
+        const uint4* cv[BPW];
+        uint32_t lim[BPW];
+#pragma unroll
+        for (int b = 0; b < BPW; ++b) {
+            cv[b] = words[b] ? cover[b] : safe;
+            lim[b] = words[b] ? words[b] - 1 : 0;
+        }
+        uint4 r[BPW * 8];
+#pragma unroll
+        for (int k = 0; k < BPW * 8; ++k) {
+            const int b = k >> 3;
+            r[k] = cv[b][min(threadIdx.x + 256u * (k & 7), lim[b])];
+        }
+#pragma unroll
+        for (int k = 0; k < BPW * 8; ++k) {
+            const int b = k >> 3;
+            const uint32_t idx = threadIdx.x + 256u * (k & 7);
+            if (idx < words[b]) {
+                uint64_t a = (static_cast<uint64_t>(r[k].y) << 32) | r[k].x;
+                uint64_t c = (static_cast<uint64_t>(r[k].w) << 32) | r[k].z;
+                const uint32_t wa = 2 * idx - shift8[b];
+                if (wa < nw[b]) a *= kP2;
+                if (wa + 1 < nw[b]) c *= kP2;
+                buf[b * kPieces + idx] = make_uint4(static_cast<uint32_t>(a), static_cast<uint32_t>(a >> 32),
+                                                    static_cast<uint32_t>(c), static_cast<uint32_t>(c >> 32));
+            }
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x >= 4 * BPW) return;
+    const uint32_t b = threadIdx.x >> 2, j = threadIdx.x & 3;
+    const uint64_t blk = first + b;
+    const bool live = blk < n;
+    const uint64_t bk = live ? blk : n - 1;
+    const uint8_t* src = base + (OFFS ? offs[bk] : bk * stride);
+    const uint32_t L = LENS ? lens[bk] : len;
+    const uint32_t nst = L >> 5;
+    const uint32_t shift = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(src) & 15);
+    const bool staged = (shift & 7) == 0 && (shift + L + 15) / 16 <= kPieces;
+    const uint8_t* s = staged ? reinterpret_cast<const uint8_t*>(buf + b * kPieces) + shift : src;
+    uint64_t acc = acc_seed(j);
+    if (staged)
+        acc = quad_stripes_aligned<16, false, true>(reinterpret_cast<const uint64_t*>(s) + j, nst, acc);
+    else if ((reinterpret_cast<uintptr_t>(src) & 7) == 0)
+        acc = quad_stripes_aligned<16>(reinterpret_cast<const uint64_t*>(src) + j, nst, acc);
+    else
+        acc = quad_stripes_unaligned(src + 8 * j, nst, acc);
+    const uint64_t v1 = quad_bcast<0>(acc), v2 = quad_bcast<1>(acc), v3 = quad_bcast<2>(acc), v4 = quad_bcast<3>(acc);
+    if (j == 0 && live) {
+        const uint64_t h0 = (L >= 32) ? converge(v1, v2, v3, v4) : kP5;
+        const uint64_t h = finish_fast(h0, L, s + 32 * static_cast<uint64_t>(nst), L & 31);
+        if (VERIFY) {
+            if (h != expected[blk]) {
+                atomicMin(first_bad, static_cast<unsigned long long>(blk));
+                atomicAdd(n_bad, 1ULL);
+            }
+        } else {
+            out[blk] = h;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // LDS-staged quad kernel ("glds"): uniform length, 16-byte aligned base/stride.
 // A 256-thread workgroup owns 64 consecutive blocks. Tiles of T stripes (32*T bytes)
 // of all 64 blocks stream HBM -> LDS with global_load_lds_dwordx4 (each wave-

@@ -129,6 +129,8 @@ constexpr int kGldsWaves = 8;
 constexpr unsigned kGldsThreads = 64 * kGldsWaves;
 constexpr unsigned kGldsBlocks = 16 * kGldsWaves;
 constexpr int kAuxNT = 2;
+constexpr uint64_t kMultiBpw = 5;          // blocks per workgroup of k_xxh64_wide_multi
+constexpr uint64_t kMultiSlotPieces = 2034; // its LDS slot per block, 16-byte pieces (kernels.h)
 constexpr uint64_t kWideBatch = 128;      // batches up to this many blocks: k_xxh64_wide
 constexpr uint64_t kCommitWide = 256;     // f1 levels up to this many blocks: k_commit_level_wide
 constexpr uint64_t kStreamBatch = 16384;  // f1 commit levels from this many blocks: k_commit_level_glds
@@ -230,6 +232,36 @@ int launch_checksum(const uint8_t* base, uint64_t stride, const uint32_t* lens, 
             else STORMCK_WIDE(false, false, true);
         }
 #undef STORMCK_WIDE
+        HIP_TRY(hipGetLastError());
+        return STORMCK_OK;
+    }
+    // up to kMultiBpw blocks per CU: k_xxh64_wide_multi, one workgroup per CU staging
+    // kMultiBpw premultiplied blocks (the c5 commit batch is one such launch)
+    static const bool multi_on = [] {
+        const char* e = std::getenv("STORMCK_WIDE_MULTI");  // probe knob: "0" disables
+        return !(e && e[0] == '0');
+    }();
+    const uint64_t ncu = cu_count();
+    if (multi_on && ncu > 0 && n <= kMultiBpw * ncu &&
+        (offs || lens ||
+         ((reinterpret_cast<uintptr_t>(base) & 7) == 0 && (stride & 7) == 0 &&
+          ((reinterpret_cast<uintptr_t>(base) & 15) + len + 15) / 16 <= kMultiSlotPieces))) {
+        const dim3 grid(static_cast<unsigned>((n + kMultiBpw - 1) / kMultiBpw));
+#define STORMCK_MULTI(LENS, OFFS, VER)                                                                       \
+    hipLaunchKernelGGL((k_xxh64_wide_multi<LENS, OFFS, VER, kMultiBpw>), grid, dim3(kThreads), 0, st, base, \
+                       stride, lens, len, offs, n, out, expected, first_bad, n_bad)
+        if (!verify) {
+            if (lens && offs) STORMCK_MULTI(true, true, false);
+            else if (lens) STORMCK_MULTI(true, false, false);
+            else if (offs) STORMCK_MULTI(false, true, false);
+            else STORMCK_MULTI(false, false, false);
+        } else {
+            if (lens && offs) STORMCK_MULTI(true, true, true);
+            else if (lens) STORMCK_MULTI(true, false, true);
+            else if (offs) STORMCK_MULTI(false, true, true);
+            else STORMCK_MULTI(false, false, true);
+        }
+#undef STORMCK_MULTI
         HIP_TRY(hipGetLastError());
         return STORMCK_OK;
     }
