@@ -119,12 +119,13 @@ def test_synth_vs_oracle_random_lengths(dev):
     assert np.array_equal(_u64(out2), want2)
 
 
-@pytest.mark.parametrize("n", [1, 7, 128, 129, 1202])
+@pytest.mark.parametrize("n", [1, 7, 128, 129, 1202, 1280, 1281])
 def test_wide_path_premultiplied_staging(dev, n):
     """Batches of <= 128 blocks take k_xxh64_wide: blocks whose start is 8-byte aligned
     (shift 0 or 8 within their 16-byte cover) are staged with their stripe words
     premultiplied by P2; other starts, and covers over 32 KiB, take the plain path.
-    129 and 1,202 (a storm commit batch) cross over to the register-quad kernel.
+    129 to 5 blocks per CU (1,280 on MI355X; 1,202 = a storm commit batch) take
+    k_xxh64_wide_multi, 5 staged blocks per workgroup; 1,281 the register-quad kernel.
     Random starts 0..56 mod 16 and lengths up to 32 KiB (incl. 32760 at shift 8, the
     largest premultiplied stage), checksum and verify, vs the C oracle."""
     from oracle import oracle as o
