@@ -5,15 +5,22 @@ storm's blocks.Checksum, /root/reference/blocks/checksum.go:15-17), build the
 shard's Merkle pointer tree over the checksums, and (N > 1) all-gather the shard
 roots over RCCL and hash the combining pointer block.
 
-Workload (N = 1): BASELINE.json configs[2] — 16M x 32 KiB blocks (512 GiB) per
-GPU. 512 GiB exceeds one MI355X's 288 GB of HBM, so the blocks stream through a
-resident 4M-block (128 GiB) arena, 4 passes per step; the arena
-holds synthetic blocks written by the on-device generator before timing. XXH64
-cost is data-independent; full-size parity of the 16M logical set is tested by
-tests/test_gpu_parity.py::test_c3_16m_blocks_digest (arena regenerated per pass).
+Workloads:
+  N = 1: BASELINE.json configs[2] (c3) — 16M x 32 KiB blocks (512 GiB).
+  N > 1: BASELINE.json configs[3] (c4) — 64M blocks over the N GPUs in contiguous
+         shards (strong scaling; 8M per GPU at N = 8), RCCL all-gather of the
+         shard roots.
+A shard exceeds one MI355X's 288 GB of HBM, so its blocks stream through a
+resident 4M-block (128 GiB) arena; before each pass the on-device generator
+writes that pass's own logical blocks. The regeneration has its
+own HIP events and is taken out of the step time, so `value` covers the hash
+launches, the Merkle tree and the gather. Every block hashed is distinct, and the
+printed root is checked against the libxxhash fixture of the same workload
+(tests/golden/c3c4_roots.json): a mismatch exits non-zero.
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU, RCCL)
+    python bench.py --gpus N ...   (no launcher: bench.py spawns the N ranks itself)
 """
 from __future__ import annotations
 
@@ -31,6 +38,9 @@ HBM_PEAK_GBS = 8000.0  # MI355X spec, /opt/skills/guides/MI355X_MICROARCH.md (ch
 BLOCK = 32768          # blocks.BlockSize, /root/reference/blocks/types.go:4
 FANOUT = 1200          # pointer.PointersPerBlock, /root/reference/blocks/pointer/params.go:6
 REV = 1
+C3_BLOCKS = 16 << 20  # BASELINE.json configs[2]
+C4_BLOCKS = 64 << 20  # BASELINE.json configs[3]
+SYNTH_SEED = 0x53544F524D  # synthetic block generator seed ("STORM")
 KERNEL = "k_xxh64_glds_skew<16,nt,8w,4KiB>"  # dominant kernel (storm_amd/csrc/kernels.h), as named in profiles/traffic.json
 
 
@@ -39,7 +49,9 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=2)
-    p.add_argument("--blocks", type=int, default=16 << 20, help="blocks per GPU per step")
+    p.add_argument("--blocks", type=int, default=0,
+                   help="blocks per GPU per step (weak scaling); default: c3 (16M) at N = 1, c4 (64M total) at N > 1")
+    p.add_argument("--total-blocks", type=int, default=0, help="blocks over all GPUs per step (strong scaling)")
     p.add_argument("--arena", type=int, default=4 << 20, help="resident arena (blocks)")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget (rank 0, N=1)")
     p.add_argument("--no-cpu", action="store_true")
@@ -130,7 +142,8 @@ def cpu_baseline(seconds: float):
         if el >= seconds * 0.75:
             break
     one = reps * n * BLOCK / el / 2**30
-    threads = min(16, len(os.sched_getaffinity(0)))
+    host = host_cpu_info()
+    threads = host["usable_cpus"]  # every CPU this process may use (affinity, cgroup quota)
     reps_mt, t0 = 0, time.perf_counter()
     while True:
         o.checksum_batch(buf, n, BLOCK, BLOCK, threads=threads)
@@ -143,7 +156,7 @@ def cpu_baseline(seconds: float):
     return {"value": round(one, 3), "unit": "GiB/s", "cores": 1, "kind": "port",
             "sample": f"{n} x 32 KiB synthetic blocks (1 GiB) hashed {reps}x in {el:.1f} s by oracle/xxh64_oracle.c "
                       f"(-O3, 1 thread); Go reference unbuildable here (no Go toolchain)",
-            "all_threads": {"value": round(multi, 3), "threads": threads}}
+            "all_threads": {"value": round(multi, 3), "threads": threads}, "host": host}
 
 
 def cpu_commit_baseline(seconds: float):
@@ -342,15 +355,126 @@ def keytags_workload(a):
     print(json.dumps(res), flush=True)
 
 
+def host_cpu_info():
+    """The host the CPU baseline runs on: CPU model, logical CPUs, this process's
+    affinity and its cgroup CPU quota (a GPU box shares a large host between GPUs)."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            if q != "max":
+                quota = int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    aff = len(os.sched_getaffinity(0))
+    usable = aff if quota is None else max(1, min(aff, int(quota + 0.5)))
+    return {"model": model, "nproc": os.cpu_count(), "affinity_cpus": aff, "cgroup_cpu_quota": quota,
+            "usable_cpus": usable}
+
+
+def _rank_entry(env, argv, entry):
+    """Body of one spawned rank: the launcher's environment, then bench main() (or
+    `entry` = "module:function", which the CPU tests use to rehearse the launcher)."""
+    os.environ.update(env)
+    sys.argv = list(argv)
+    if entry:
+        import importlib
+        mod, fn = entry.split(":")
+        getattr(importlib.import_module(mod), fn)()
+    else:
+        main()
+
+
+def spawn_ranks(n: int, argv, entry=None, timeout: float = 0.0) -> int:
+    """`bench.py --gpus N` without torchrun: start N rank processes (spawn context) with
+    RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT set, exactly as
+    torch.distributed.run would. The parent never touches the GPU. A rank that fails
+    would leave the others blocked inside a collective, so the parent ends them
+    (their exact PIDs) and returns the failing exit code."""
+    import multiprocessing as mp
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    procs = []
+    for r in range(n):
+        env = {"RANK": str(r), "LOCAL_RANK": str(r), "WORLD_SIZE": str(n), "LOCAL_WORLD_SIZE": str(n),
+               "GROUP_RANK": "0", "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)}
+        p = ctx.Process(target=_rank_entry, args=(env, list(argv), entry))
+        p.start()
+        procs.append(p)
+    rc, t0 = 0, time.time()
+    while any(p.is_alive() for p in procs):
+        failed = [p for p in procs if p.exitcode not in (None, 0)]
+        late = timeout > 0 and time.time() - t0 > timeout
+        if failed or late:
+            rc = failed[0].exitcode if failed else 124
+            for p in procs:
+                if p.is_alive():
+                    p.terminate()
+            for p in procs:
+                p.join(10)
+                if p.is_alive():
+                    p.kill()
+            break
+        time.sleep(0.1)
+    for p in procs:
+        p.join()
+    if rc == 0:
+        rc = next((p.exitcode for p in procs if p.exitcode), 0)
+    return rc if rc >= 0 else 128 - rc
+
+
+def root_fixture(n_total: int, world: int, distributed: bool):
+    """The libxxhash root of this workload from tests/golden/c3c4_roots.json
+    (oracle/gen_golden.py --c4), as (cs, addr, rev, type), or None if the workload has
+    none (a non-default --blocks / --total-blocks)."""
+    path = os.path.join(ROOT, "tests", "golden", "c3c4_roots.json")
+    if not os.path.exists(path):
+        return None, None
+    with open(path) as f:
+        fx = json.load(f)
+    row = None
+    if world == 1 and not distributed and n_total == fx["c3"]["n"]:
+        row, name = fx["c3"]["root"], "c3"
+    elif world > 1 and n_total == fx["c4"]["n_total"] and str(world) in fx["c4"]["worlds"]:
+        row, name = fx["c4"]["worlds"][str(world)]["global_root"], f"c4 world {world}"
+    if row is None:
+        return None, None
+    return (int(row[0], 16), int(row[1], 16), int(row[2], 16), int(row[3])), name
+
+
 def main():
     a = parse()
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # no launcher: one rank process per GPU, started before this process touches a GPU
+        sys.exit(spawn_ranks(a.gpus, sys.argv))
     if a.workload == "commit":
         return commit_workload(a)
     if a.workload == "keytags":
         return keytags_workload(a)
     if a.workload == "c5":
         return c5_workload(a)
-    import numpy as np
+    rc = block_checksum_workload(a)
+    if rc:
+        sys.exit(rc)
+
+
+def block_checksum_workload(a) -> int:
+    """c3 (N = 1) / c4 (N > 1): the BASELINE metric. Returns a non-zero exit code when
+    the printed root differs from the libxxhash fixture of the same workload."""
     import torch
 
     from storm_amd import dist as sdist
@@ -373,32 +497,51 @@ def main():
             dist.init_process_group("gloo")
     engine.init(gpu)
 
-    n_gpu = a.blocks                      # weak scaling: fixed blocks per GPU
-    n_total = n_gpu * world
-    lo = rank * n_gpu
+    # c3 at N = 1 (16M blocks); c4 at N > 1 (64M blocks in contiguous shards, strong
+    # scaling: 8M per GPU at N = 8). --blocks B: B per GPU instead (weak scaling).
+    if a.blocks:
+        n_total, scaling = a.blocks * world, "weak"
+    else:
+        n_total = a.total_blocks or (C3_BLOCKS if world == 1 else C4_BLOCKS)
+        scaling = "weak" if world == 1 else "strong"
+    lo, hi = sdist.shard_range(n_total, world, rank)
+    n_gpu = hi - lo
     arena_n = min(a.arena, n_gpu)
     passes = (n_gpu + arena_n - 1) // arena_n
     stream = torch.cuda.current_stream(dev)
     st = stream.cuda_stream
 
     arena = torch.empty((arena_n, BLOCK), dtype=torch.uint8, device=dev)
-    engine.fill_synthetic_device(arena.data_ptr(), BLOCK, arena_n, lo, 0x53544F524D, st)
     cs = torch.empty(n_gpu, dtype=torch.int64, device=dev)
     ws = torch.empty(max(engine.merkle_workspace_bytes(n_gpu, FANOUT) // 8, 1), dtype=torch.int64, device=dev)
     torch.cuda.synchronize()
 
-    ev = []  # (start, end) events around every hash-kernel launch of the timed steps
+    hash_ev, fill_ev = [], []  # (start, end[, blocks]) events of the timed steps, on `stream`
+
+    def ev_pair():
+        return torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 
     def step(record: bool):
+        # The shard's blocks do not fit in HBM (c3: 512 GiB per GPU), so each arena pass
+        # is regenerated with its own logical blocks lo + first .. (the on-device
+        # generator stands in for the data arriving). The regeneration is timed by its
+        # own events and taken out of the step time; the hash launches are timed too.
         for p in range(passes):
-            cnt = min(arena_n, n_gpu - p * arena_n)
-            if record:
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record(stream)
-            engine.checksum_device(arena.data_ptr(), BLOCK, cnt, cs[p * arena_n:].data_ptr(), BLOCK, 0, st)
-            if record:
-                e1.record(stream)
-                ev.append((e0, e1, cnt))
+            first = p * arena_n
+            cnt = min(arena_n, n_gpu - first)
+            f = ev_pair() if record else None
+            if f:
+                f[0].record(stream)
+            engine.fill_synthetic_device(arena.data_ptr(), BLOCK, cnt, lo + first, SYNTH_SEED, st)
+            e = ev_pair() if record else None
+            if f:
+                f[1].record(stream)
+                fill_ev.append(f)
+                e[0].record(stream)
+            engine.checksum_device(arena.data_ptr(), BLOCK, cnt, cs[first:].data_ptr(), BLOCK, 0, st)
+            if e:
+                e[1].record(stream)
+                hash_ev.append((e[0], e[1], cnt))
         root = engine.merkle_root_tensor(cs, lo, sdist.shard_node_addr_base(n_total, lo), REV, FANOUT, ws)
         if distributed:
             root, _ = sdist.global_root(root, REV, n_total, lambda t, r, ad: engine.combine_roots_tensor(t, r, ad, FANOUT))
@@ -418,15 +561,17 @@ def main():
     if distributed:
         dist.barrier()
     t1 = time.perf_counter()
-    elapsed = t1 - t0
+    wall = t1 - t0
+    fill_s = sum(f0.elapsed_time(f1) for f0, f1 in fill_ev) * 1e-3
+    elapsed = wall - fill_s  # the K steps without the arena regeneration
     if distributed:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed, wall], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        elapsed, wall = float(t[0].item()), float(t[1].item())
 
-    # dominant kernel: average launch duration from HIP events on its stream
-    kms = [e0.elapsed_time(e1) for (e0, e1, _) in ev]
-    kblocks = [c for (_, _, c) in ev]
+    # dominant kernel: per-launch durations from HIP events on its stream
+    kms = sorted(e0.elapsed_time(e1) for (e0, e1, _) in hash_ev)
+    kblocks = [c for (_, _, c) in hash_ev]
     avg_ms = sum(kms) / len(kms)
     avg_blocks = sum(kblocks) / len(kblocks)
     alg_bytes = avg_blocks * (BLOCK + 8)          # L bytes read + 8 bytes written per block
@@ -434,13 +579,14 @@ def main():
 
     total_bytes = n_total * BLOCK * a.steps
     value = total_bytes / elapsed / 2**30
-    traffic = None
+    traffic, prof = None, None
     tpath = os.path.join(ROOT, "profiles", "traffic.json")
     if os.path.exists(tpath):
         with open(tpath) as f:
             tj = json.load(f)
         if tj.get("arena_blocks") == arena_n and tj.get("kernel") == KERNEL:
             traffic = tj.get("hbm_bytes_per_launch")
+            prof = tj.get("source")
 
     # also report against a measured stream-read peak. Measured here, after
     # the timed region, on the same arena: the rate depends on where the arena lands in
@@ -450,27 +596,48 @@ def main():
     gather = ""
     if distributed:
         gather = " + RCCL all-gather of shard roots" if a.dist_backend == "nccl" else " + gloo all-gather of shard roots (rehearsal)"
+    rc = 0
     if rank == 0:
         root_t = engine.as_tuple(root)
+        want, fx_name = root_fixture(n_total, world, distributed)
+        if want is None:
+            check = "no fixture for this workload"
+        elif want == root_t:
+            check = f"match ({fx_name}, tests/golden/c3c4_roots.json)"
+        else:
+            check = f"MISMATCH vs {fx_name} fixture root 0x{want[0]:016x}"
+            rc = 3
+        cfg = "c3" if (world == 1 and n_total == C3_BLOCKS) else ("c4" if n_total == C4_BLOCKS else "custom")
         res = {
             "metric": METRIC, "value": round(value, 2), "unit": "GiB/s", "n_gpus": world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "u64", "data": "synthetic",
-            "config": {"workload": f"c3: {n_gpu / 2**20:g}M x 32 KiB blocks per GPU, XXH64 seed 0 (blocks.Checksum) "
+            "scaling": scaling, "vs_baseline": None, "dtype": "u64", "data": "synthetic",
+            "config": {"workload": f"{cfg}: {n_total / 2**20:g}M x 32 KiB blocks over {world} GPU(s) "
+                                   f"({n_gpu / 2**20:g}M on rank 0), XXH64 seed 0 (blocks.Checksum) "
                                    "+ shard Merkle pointer tree" + gather,
-                       "blocks_per_gpu": n_gpu, "block_bytes": BLOCK, "arena_blocks": arena_n,
-                       "passes_per_step": passes, "parallelism": f"dp{world} (contiguous block ranges)"},
+                       "total_blocks": n_total, "blocks_per_gpu": n_gpu, "block_bytes": BLOCK,
+                       "arena_blocks": arena_n, "passes_per_step": passes,
+                       "parallelism": f"dp{world} (contiguous block ranges)",
+                       "timed": "K steps between barrier + synchronize, minus the on-device regeneration of "
+                                "each arena pass (its own HIP events)",
+                       "ms_per_step_with_regeneration": round(wall / a.steps * 1e3, 3)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "kernel": KERNEL, "avg_launch_ms": round(avg_ms, 4),
-                         "algorithmic_bytes_per_launch": int(alg_bytes), "measured_read_peak": read_peak},
+                         "launch_ms": {"n": len(kms), "min": round(kms[0], 4),
+                                       "median": round(kms[len(kms) // 2], 4), "max": round(kms[-1], 4)},
+                         "algorithmic_bytes_per_launch": int(alg_bytes), "profile_source": prof,
+                         "measured_read_peak": read_peak},
             "root": "0x%016x" % root_t[0],
+            "root_pointer": ["0x%016x" % v for v in root_t[:3]] + [root_t[3]],
+            "root_check": check,
         }
         if world == 1 and not a.no_cpu:
             res["cpu_baseline"] = cpu_baseline(a.cpu_seconds)
         print(json.dumps(res), flush=True)
     if distributed:
         dist.destroy_process_group()
+    return rc
 
 
 if __name__ == "__main__":

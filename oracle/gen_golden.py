@@ -310,7 +310,111 @@ def gen_big() -> None:
                                  "seed": h(SEED), "digests": res})
 
 
+def pack_level_np(cs: np.ndarray, addr_base: int, rev: int, typ: int, fanout: int) -> np.ndarray:
+    """Every parent node of one tree level as storm pointer.Block bytes, [pm, size] uint8
+    (vectorised form of pack_pointer_block over children {cs[i], addr_base + i, rev})."""
+    m = len(cs)
+    pm = (m + fanout - 1) // fanout
+    size = (25 * fanout + 7) & ~7
+    ptr = np.zeros((pm * fanout, 3), dtype="<u8")
+    ptr[:m, 0] = cs
+    ptr[:m, 1] = np.arange(addr_base, addr_base + m, dtype=np.uint64)
+    ptr[:m, 2] = rev
+    typ_b = np.zeros(pm * fanout, dtype=np.uint8)
+    typ_b[:m] = typ
+    out = np.zeros((pm, size), dtype=np.uint8)
+    out[:, :24 * fanout] = ptr.view(np.uint8).reshape(pm, 24 * fanout)
+    out[:, 24 * fanout:25 * fanout] = typ_b.reshape(pm, fanout)
+    return out
+
+
+def tree_root_np(leaf_cs: np.ndarray, leaf_base: int, node_base: int, rev: int, fanout: int):
+    """tree_root for large n: same rule, levels packed with pack_level_np."""
+    n = len(leaf_cs)
+    if n <= 1:
+        return tree_root([int(x) for x in leaf_cs], leaf_base, node_base, rev, fanout)
+    cur, base, typ, nxt = np.asarray(leaf_cs, dtype=np.uint64), leaf_base, 2, node_base
+    while len(cur) > 1:
+        nodes = pack_level_np(cur, base, rev, typ, fanout)
+        cur = np.array([xx(memoryview(nodes[k])) for k in range(nodes.shape[0])], dtype=np.uint64)
+        base, nxt, typ = nxt, nxt + len(cur), 1
+    return (int(cur[0]), base, rev, typ)
+
+
+def _c4_worker(args):
+    first, count, path, total = args
+    sys.path.insert(0, ROOT)
+    from oracle import oracle as o  # generator only; hashing stays libxxhash
+    stride = 32768
+    cs = np.memmap(path, dtype=np.uint64, mode="r+", shape=(total,))
+    buf = o.fill_synthetic(count, stride, first)
+    mv = memoryview(buf)
+    cs[first:first + count] = [xxhash.xxh64_intdigest(mv[i * stride:(i + 1) * stride]) for i in range(count)]
+    cs.flush()
+    return count
+
+
+def gen_c4() -> None:
+    """c3 / c4 roots (BASELINE.json configs[2], configs[3]) over the synthetic 32 KiB
+    blocks 0..64M-1, hashed with libxxhash on every host core (several minutes).
+
+    c3: the 16M-block shard tree bench.py builds at N = 1 (leaves 0..16M-1, leaf
+    addresses = block index, interior nodes from 16M, BirthRevision 1, fan-out 1200).
+    c4: 64M blocks split into `world` contiguous shards (storm_amd.dist.shard_range
+    rule restated here); shard s's tree has leaf addresses lo_s.., interior nodes from
+    64M + lo_s; the global root hashes one pointer block of the world shard roots and
+    has address 2 * 64M (storm_amd.dist.global_root_addr). Roots for world 2, 4 and 8
+    (the bench's N > 1 lines, strong scaling over the c4 set)."""
+    import multiprocessing as mp
+    n_total, rev, f = 1 << 26, 1, 1200
+    # the numpy packer agrees with the per-entry packer on ragged trees
+    for n_chk, f_chk in ((12345, 10), (5000, 1200), (1201, 1200)):
+        leaf = splitmix_np(np.arange(n_chk, dtype=np.uint64) ^ np.uint64(SEED))
+        assert tree_root_np(leaf, 3, n_chk + 3, 5, f_chk) == tree_root(leaf, 3, n_chk + 3, 5, f_chk)
+    path = os.environ.get("C4_CS_CACHE", "/tmp/c4_checksums.u64")
+    t = time.time()
+    if not (os.path.exists(path) and os.path.getsize(path) == 8 * n_total):
+        np.memmap(path, dtype=np.uint64, mode="w+", shape=(n_total,)).flush()
+        chunk = 1 << 14
+        jobs = [(first, chunk, path, n_total) for first in range(0, n_total, chunk)]
+        with mp.get_context("fork").Pool(max(1, (os.cpu_count() or 2) - 1)) as pool:
+            done = 0
+            for c in pool.imap_unordered(_c4_worker, jobs):
+                done += c
+                if done % (1 << 22) == 0:
+                    print(f"  c4 checksums {done >> 20}M / 64M {time.time() - t:.0f}s", flush=True)
+    cs = np.memmap(path, dtype=np.uint64, mode="r", shape=(n_total,))
+    # pinned against the independent single-process digests of gen_big (16M prefix)
+    with open(os.path.join(OUT, "synth_digests.json")) as fh:
+        dig = json.load(fh)["digests"][str(1 << 24)]["digest"]
+    assert h(xx(np.ascontiguousarray(cs[:1 << 24]).astype("<u8").tobytes())) == dig, "16M prefix digest"
+    c3 = tree_root_np(cs[:1 << 24], 0, 1 << 24, rev, f)
+    worlds = {}
+    for world in (2, 4, 8):
+        table = []
+        for r in range(world):
+            q, rem = divmod(n_total, world)
+            lo = r * q + min(r, rem)
+            hi = lo + q + (1 if r < rem else 0)
+            table.append(tree_root_np(cs[lo:hi], lo, n_total + lo, rev, f))
+        groot = (xx(pack_pointer_block(table, f)), 2 * n_total, rev, 1)
+        worlds[str(world)] = {"shard_roots": [[h(v) for v in r_[:3]] + [r_[3]] for r_ in table],
+                              "global_root": [h(v) for v in groot[:3]] + [groot[3]]}
+    write("c3c4_roots.json", {
+        "rule": "synth_c1.json rule, stride = length = 32768, fan-out 1200, BirthRevision 1; see gen_c4",
+        "seed": h(SEED),
+        "c3": {"n": 1 << 24, "leaf_addr_base": 0, "node_addr_base": 1 << 24,
+               "root": [h(v) for v in c3[:3]] + [c3[3]]},
+        "c4": {"n_total": n_total, "digest": h(xx(np.ascontiguousarray(cs).astype("<u8").tobytes())),
+               "every_1048576th": [h(int(v)) for v in cs[::1 << 20]], "worlds": worlds},
+    })
+    print(f"  c4 done {time.time() - t:.0f}s")
+
+
 if __name__ == "__main__":
+    if "--c4" in sys.argv:  # only the c3/c4 roots (several minutes on every core)
+        gen_c4()
+        sys.exit(0)
     gen_kat()
     gen_synth_c1()
     gen_mixed()
