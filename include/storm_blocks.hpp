@@ -9,8 +9,11 @@
 // Block layouts (Go amd64, padding included) mirror blocks/{pointer,blob,objectlist,
 // spacelist,singularity}/block.go; the `test` build-tag fan-outs are template args.
 //
-// Every hash is computed on the gfx950 device by libstormck; a device failure throws
-// storm::blocks::DeviceError (Go's Checksum cannot fail, so there is no error value).
+// Single calls (Checksum, BlockChecksum, VerifyChecksum) hash on the calling thread
+// through stormck_xxh64, the library's single-call leg: one buffer is four serial
+// XXH64 chains, which one host core walks faster than the GPU, and like
+// Go's Checksum it cannot fail. Batches run on the gfx950 device; a device failure
+// throws storm::blocks::DeviceError. ChecksumGPU is the single call on the device.
 #pragma once
 
 #include <cstddef>
@@ -75,9 +78,12 @@ inline std::string go_hex(uint64_t v) {
 }  // namespace detail
 
 // Checksum computes checksum of bytes.
-inline Hash Checksum(const void* b, size_t n) {
+inline Hash Checksum(const void* b, size_t n) { return stormck_xxh64(b, n); }
+
+// The same single call on the device (k_xxh64_single), up to 256 MiB.
+inline Hash ChecksumGPU(const void* b, size_t n) {
     uint64_t out = 0;
-    detail::check(stormck_checksum(b, n, &out));
+    detail::check(stormck_checksum_gpu(b, n, &out));
     return out;
 }
 inline Hash Checksum(const std::vector<uint8_t>& b) { return Checksum(b.data(), b.size()); }

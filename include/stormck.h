@@ -19,8 +19,11 @@
  * "_host" entry points take host memory and return when the results are in host
  * memory (H2D -> kernel -> D2H, pipelined).
  *
- * There is no CPU fallback: without a usable gfx950 device every compute entry
- * point returns STORMCK_ENODEV.
+ * There is no CPU fallback: without a usable gfx950 device every batched, device
+ * and Merkle entry point returns STORMCK_ENODEV. The one host computation is the
+ * latency leg of a SINGLE call (stormck_xxh64 / stormck_checksum): one buffer is four
+ * serial XXH64 chains, which one host core walks faster than the GPU at every length
+ * (DESIGN.md §5), so single calls stay on the host by design.
  */
 #ifndef STORMCK_H
 #define STORMCK_H
@@ -98,8 +101,18 @@ int stormck_checksum_host(const void* base, uint64_t stride, const uint32_t* len
  * *n_bad = mismatch count. Returns STORMCK_EMISMATCH if n_bad > 0. */
 int stormck_verify_host(const void* base, uint64_t stride, const uint32_t* lens, uint32_t len, uint64_t n,
                         const uint64_t* expected, uint64_t* first_bad, uint64_t* n_bad);
-/* Single-buffer blocks.Checksum through the device (batch of one). */
+/* ---- single calls (Go blocks.Checksum / BlockChecksum / VerifyChecksum, one block)
+ * stormck_xxh64: XXH64 seed 0 of p[0..n_bytes) on the calling host thread; cannot
+ * fail (p may be NULL only when n_bytes == 0). What the Go shim's Checksum calls.
+ * stormck_checksum: the single-call dispatch. Below the measured host/device crossover
+ * (never reached: the device single call is slower at every length) it
+ * is stormck_xxh64; any length, no device needed.
+ * stormck_checksum_gpu: the same hash through the device: one k_xxh64_single launch
+ * for slices up to 64 KiB, the host pipeline with a batch of one up to 256 MiB;
+ * longer slices return STORMCK_EINVAL. Needs a device. */
+uint64_t stormck_xxh64(const void* p, uint64_t n_bytes);
 int stormck_checksum(const void* p, uint64_t n_bytes, uint64_t* out);
+int stormck_checksum_gpu(const void* p, uint64_t n_bytes, uint64_t* out);
 /* Page-lock a host range so the host path can DMA from it without staging copies. */
 int stormck_host_register(void* p, uint64_t bytes);
 int stormck_host_unregister(void* p);

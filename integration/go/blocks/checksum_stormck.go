@@ -4,11 +4,16 @@
 //
 // A storm maintainer adds this file to github.com/outofforest/storm/blocks and
 // puts `//go:build !stormck` on the existing blocks/checksum.go. `go build
-// -tags stormck` then routes every block checksum through libstormck (MI355X,
-// gfx950); without the tag storm is unchanged. Signatures of Checksum,
-// BlockChecksum and VerifyChecksum are identical to blocks/checksum.go:10-27;
-// ChecksumBatch / VerifyChecksumBatch / RegisterHostMemory are additions for
-// batched callers (level-synchronous commit, batched cold-read verify).
+// -tags stormck` then routes block checksums through libstormck; without the tag
+// storm is unchanged. Signatures of Checksum, BlockChecksum and VerifyChecksum are
+// identical to blocks/checksum.go:10-27. Those single calls (one block, from
+// cache/trace.go:282,307, cache/cache.go:73,160, persistence/init.go:44) take the
+// library's host leg, stormck_xxh64: one buffer is four serial XXH64 chains, which
+// one core walks faster than a GPU launch (DESIGN.md §5), so unchanged callers pay
+// what xxhash.Sum64 costs them today, and like Sum64 the call cannot fail.
+// ChecksumBatch / VerifyChecksumBatch / ReadVerifyBatch / CommitBatch are additions
+// for batched callers (level-synchronous commit, batched cold-read verify): those
+// run on the MI355X (gfx950).
 //
 // Not compiled in this repository (no Go toolchain in the build image); the C
 // side it binds is exercised by tests/test_abi.py and tests/test_cpp_mirror.py.
@@ -47,15 +52,11 @@ func BlockChecksum[T Block](b *T) Hash {
 }
 
 // Checksum computes checksum of bytes (XXH64 seed 0, bit-exact with xxhash.Sum64).
-// The reference cannot fail; a device failure here is unrecoverable and panics.
+// Like the reference it cannot fail: stormck_xxh64 hashes on the calling thread.
 func Checksum(b []byte) Hash {
-	var out C.uint64_t
 	// cgo pointer rules: b holds no Go pointers and libstormck does not retain it
 	// after the (synchronous) call returns.
-	if rc := C.stormck_checksum(bytesPtr(b), C.uint64_t(len(b)), &out); rc != C.STORMCK_OK {
-		panic(stormckError(rc))
-	}
-	return Hash(out)
+	return Hash(C.stormck_xxh64(bytesPtr(b), C.uint64_t(len(b))))
 }
 
 // VerifyChecksum verifies that checksum of provided data matches the expected one.
@@ -89,6 +90,9 @@ func ChecksumBatch(data []byte, n, stride, length int, out []Hash) error {
 func VerifyChecksumBatch(data []byte, n, stride, length int, expected []Hash) (firstBad, nBad int, err error) {
 	if n == 0 {
 		return 0, 0, nil
+	}
+	if len(expected) < n || len(data) < (n-1)*stride+length {
+		return 0, 0, errors.New("VerifyChecksumBatch: buffer too small")
 	}
 	var fb, nb C.uint64_t
 	rc := C.stormck_verify_host(bytesPtr(data), C.uint64_t(stride), nil, C.uint32_t(length), C.uint64_t(n),
@@ -124,9 +128,12 @@ func ReadVerifyBatch(f *os.File, addresses []BlockAddress, lens []uint32, expect
 }
 
 // RegisterHostMemory page-locks a long-lived buffer (e.g. cache.data, allocated once
-// in cache.New, cache/cache.go:36-40) so batches DMA straight from it. The Go heap
-// does not move large allocations; the caller keeps the slice alive until
-// UnregisterHostMemory.
+// in cache.New, cache/cache.go:36-40) so batches DMA straight from it and CommitBatch
+// can let the GPU read and write it in place. This keeps a reference to the memory
+// inside the HIP runtime after the call returns, which the cgo pointer rules do not
+// allow for Go-heap memory: allocate the buffer outside the Go heap (C.malloc, mmap or
+// hipHostMalloc, wrapped with unsafe.Slice) and keep it registered until
+// UnregisterHostMemory. See INTEGRATION.md §3.
 func RegisterHostMemory(b []byte) error {
 	if rc := C.stormck_host_register(bytesPtr(b), C.uint64_t(len(b))); rc != C.STORMCK_OK {
 		return stormckError(rc)

@@ -2,7 +2,8 @@
 
 Loads the in-tree build ``storm_amd/lib/libstormck.so``. There is no fallback:
 if the library is missing, importing this module raises; if no gfx950 device is
-present, every compute call raises :class:`NoDeviceError`.
+present, every batched / device compute call raises :class:`NoDeviceError`
+(single calls hash on the host by design: include/stormck.h).
 """
 from __future__ import annotations
 
@@ -50,7 +51,9 @@ SIGNATURES = {
     "stormck_verify_device": (c_int, [c_void_p, c_uint64, c_void_p, c_uint32, c_uint64, c_void_p, c_void_p, c_void_p]),
     "stormck_checksum_host": (c_int, [c_void_p, c_uint64, c_void_p, c_uint32, c_uint64, c_void_p]),
     "stormck_verify_host": (c_int, [c_void_p, c_uint64, c_void_p, c_uint32, c_uint64, c_void_p, c_void_p, c_void_p]),
+    "stormck_xxh64": (c_uint64, [c_void_p, c_uint64]),
     "stormck_checksum": (c_int, [c_void_p, c_uint64, POINTER(c_uint64)]),
+    "stormck_checksum_gpu": (c_int, [c_void_p, c_uint64, POINTER(c_uint64)]),
     "stormck_host_register": (c_int, [c_void_p, c_uint64]),
     "stormck_host_unregister": (c_int, [c_void_p]),
     "stormck_host_device_pointer": (c_int, [c_void_p, c_void_p]),

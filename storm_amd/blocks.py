@@ -12,8 +12,13 @@ Same names, argument meaning and error behaviour as the reference:
 =====================  ===========================================================
 
 plus the batch entry points the GPU path exists for (``ChecksumBatch``,
-``VerifyChecksumBatch``). Every hash is computed by the gfx950 kernels in
-libstormck; there is no host-side hash in the product.
+``VerifyChecksumBatch``, ``ReadVerifyBatch``; f1's batched commit is in
+``storm_amd.commit``). Batches run on the gfx950 kernels in libstormck and fail
+loudly without a device. A single ``Checksum`` is one buffer, four serial XXH64
+chains: libstormck hashes it on the calling host thread (stormck_checksum, the
+latency leg SURVEY.md §8b specifies; measured faster than the device single call at
+every length). ``ChecksumGPU`` is the same call through the device
+(k_xxh64_single), for tests and A/B.
 """
 from __future__ import annotations
 
@@ -70,10 +75,19 @@ def _as_u8(b) -> np.ndarray:
 
 
 def Checksum(b) -> Hash:
-    """XXH64 (seed 0) of the bytes of ``b``."""
+    """XXH64 (seed 0) of the bytes of ``b`` (stormck_checksum: the single-call leg)."""
     a = _as_u8(b)
     out = ctypes.c_uint64(0)
     _lib.check(_lib.lib.stormck_checksum(a.ctypes.data if a.size else None, a.size, ctypes.byref(out)))
+    return out.value
+
+
+def ChecksumGPU(b) -> Hash:
+    """The same hash through the device (stormck_checksum_gpu): k_xxh64_single for up
+    to 64 KiB, a batch of one through the host pipeline up to 256 MiB."""
+    a = _as_u8(b)
+    out = ctypes.c_uint64(0)
+    _lib.check(_lib.lib.stormck_checksum_gpu(a.ctypes.data if a.size else None, a.size, ctypes.byref(out)))
     return out.value
 
 

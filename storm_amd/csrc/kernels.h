@@ -936,6 +936,164 @@ __global__ __launch_bounds__(256) void k_pointer_level(const uint64_t* __restric
     if (j == 0 && pj < pm) parent_cs[pj] = h;
 }
 
+// Wide levels at a fan-out F that tiles evenly (storm's F = 1200, 30,000 B nodes):
+// one wave per 16 nodes, a quad per node, and the node words staged in LDS already
+// multiplied by P2, so the chain lanes issue only add, rotate and the P1 multiply.
+//
+// k_pointer_level above makes every lane synthesise its own word per round: the index
+// arithmetic, a field select, an 8-byte child load and the P2 multiply sit in the
+// chain's instruction stream (~25 instructions a round, 148 us for the 13,981 nodes
+// over 16M leaves). Here the wave instead works tile by tile. A tile is 15 stripes of
+// every node = 20 child slots (60 words); the pointer region is F/20 tiles. For each
+// tile:
+//   * produce: lane l owns 5 (node, slot) items. Their child checksums arrive
+//     D tiles ahead in registers (coalesced 8-byte loads: the wave's 16 nodes are
+//     contiguous children), and the lane writes {cs*P2, (addr_base+i)*P2, rev*P2}
+//     into the tile's LDS ring slot. Address words are linear in i, so each item's
+//     premultiplied address advances by 20*P2 per tile (one 64-bit add);
+//   * consume: the quads walk the previous tile's 15 rounds from LDS. A node's tile
+//     row is 15 stripes (odd), so the 8 quads of a 32-lane ds_read_b64 group hit 8
+//     distinct 32-byte bank groups.
+// One wave owns its LDS (15 KiB), so no barrier: LDS operations of one wave execute in
+// order. The type bytes (37 stripes + the 16-byte tail at F = 1200) are the constant
+// type byte for full nodes; only the level's last node can be partial, and the one
+// wave that holds it takes the masked variant (FULL = false) of the same code.
+constexpr uint32_t kRingTileStripes = 15;  // stripes of one node per tile (odd: conflict-free reads)
+constexpr uint32_t kRingTileSlots = 20;    // child slots per tile (60 words)
+
+template <uint32_t F, int D, bool FULL>
+__device__ __forceinline__ void pointer_level_ring_body(const uint64_t* __restrict__ cs, uint64_t m, uint64_t pm,
+                                                        uint64_t node0, uint64_t addr_base, uint64_t rev, uint8_t type,
+                                                        uint64_t* __restrict__ parent_cs,
+                                                        uint64_t (*ring)[16][kRingTileStripes * 4]) {
+    constexpr uint32_t TS = kRingTileStripes, SL = kRingTileSlots, NT = F / SL, IT = 16 * SL / 64;
+    constexpr uint32_t kSize = (F * 25u + 7u) & ~7u, kWords = kSize / 8, kNst = kSize / 32;
+    constexpr uint32_t kPtrStripes = 3 * F / 4;
+    static_assert(F % SL == 0 && NT % D == 0 && IT * 64 == 16 * SL, "tile shape");
+    const uint32_t lane = threadIdx.x, q = lane >> 2, j = lane & 3;
+    const uint64_t rep = 0x0101010101010101ULL * type;
+    const uint64_t rev_pm = rev * kP2, step_pm = static_cast<uint64_t>(SL) * kP2;
+
+    // producer items: item r of this lane is slot pu[r] of node pq[r] in every tile
+    uint32_t pq[IT], pu[IT], cnt_i[IT];
+    const uint64_t* gp[IT];
+    uint64_t addr_pm[IT];
+#pragma unroll
+    for (uint32_t r = 0; r < IT; ++r) {
+        const uint32_t item = lane + 64 * r;
+        pq[r] = item / SL;
+        pu[r] = item % SL;
+        uint64_t node = node0 + pq[r];
+        if (!FULL) {
+            if (node >= pm) node = pm - 1;  // idle quads of the last wave: hash a copy, store nothing
+            const uint64_t left = m - node * F;
+            cnt_i[r] = static_cast<uint32_t>(left < F ? left : F);
+        }
+        const uint64_t g = node * F + pu[r];
+        gp[r] = cs + g;
+        addr_pm[r] = (addr_base + g) * kP2;
+    }
+    uint64_t raw[D][IT];
+    auto load_tile = [&](uint32_t t, uint64_t* dst) {
+#pragma unroll
+        for (uint32_t r = 0; r < IT; ++r) {
+            if (FULL) {
+                dst[r] = gp[r][t * SL];
+            } else {
+                const uint32_t slot = t * SL + pu[r];
+                dst[r] = slot < cnt_i[r] ? gp[r][t * SL] : 0;
+            }
+        }
+    };
+    auto produce = [&](uint32_t t, const uint64_t* src, int slot) {
+        uint64_t* row_base = &ring[slot][0][0];
+#pragma unroll
+        for (uint32_t r = 0; r < IT; ++r) {
+            uint64_t* w = row_base + pq[r] * (TS * 4) + 3 * pu[r];
+            const uint64_t a = addr_pm[r] + t * step_pm;
+            if (FULL) {
+                w[0] = src[r] * kP2;
+                w[1] = a;
+                w[2] = rev_pm;
+            } else {
+                const bool valid = t * SL + pu[r] < cnt_i[r];
+                w[0] = src[r] * kP2;  // src is 0 for a missing child
+                w[1] = valid ? a : 0;
+                w[2] = valid ? rev_pm : 0;
+            }
+        }
+    };
+
+    uint64_t acc = acc_seed(j);
+#pragma unroll
+    for (int d = 0; d < D; ++d) load_tile(d, raw[d]);
+    produce(0, raw[0], 0);
+    load_tile(D, raw[0]);
+    // Tile t: produce tile t+1 into ring slot (t+1)&1 and refill its registers with
+    // tile t+1+D, then walk the 15 chain rounds of tile t (slot t&1). D is even and t0
+    // a multiple of D, so the slots are compile-time constants. (Merging the three
+    // into one basic block so the scheduler interleaves them measured 6 % slower.)
+    static_assert(D % 2 == 0, "static ring slots");
+    for (uint32_t t0 = 0; t0 < NT; t0 += D) {
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            const uint32_t t = t0 + d;
+            const int nb = (d + 1) % D;
+            if (t + 1 < NT) {
+                produce(t + 1, raw[nb], (d + 1) & 1);
+                if (t + 1 + D < NT) load_tile(t + 1 + D, raw[nb]);
+            }
+            __builtin_amdgcn_wave_barrier();
+            const uint64_t* row = &ring[d & 1][q][j];
+#pragma unroll
+            for (uint32_t s = 0; s < TS; ++s) acc = round_pm(acc, row[4 * s]);
+            __builtin_amdgcn_wave_barrier();
+        }
+    }
+    // type bytes: stripes kPtrStripes .. kNst-1, then the tail words
+    const uint64_t node = node0 + q;
+    uint32_t cnt = F;
+    if (!FULL) {
+        const uint64_t nn = node < pm ? node : pm - 1;
+        const uint64_t left = m - nn * F;
+        cnt = static_cast<uint32_t>(left < F ? left : F);
+    }
+    auto type_word = [&](uint32_t k) -> uint64_t {  // k: word index within the type region
+        if (FULL) return rep;
+        const uint32_t pos = 8 * k;
+        if (pos >= cnt) return 0;
+        const uint32_t nb = (cnt - pos) >= 8 ? 8 : (cnt - pos);
+        return nb == 8 ? rep : (rep & ((1ULL << (8 * nb)) - 1));
+    };
+    if (FULL) {
+        const uint64_t rep_pm = rep * kP2;
+        for (uint32_t s = kPtrStripes; s < kNst; ++s) acc = round_pm(acc, rep_pm);
+    } else {
+        for (uint32_t s = kPtrStripes; s < kNst; ++s) acc = round(acc, type_word(4 * (s - kPtrStripes) + j));
+    }
+    const uint64_t v1 = quad_bcast<0>(acc), v2 = quad_bcast<1>(acc), v3 = quad_bcast<2>(acc), v4 = quad_bcast<3>(acc);
+    uint64_t h = converge(v1, v2, v3, v4) + kSize;
+    for (uint32_t k = 4 * kNst; k < kWords; ++k) {
+        h ^= round(0, type_word(k - 3 * F));
+        h = rotl<27>(h) * kP1 + kP4;
+    }
+    h = avalanche(h);
+    if (j == 0 && node < pm) parent_cs[node] = h;
+}
+
+template <uint32_t F, int D>
+__global__ __launch_bounds__(64) void k_pointer_level_ring(const uint64_t* __restrict__ cs, uint64_t m,
+                                                           uint64_t addr_base, uint64_t rev, uint8_t type,
+                                                           uint64_t* __restrict__ parent_cs) {
+    __shared__ uint64_t ring[2][16][kRingTileStripes * 4];  // 15 KiB: two tiles of 16 nodes
+    const uint64_t pm = (m + F - 1) / F;
+    const uint64_t node0 = static_cast<uint64_t>(blockIdx.x) * 16;
+    if (node0 + 16 <= m / F)  // every node of this wave has F children (wave-uniform branch)
+        pointer_level_ring_body<F, D, true>(cs, m, pm, node0, addr_base, rev, type, parent_cs, ring);
+    else
+        pointer_level_ring_body<F, D, false>(cs, m, pm, node0, addr_base, rev, type, parent_cs, ring);
+}
+
 // Small levels (a handful of nodes, e.g. the top of a shard tree): one workgroup per
 // node. All 256 threads synthesise the node's words into LDS at once, then quad 0
 // hashes from LDS. A quad synthesising its own words issues ~25 instructions per

@@ -21,6 +21,7 @@
 
 #include "../../include/stormck.h"
 #include "kernels.h"
+#include "xxh64_host.h"
 
 using namespace stormck;
 
@@ -148,6 +149,9 @@ constexpr uint32_t kMaxFanout = 1u << 16;
 // a node is then about one XXH64 chain (~26 us for 30,000 B); larger levels put a quad
 // on each node, 64 nodes per workgroup, to keep every CU busy.
 constexpr uint64_t kWideNodes = 256;
+// k_pointer_level_ring: child-checksum tiles loaded this many tiles ahead of the LDS
+// tile being produced (each tile is 15 rounds of the chain).
+constexpr int kRingPrefetch = 4;
 
 // Skewed persistent streaming kernel (k_xxh64_glds_skew): wave v starts kSkewTiles*v
 // tiles late, 4 KiB apart at 16-stripe tiles (profiles/r01_probe_phase_skew.txt). Its
@@ -696,12 +700,37 @@ int stormck_verify_host(const void* base, uint64_t stride, const uint32_t* lens,
     return STORMCK_OK;
 }
 
+uint64_t stormck_xxh64(const void* p, uint64_t n_bytes) {
+    static const uint8_t empty = 0;
+    return host::xxh64(n_bytes ? p : &empty, n_bytes);
+}
+
 int stormck_checksum(const void* p, uint64_t n_bytes, uint64_t* out) {
     if (!out) return fail(STORMCK_EINVAL, "out is null");
-    if (n_bytes > 0xffffffffULL) return fail(STORMCK_EINVAL, "block longer than 4 GiB");
+    if (n_bytes > 0 && !p) return fail(STORMCK_EINVAL, "p is null");
+    // Latency dispatch of a single call. One buffer is four serial chains, so the GPU
+    // brings no parallelism to it: measured on MI355X, the device single call
+    // (stormck_checksum_gpu) is slower than one host core at every length, 72 B to
+    // 256 MiB ("Single calls"). The crossover is therefore "never";
+    // STORMCK_SINGLE_GPU_MIN=<bytes> sends single calls of at least that many bytes to
+    // the device (A/B measurement only).
+    static const uint64_t gpu_min = [] {
+        const char* e = std::getenv("STORMCK_SINGLE_GPU_MIN");
+        return e ? std::strtoull(e, nullptr, 10) : UINT64_MAX;
+    }();
+    if (n_bytes >= gpu_min) return stormck_checksum_gpu(p, n_bytes, out);
+    *out = stormck_xxh64(p, n_bytes);
+    return STORMCK_OK;
+}
+
+int stormck_checksum_gpu(const void* p, uint64_t n_bytes, uint64_t* out) {
+    if (!out) return fail(STORMCK_EINVAL, "out is null");
     static const uint8_t empty = 0;
     if (n_bytes == 0) p = &empty;  // XXH64 of an empty slice: nothing is read
     if (!p) return fail(STORMCK_EINVAL, "p is null");
+    if (n_bytes > kChunkBytes)
+        return fail(STORMCK_EINVAL, "single device call longer than the 256 MiB staging chunk "
+                                    "(stormck_checksum hashes any length)");
     if (n_bytes > kSingleMax)
         return host_pipeline(p, 0, nullptr, static_cast<uint32_t>(n_bytes), 1, out, nullptr, nullptr, nullptr);
     // latency path: memcpy into pinned staging, one kernel that reads it over PCIe and
@@ -758,6 +787,20 @@ int stormck_pointer_level_device(const uint64_t* d_child_cs, uint64_t m, uint64_
         hipLaunchKernelGGL(k_pointer_level_wide, dim3(static_cast<unsigned>(pm)), dim3(kThreads), 0,
                            static_cast<hipStream_t>(stream), d_child_cs, m, child_addr_base, rev, child_type, fanout,
                            d_parent_cs);
+        HIP_TRY(hipGetLastError());
+        return STORMCK_OK;
+    }
+    static const bool ring_on = [] {
+        const char* e = std::getenv("STORMCK_POINTER_RING");  // probe knob: "0" = the register-quad kernel
+        return !(e && e[0] == '0');
+    }();
+    if (ring_on && fanout == STORMCK_POINTERS_PER_BLOCK) {
+        // storm's fan-out: one wave per 16 nodes, premultiplied words staged in LDS
+        const uint64_t waves = (pm + 15) / 16;
+        if (waves > 0x7fffffffULL) return fail(STORMCK_EINVAL, "level too large");
+        hipLaunchKernelGGL((k_pointer_level_ring<STORMCK_POINTERS_PER_BLOCK, kRingPrefetch>),
+                           dim3(static_cast<unsigned>(waves)), dim3(64), 0, static_cast<hipStream_t>(stream),
+                           d_child_cs, m, child_addr_base, rev, child_type, d_parent_cs);
         HIP_TRY(hipGetLastError());
         return STORMCK_OK;
     }
@@ -857,9 +900,14 @@ int stormck_read_verify_fd(int fd, const uint64_t* addresses, const uint32_t* le
     if (n == 0) return STORMCK_OK;
     if (fd < 0 || !addresses || !lens || !dst || !expected) return fail(STORMCK_EINVAL, "null argument");
     const bool full = (flags & STORMCK_READ_FULL_BLOCK) != 0;
+    if (block_size == 0) return fail(STORMCK_EINVAL, "block_size is 0");
+    const uint64_t max_addr = (static_cast<uint64_t>(INT64_MAX) - block_size) / block_size;
     for (uint64_t i = 0; i < n; ++i) {
         const uint64_t want = full ? block_size : lens[i];
         if (lens[i] > block_size || want > dst_stride) return fail(STORMCK_EINVAL, "block does not fit its slot");
+        if (addresses[i] > max_addr)
+            return fail(STORMCK_EINVAL, "address " + std::to_string(addresses[i]) + " of block index " +
+                                            std::to_string(i) + " is beyond any file offset");
     }
     int rc = device_check();
     if (rc) return rc;

@@ -1,4 +1,5 @@
-// C++ mirror of storm's blocks tests, run against libstormck on the GPU.
+// C++ mirror of storm's blocks tests, run against libstormck (batches and ChecksumGPU on
+// the GPU, single calls on the library's host leg).
 // Each TEST mirrors a reference test (file:line in its comment). Relations are
 // asserted here; absolute values are printed as one JSON object for
 // tests/test_cpp_mirror.py to compare with tests/golden/layouts.json.
@@ -44,6 +45,7 @@ static std::string TestPointerChecksum() {
     b->Pointers[2].Checksum = 4;
     seq.push_back(BlockChecksum(b.get()));
     for (size_t i = 1; i < seq.size(); ++i) EXPECT(seq[i] != seq[i - 1]);
+    EXPECT(ChecksumGPU(b.get(), sizeof(*b)) == seq.back());  // the device single call agrees
     std::string out = "[";
     for (size_t i = 0; i < seq.size(); ++i) out += (i ? "," : "") + hex(seq[i]);
     return out + "]";
@@ -151,6 +153,8 @@ static void TestNewBlocksProduceConsistentResult() {
 static void TestKnownAnswers() {
     EXPECT(Checksum("abc", 3) == 0x44BC2CF5AD770999ULL);
     EXPECT(Checksum(nullptr, 0) == 0xEF46DB3751D8E999ULL);
+    EXPECT(ChecksumGPU("abc", 3) == 0x44BC2CF5AD770999ULL);
+    EXPECT(ChecksumGPU(nullptr, 0) == 0xEF46DB3751D8E999ULL);
     auto err = VerifyChecksum(42, "abc", 3, 0);
     EXPECT(err && err->message() == "checksum mismatch for block 42, computed: 0x44bc2cf5ad770999, expected: 0x0");
 }

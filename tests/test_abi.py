@@ -1,7 +1,9 @@
 """The C-ABI library loads and exports exactly what include/stormck.h declares (CPU).
 
-No compute happens here: on a machine without a gfx950 device every compute
-entry point must fail loudly (STORMCK_ENODEV), never fall back to the CPU.
+On a machine without a gfx950 device every batched / device entry point must fail
+loudly (STORMCK_ENODEV), never fall back to the CPU. The one host computation is the
+single-call latency leg (stormck_xxh64 / stormck_checksum), checked here against the
+oracle and the known answers.
 """
 import ctypes
 import os
@@ -66,9 +68,11 @@ def test_no_device_fails_loudly():
     from storm_amd import _lib, blocks, engine
     assert _lib.device_count() == 0
     with pytest.raises(_lib.NoDeviceError):
-        blocks.Checksum(b"abc")
+        blocks.ChecksumGPU(b"abc")
     with pytest.raises(_lib.NoDeviceError):
         blocks.ChecksumBatch(bytes(64), 2, 32, 32)
+    with pytest.raises(_lib.NoDeviceError):
+        blocks.VerifyChecksumBatch(bytes(64), 2, 32, [0, 0], 32)
     with pytest.raises(_lib.NoDeviceError):
         engine.checksum_device(1 << 20, 32, 1, 1 << 21, 32)
     assert "no HIP device" in _lib.last_error() or "gfx950" in _lib.last_error()
@@ -83,6 +87,12 @@ def test_argument_errors_precede_the_device_check():
     out = ctypes.c_uint64()
     cases = [
         ("null out", lambda: L.stormck_checksum(b"abc", 3, None)),
+        ("null p", lambda: L.stormck_checksum(None, 3, ctypes.byref(out))),
+        ("gpu null out", lambda: L.stormck_checksum_gpu(b"abc", 3, None)),
+        ("gpu over 256 MiB", lambda: L.stormck_checksum_gpu(1 << 20, (256 << 20) + 1, ctypes.byref(out))),
+        ("read-verify address overflow", lambda: L.stormck_read_verify_fd(
+            0, (ctypes.c_uint64 * 1)(1 << 60), (ctypes.c_uint32 * 1)(100), 1, 32768, (ctypes.c_uint8 * 64)(), 64,
+            (ctypes.c_uint64 * 1)(0), 0, ctypes.byref(out), ctypes.byref(out))),
         ("overlap", lambda: L.stormck_checksum_device(1 << 20, 16, None, 32, 2, 1 << 21, None)),
         ("null base", lambda: L.stormck_checksum_device(None, 32, None, 32, 2, 1 << 21, None)),
         ("gather null", lambda: L.stormck_checksum_gather_device(1 << 20, None, None, 32, 2, 1 << 21, None)),
@@ -146,3 +156,30 @@ def test_commit_planning_runs_then_fails_loudly_without_device():
     rc = _lib.lib.stormck_commit_device(1 << 20, bp.ctypes.data, len(bp), 5, ctypes.byref(la), cs.ctypes.data, None)
     assert rc == _lib.ENODEV
     assert np.array_equal(bp, before) and la.value == last
+
+
+def test_single_call_host_leg_matches_oracle_and_known_answers():
+    """stormck_xxh64 / stormck_checksum (the single-call leg, no device needed): the
+    public XXH64 answers, every fixture length on zero and iota data, and random buffers
+    of every length 0..300 at every start offset mod 8, against the C oracle."""
+    import numpy as np
+    from oracle import oracle as o
+    from storm_amd import _lib, blocks
+    from tests.conftest import hx, load_golden
+    kat = load_golden("kat.json")
+    for s_, v in kat["public"].items():
+        assert blocks.Checksum(s_.encode()) == hx(v)
+        assert _lib.lib.stormck_xxh64(s_.encode(), len(s_)) == hx(v)
+    for r in kat["rows"]:
+        n = r["len"]
+        assert blocks.Checksum(bytes(n)) == hx(r["zeros"]), n
+        assert blocks.Checksum(bytes(i & 0xFF for i in range(n))) == hx(r["iota"]), n
+    rng = np.random.default_rng(11)
+    buf = rng.integers(0, 256, size=400, dtype=np.uint8)
+    for n in range(0, 301):
+        for off in range(8):
+            sl = buf[off:off + n]
+            assert blocks.Checksum(sl) == o.xxh64(sl), (n, off)
+    big = rng.integers(0, 256, size=(300 << 20) + 13, dtype=np.uint8)  # past the 256 MiB device limit
+    assert blocks.Checksum(big) == o.xxh64(big)
+    assert _lib.lib.stormck_xxh64(None, 0) == 0xEF46DB3751D8E999

@@ -52,17 +52,28 @@ def test_kat_lengths_device(dev):
         assert [int(v) for v in _u64(out)] == [hx(r[pattern]) for r in rows]
 
 
-def test_public_answers_single_call(dev):
+@pytest.fixture(params=["host", "gpu"])
+def single(request, dev, monkeypatch):
+    """Runs a single-call test through both legs: blocks.Checksum (the host latency leg,
+    stormck_checksum) and the device single call (stormck_checksum_gpu,
+    k_xxh64_single). BlockChecksum / VerifyChecksum call the module's Checksum."""
+    from storm_amd import blocks
+    if request.param == "gpu":
+        monkeypatch.setattr(blocks, "Checksum", blocks.ChecksumGPU)
+    return request.param
+
+
+def test_public_answers_single_call(single):
     from storm_amd import blocks
     for s, v in load_golden("kat.json")["public"].items():
         assert blocks.Checksum(s.encode()) == hx(v)
 
 
 def test_single_call_latency_path_lengths(dev):
-    """stormck_checksum (one Go blocks.Checksum call): slices up to 64 KiB go through the
-    one-launch kernel that reads pinned host memory (every staging round count 1..16,
-    clamped last round), longer ones through the host pipeline. Unaligned Python views
-    exercise the host-side copy."""
+    """stormck_checksum_gpu (one blocks.Checksum call on the device): slices up to 64 KiB
+    go through the one-launch kernel that reads pinned host memory (every staging round
+    count 1..16, clamped last round), longer ones through the host pipeline. Unaligned
+    Python views exercise the host-side copy."""
     from oracle import oracle as o
     from storm_amd import blocks
     rng = np.random.default_rng(5)
@@ -72,7 +83,24 @@ def test_single_call_latency_path_lengths(dev):
     for L in lengths:
         for off in (0, 3):
             sl = data[off:off + L]  # numpy view: off = 3 hands the library an unaligned pointer
+            assert blocks.ChecksumGPU(sl) == o.xxh64(sl), (L, off)
             assert blocks.Checksum(sl) == o.xxh64(sl), (L, off)
+
+
+def test_single_call_length_limits(dev):
+    """The device single call takes up to the 256 MiB staging chunk (a batch of one
+    through the host pipeline) and refuses longer slices with EINVAL; the single-call
+    leg blocks.Checksum hashes any length (stormck.h)."""
+    from oracle import oracle as o
+    from storm_amd import _lib, blocks
+    rng = np.random.default_rng(6)
+    big = rng.integers(0, 256, size=(256 << 20) + 1, dtype=np.uint8)
+    want = o.xxh64(big[:256 << 20])
+    assert blocks.ChecksumGPU(big[:256 << 20]) == want
+    with pytest.raises(_lib.StormckError) as e:
+        blocks.ChecksumGPU(big)
+    assert e.value.code == _lib.EINVAL and "256 MiB" in str(e.value)
+    assert blocks.Checksum(big) == o.xxh64(big)
 
 
 # ---------------------------------------------------------------------------
@@ -236,6 +264,7 @@ def test_mixed_c5(dev):
 def test_empty_and_zero(dev):
     from storm_amd import blocks, engine
     assert blocks.Checksum(b"") == 0xEF46DB3751D8E999
+    assert blocks.ChecksumGPU(b"") == 0xEF46DB3751D8E999
     engine.checksum_device(0, 0, 0, 0, 0)  # n == 0 is a no-op
     buf = torch.zeros((4, 64), dtype=torch.uint8, device=dev)
     out = engine.checksum_tensor(buf, length=0)
@@ -371,7 +400,7 @@ def test_host_batch_paths(dev):
 # Go API mirror, with the reference's relational tests
 # ---------------------------------------------------------------------------
 
-def test_pointer_block_checksum_sequence(dev):
+def test_pointer_block_checksum_sequence(single):
     # /root/reference/blocks/pointer/block_test.go:11-35
     from storm_amd import blocks, layouts
     seq = [hx(v) for v in load_golden("layouts.json")["pointer_block_test_sequence"]]
@@ -391,7 +420,7 @@ def test_pointer_block_checksum_sequence(dev):
     assert len(set(got)) == len(got)  # every field change changes the checksum
 
 
-def test_zero_blocks_and_singularity(dev):
+def test_zero_blocks_and_singularity(single):
     from storm_amd import blocks, layouts
     g = load_golden("layouts.json")
     for tag in ("prod", "test"):
@@ -417,7 +446,7 @@ def test_zero_blocks_and_singularity(dev):
     assert blocks.VerifyChecksum(0, bytes(copy), cs) is None
 
 
-def test_verify_checksum_error_format(dev):
+def test_verify_checksum_error_format(single):
     # blocks/checksum.go:25-26: "checksum mismatch for block %d, computed: %#v, expected: %#v"
     from storm_amd import blocks
     err = blocks.VerifyChecksum(42, b"abc", 0)
@@ -426,7 +455,7 @@ def test_verify_checksum_error_format(dev):
     assert blocks.VerifyChecksum(42, b"abc", 0x44BC2CF5AD770999) is None
 
 
-def test_blob_block_change_changes_checksum(dev):
+def test_blob_block_change_changes_checksum(single):
     # blocks/blob/block_test.go:13-49
     from storm_amd import blocks, layouts
     g = load_golden("layouts.json")["blob_test_block"]
@@ -480,6 +509,35 @@ def test_pack_pointer_blocks_materialised(dev):
             assert bytes(host[j, :size]) == o.pack_pointer_block_py(ent, fanout)
 
 
+@pytest.mark.parametrize("m", [257 * 1200, 300 * 1200 + 1, 4000 * 1200 - 7, 320 * 1200])
+def test_pointer_level_ring_kernel(dev, m):
+    """Levels of more than 256 nodes at storm's fan-out take k_pointer_level_ring (one
+    wave per 16 nodes, premultiplied words staged in LDS). Shapes: full last wave (320
+    nodes), a last wave holding 1 node and 15 idle quads (257), a last node with one
+    child (300 + 1), and a ragged 4,000-node level; addresses and revision above 2^32.
+    Equal to the materialised pointer blocks hashed by the batch kernels on every node,
+    and to the oracle's packer + XXH64 on a sample."""
+    from oracle import oracle as o
+    from storm_amd import engine
+    fanout, base, rev = 1200, (1 << 40) + 5, (1 << 33) + 1
+    leaf = o.synth_leaf_checksums(m, 0x1234 + m)
+    d_leaf = _to_dev(leaf.view(np.int64), dev)
+    pm = (m + fanout - 1) // fanout
+    fused = torch.empty(pm, dtype=torch.int64, device=dev)
+    engine.pointer_level_device(d_leaf.data_ptr(), m, base, rev, 2, fanout, fused.data_ptr())
+    size = o.pointer_block_size(fanout)
+    stride = (size + 15) // 16 * 16
+    blk = torch.zeros((pm, stride), dtype=torch.uint8, device=dev)
+    engine.pack_pointer_blocks_device(d_leaf.data_ptr(), m, base, rev, 2, fanout, blk.data_ptr(), stride)
+    via_bytes = engine.checksum_tensor(blk, length=size)
+    torch.cuda.synchronize()
+    got = _u64(fused)
+    assert np.array_equal(got, _u64(via_bytes))
+    for jn in sorted({0, 1, 15, 16, pm // 2, pm - 2, pm - 1}):
+        ent = [(int(leaf[k]), base + k, rev, 2) for k in range(jn * fanout, min(m, (jn + 1) * fanout))]
+        assert int(got[jn]) == o.xxh64(o.pack_pointer_block_py(ent, fanout)), jn
+
+
 def test_combine_roots_device(dev):
     from storm_amd import engine
     g = load_golden("merkle.json")["combine"]
@@ -499,7 +557,7 @@ def test_one_hip_runtime_whatever_the_import_order(dev):
     code = ("from storm_amd import blocks\n"
             "import torch\n"
             "x = torch.ones(4, device='cuda:0')\n"
-            "assert blocks.Checksum(b'abc') == 0x44BC2CF5AD770999\n"
+            "assert blocks.ChecksumGPU(b'abc') == 0x44BC2CF5AD770999\n"
             "assert float(x.sum()) == 4.0\n"
             "print('ok')\n")
     from tests.conftest import ROOT
