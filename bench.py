@@ -586,7 +586,10 @@ def block_checksum_workload(a) -> int:
             tj = json.load(f)
         if tj.get("arena_blocks") == arena_n and tj.get("kernel") == KERNEL:
             traffic = tj.get("hbm_bytes_per_launch")
-            prof = tj.get("source")
+            # the committed rocprofv3 session this line's frac can be recomputed from
+            # (tools/collect_profile.py): its kernel-trace average and the frac it implies
+            prof = {k: tj.get(k) for k in ("source", "profile_calls", "profile_avg_launch_ms", "profile_frac",
+                                           "traffic_over_algorithmic")}
 
     # also report against a measured stream-read peak. Measured here, after
     # the timed region, on the same arena: the rate depends on where the arena lands in

@@ -162,8 +162,12 @@ int stormck_merkle_root_device(const uint64_t* d_leaf_cs, uint64_t n, uint64_t l
  * addresses[i] * block_size) is read with parallel pread() into
  * dst + i*dst_stride (e.g. the cache slots), then all n are verified on the GPU
  * against expected[i]. With STORMCK_READ_FULL_BLOCK each read covers block_size
- * bytes (what an O_DIRECT descriptor needs; dst/dst_stride must then satisfy the
- * descriptor's alignment) while lens[i] bytes are still what is hashed.
+ * bytes while lens[i] bytes are still what is hashed. A descriptor opened with
+ * O_DIRECT (no page cache) always reads full blocks; dst, dst_stride and block_size
+ * must then be 512-byte aligned (the device's own alignment may be stricter).
+ * Consecutive addresses whose slots are contiguous (dst_stride == block_size) are
+ * read with one pread of up to 1 MiB. With dst registered (stormck_host_register)
+ * the verify DMAs straight from the slots, with no staging copy.
  * *first_bad = first mismatching index (n if none), *n_bad = count; returns
  * STORMCK_EMISMATCH if any block fails, STORMCK_EINVAL on a short read. */
 #define STORMCK_READ_FULL_BLOCK 1u

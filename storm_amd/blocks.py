@@ -23,6 +23,7 @@ every length). ``ChecksumGPU`` is the same call through the devic
 from __future__ import annotations
 
 import ctypes
+import os
 from enum import IntEnum
 from typing import Optional, Sequence, Tuple
 
@@ -159,7 +160,8 @@ def ReadVerifyBatch(fd: int, addresses, lens, expected, dst, dst_stride: int, bl
     """Batched cold read + verify (cache.fetchBlock for many blocks: Store.ReadBlock,
     persistence/store.go:39-51, then VerifyChecksum): reads block i from file `fd` at
     addresses[i] * block_size into dst + i*dst_stride and verifies it on the GPU.
-    Returns (first_bad, n_bad); first_bad == n when every block verifies."""
+    Returns (first_bad, n_bad); first_bad == n when every block verifies. A descriptor
+    opened with O_DIRECT reads whole blocks into 512-byte aligned slots (stormck.h)."""
     ad = np.ascontiguousarray(np.asarray(addresses, dtype=np.uint64))
     la = np.ascontiguousarray(np.asarray(lens, dtype=np.uint32))
     ex = np.ascontiguousarray(np.asarray(expected, dtype=np.uint64))
@@ -169,6 +171,8 @@ def ReadVerifyBatch(fd: int, addresses, lens, expected, dst, dst_stride: int, bl
     n = ad.size
     if la.size != n or ex.size != n:
         raise ValueError("addresses, lens and expected need one entry per block")
+    import fcntl
+    full_block = full_block or bool(fcntl.fcntl(fd, fcntl.F_GETFL) & os.O_DIRECT)  # O_DIRECT reads whole blocks
     if n and d.size < (n - 1) * dst_stride + (block_size if full_block else int(la.max())):
         raise ValueError("dst too small")
     if n == 0:

@@ -16,8 +16,11 @@
 #include <thread>
 #include <vector>
 
+#include <fcntl.h>
 #include <pthread.h>
 #include <unistd.h>
+
+#include <cerrno>
 
 #include "../../include/stormck.h"
 #include "kernels.h"
@@ -899,8 +902,16 @@ int stormck_read_verify_fd(int fd, const uint64_t* addresses, const uint32_t* le
     *n_bad = 0;
     if (n == 0) return STORMCK_OK;
     if (fd < 0 || !addresses || !lens || !dst || !expected) return fail(STORMCK_EINVAL, "null argument");
-    const bool full = (flags & STORMCK_READ_FULL_BLOCK) != 0;
     if (block_size == 0) return fail(STORMCK_EINVAL, "block_size is 0");
+    // An O_DIRECT descriptor (pkg/filedev's device file opened to bypass the page cache,
+    // the reference's TODO at persistence/init.go:54 / cache/cache.go:82) only takes
+    // whole, aligned blocks: reads cover block_size bytes into 512-byte aligned slots.
+    const int fl = fcntl(fd, F_GETFL);
+    if (fl < 0) return fail(STORMCK_EINVAL, std::string("fcntl(F_GETFL): ") + std::strerror(errno));
+    const bool direct = (fl & O_DIRECT) != 0;
+    const bool full = direct || (flags & STORMCK_READ_FULL_BLOCK) != 0;
+    if (direct && ((reinterpret_cast<uintptr_t>(dst) | dst_stride | block_size) & 511))
+        return fail(STORMCK_EINVAL, "O_DIRECT descriptor: dst, dst_stride and block_size must be 512-byte aligned");
     const uint64_t max_addr = (static_cast<uint64_t>(INT64_MAX) - block_size) / block_size;
     for (uint64_t i = 0; i < n; ++i) {
         const uint64_t want = full ? block_size : lens[i];
@@ -912,31 +923,42 @@ int stormck_read_verify_fd(int fd, const uint64_t* addresses, const uint32_t* le
     int rc = device_check();
     if (rc) return rc;
     // Reads (Store.ReadBlock: Seek(address*BlockSize) + Read) run on a reader thread
-    // one super-chunk ahead of the GPU verify of the previous super-chunk.
-    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-    const unsigned nt = std::min(16u, hw);
+    // one super-chunk ahead of the GPU verify of the previous super-chunk. Runs of
+    // consecutive addresses whose slots are contiguous (full blocks, dst_stride ==
+    // block_size) are read with one pread of up to kRunBytes. An O_DIRECT descriptor
+    // reaches the device, whose rate needs queue depth: 32 reader threads instead of 16
+    // (STORMCK_READ_THREADS overrides).
+    constexpr uint64_t kRunBytes = 1ULL << 20;
+    const uint64_t max_run = full && dst_stride == block_size ? std::max<uint64_t>(1, kRunBytes / block_size) : 1;
+    unsigned nt = direct ? 32u : std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
+    if (const char* e = std::getenv("STORMCK_READ_THREADS")) nt = std::max(1, std::atoi(e));
     const uint64_t per_super = std::max<uint64_t>(1, (1ULL << 30) / std::max<uint64_t>(dst_stride, 1));
     const uint64_t nsuper = (n + per_super - 1) / per_super;
-    std::atomic<int> err{0};
+    std::atomic<int> err{0}, err_no{0};
     std::atomic<uint64_t> bad_index{n};
     std::atomic<uint64_t> ready{0};  // super-chunks fully read
     std::atomic<bool> stop{false};
     std::mutex mu;
     std::condition_variable cv;
     auto read_range = [&](uint64_t lo, uint64_t hi) {
-        for (uint64_t i = lo; i < hi && !err.load(std::memory_order_relaxed); ++i) {
+        for (uint64_t i = lo; i < hi && !err.load(std::memory_order_relaxed);) {
+            uint64_t k = i + 1;
+            while (k < hi && k - i < max_run && addresses[k] == addresses[k - 1] + 1) ++k;
             uint8_t* d = static_cast<uint8_t*>(dst) + i * dst_stride;
-            const uint64_t want = full ? block_size : lens[i];
+            const uint64_t want = full ? (k - i) * block_size : lens[i];
+            const uint64_t off = addresses[i] * block_size;
             uint64_t got = 0;
             while (got < want) {
-                const ssize_t r = pread(fd, d + got, want - got, static_cast<off_t>(addresses[i] * block_size + got));
+                const ssize_t r = pread(fd, d + got, want - got, static_cast<off_t>(off + got));
                 if (r <= 0) {
+                    if (r < 0) err_no.store(errno);
                     err.store(r < 0 ? 1 : 2);
-                    bad_index.store(i);
+                    bad_index.store(i + (full ? got / block_size : 0));
                     return;
                 }
                 got += static_cast<uint64_t>(r);
             }
+            i = k;
         }
     };
     std::thread reader([&] {
@@ -981,8 +1003,9 @@ int stormck_read_verify_fd(int fd, const uint64_t* addresses, const uint32_t* le
     stop.store(true);
     reader.join();
     if (err.load()) {
-        return fail(STORMCK_EINVAL, std::string(err.load() == 1 ? "pread failed" : "short read (block beyond end of device)") +
-                                        " at block index " + std::to_string(bad_index.load()));
+        const std::string what = err.load() == 1 ? std::string("pread failed (") + std::strerror(err_no.load()) + ")"
+                                                 : std::string("short read (block beyond end of device)");
+        return fail(STORMCK_EINVAL, what + " at block index " + std::to_string(bad_index.load()));
     }
     if (rc) return rc;
     if (*n_bad > 0) {

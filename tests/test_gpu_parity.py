@@ -648,6 +648,69 @@ def test_read_verify_fd_f2(dev, tmp_path):
         os.close(fd)
 
 
+def _odirect_dir(tmp_path):
+    """A directory whose filesystem takes O_DIRECT (tmpfs does not), or None."""
+    import os
+    for d in (str(tmp_path), os.getcwd(), os.path.expanduser("~")):
+        probe = os.path.join(d, f".odirect_{os.getpid()}")
+        try:
+            fd = os.open(probe, os.O_RDWR | os.O_CREAT | os.O_DIRECT, 0o600)
+        except OSError:
+            continue
+        os.close(fd)
+        os.unlink(probe)
+        return d
+    return None
+
+
+def test_read_verify_o_direct_into_registered_slots(dev, tmp_path):
+    """f3: the device image opened with O_DIRECT (no page cache, pkg/filedev with the
+    reference's O_DIRECT TODO, persistence/init.go:54), read into page-aligned,
+    registered slots (full blocks; the verify DMAs straight from them). Addresses mix
+    runs of consecutive blocks (one pread per run) and random ones; clean blocks verify,
+    a corrupted block on the device is found, misaligned slots are refused."""
+    import mmap
+    import os
+    from oracle import oracle as o
+    from storm_amd import _lib, blocks
+    d = _odirect_dir(tmp_path)
+    if d is None:
+        pytest.skip("no O_DIRECT-capable filesystem on this box")
+    rng = np.random.default_rng(17)
+    nblocks, bs = 4096, 32768
+    image = rng.integers(0, 256, size=(nblocks, bs), dtype=np.uint8)
+    path = os.path.join(d, f"odirect_dev_{os.getpid()}.img")
+    image.tofile(path)
+    n = 3000
+    runs = np.concatenate([np.arange(100, 164), np.arange(2000, 2040), np.arange(4000, 4096)])
+    addresses = np.concatenate([runs, rng.choice(nblocks, size=n - runs.size, replace=False)]).astype(np.uint64)
+    lens = rng.choice([72, 28808, 30000, 31808, 32768], size=n).astype(np.uint32)
+    expected = o.checksum_batch(image[addresses.astype(np.int64)], n, bs, lens=lens, threads=8)
+    mm = mmap.mmap(-1, n * bs)  # page-aligned slots
+    dst = np.frombuffer(mm, dtype=np.uint8).reshape(n, bs)
+    blocks.RegisterHostMemory(dst)
+    fd = os.open(path, os.O_RDWR | os.O_DIRECT)
+    try:
+        assert blocks.ReadVerifyBatch(fd, addresses, lens, expected, dst, bs) == (n, 0)
+        for i in (0, 63, 64, 200, 2999):
+            assert np.array_equal(dst[i], image[int(addresses[i])])  # whole blocks landed
+        # corrupt block 2010 on the device itself (an O_DIRECT write of one aligned block)
+        blk = mmap.mmap(-1, bs)
+        blk.write(image[2010].tobytes())
+        blk[5] ^= 0xFF
+        os.pwrite(fd, blk, 2010 * bs)
+        first = int(np.nonzero(addresses == 2010)[0][0])
+        assert blocks.ReadVerifyBatch(fd, addresses, lens, expected, dst, bs) == (first, 1)
+        misaligned = np.frombuffer(mm, dtype=np.uint8)[16:16 + (n - 1) * bs].reshape(n - 1, bs)
+        with pytest.raises(_lib.StormckError) as e:
+            blocks.ReadVerifyBatch(fd, addresses[:10], lens[:10], expected[:10], misaligned, bs)
+        assert e.value.code == _lib.EINVAL and "aligned" in str(e.value)
+    finally:
+        os.close(fd)
+        blocks.UnregisterHostMemory(dst)
+        os.unlink(path)
+
+
 def test_quad_paths_verify_and_gather_variants(dev):
     """Register-quad kernel in every shape: verify with per-block lengths (LENS+VERIFY),
     gather with offsets and a uniform length (OFFS only), verify through offsets is

@@ -1,0 +1,94 @@
+"""Collect one rocprofv3 evidence session (tools/profile.sh <tag>, run on the GPU box)
+into profiles/<tag>/ and write profiles/traffic.json for bench.py.
+
+From gpurun_out/prof_<tag>/:
+  trace/**/*kernel_stats.csv         -> kernel_stats.csv (kernel trace + stats of bench.py)
+  trace.log (its JSON line)          -> bench_under_rocprof.json (the bench line of THAT process)
+  fetch/**/*counter_collection.csv   -> pmc_fetch_size.csv   (separate --pmc FETCH_SIZE pass)
+  write/**/*counter_collection.csv   -> pmc_write_size.csv   (separate --pmc WRITE_SIZE pass)
+  calib/**/*counter_collection.csv   -> pmc_fetch_calibration_probe.csv
+
+traffic.json (per launch of the dominant kernel, one 4M-block arena pass):
+  hbm_bytes_per_launch = FETCH_SIZE x 1024 x correction + WRITE_SIZE x 1024, where the
+  gfx950 FETCH_SIZE correction is calibrated on a read-peak kernel of known byte count
+  (MI355X_MICROARCH.md, HBM / rocprofv3 section: FETCH_SIZE counts half of a wide
+  coalesced stream);
+  profile_avg_launch_ms = the kernel-trace average of that kernel in the same session,
+  and profile_frac = algorithmic bytes / that average / 8 TB/s, so the bench line's
+  roofline.frac can be recomputed from the committed profile.
+
+    python tools/collect_profile.py <tag> [arena_blocks]
+"""
+import csv
+import glob
+import json
+import os
+import shutil
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KERNEL = "k_xxh64_glds_skew<16, 2, false, 8, 8, true>"  # rocprofv3 name of the dominant kernel
+BLOCK = 32768
+PEAK = 8e12
+
+
+def one(pattern):
+    hits = sorted(glob.glob(pattern, recursive=True))
+    if not hits:
+        raise SystemExit(f"no file matches {pattern}")
+    return hits[0]
+
+
+def rows(path):
+    with open(path) as f:
+        return list(csv.DictReader(f))
+
+
+def main(tag, arena):
+    src = os.path.join(ROOT, "gpurun_out", f"prof_{tag}")
+    dst = os.path.join(ROOT, "profiles", tag)
+    os.makedirs(dst, exist_ok=True)
+    files = {
+        "kernel_stats.csv": one(os.path.join(src, "trace", "**", "*kernel_stats.csv")),
+        "pmc_fetch_size.csv": one(os.path.join(src, "fetch", "**", "*counter_collection.csv")),
+        "pmc_write_size.csv": one(os.path.join(src, "write", "**", "*counter_collection.csv")),
+        "pmc_fetch_calibration_probe.csv": one(os.path.join(src, "calib", "**", "*counter_collection.csv")),
+    }
+    for name, path in files.items():
+        shutil.copy(path, os.path.join(dst, name))
+    bench_line = None
+    with open(os.path.join(src, "trace.log")) as f:
+        for line in f:
+            if line.startswith("{"):
+                bench_line = json.loads(line)
+    with open(os.path.join(dst, "bench_under_rocprof.json"), "w") as f:
+        json.dump(bench_line, f, indent=1)
+
+    fetch = [r for r in rows(files["pmc_fetch_size.csv"]) if KERNEL in r["Kernel_Name"]]
+    write = [r for r in rows(files["pmc_write_size.csv"]) if KERNEL in r["Kernel_Name"]]
+    calib = [r for r in rows(files["pmc_fetch_calibration_probe.csv"]) if "k_readpeak" in r["Kernel_Name"]]
+    probe_bytes = 8 << 30  # tools/probe 8: every read-peak launch reads 8 GiB exactly once
+    corr = probe_bytes / (sum(float(r["Counter_Value"]) for r in calib) / len(calib) * 1024)
+    fk = sum(float(r["Counter_Value"]) for r in fetch) / len(fetch)
+    wk = sum(float(r["Counter_Value"]) for r in write) / len(write)
+    hbm = fk * 1024 * corr + wk * 1024
+    alg = arena * (BLOCK + 8)
+    stats = [r for r in rows(files["kernel_stats.csv"]) if KERNEL in r["Name"]]
+    avg_ns = float(stats[0]["AverageNs"])
+    out = {"kernel": "k_xxh64_glds_skew<16,nt,8w,4KiB>", "arena_blocks": arena, "fetch_size_kb": fk,
+           "write_size_kb": wk, "fetch_correction": round(corr, 4), "hbm_bytes_per_launch": int(hbm),
+           "algorithmic_bytes_per_launch": alg, "traffic_over_algorithmic": round(hbm / alg, 4),
+           "profile_calls": int(stats[0]["Calls"]), "profile_avg_launch_ms": round(avg_ns * 1e-6, 4),
+           "profile_min_launch_ms": round(float(stats[0]["MinNs"]) * 1e-6, 4),
+           "profile_max_launch_ms": round(float(stats[0]["MaxNs"]) * 1e-6, 4),
+           "profile_frac": round(alg / (avg_ns * 1e-9) / PEAK, 4),
+           "bench_under_rocprof": {"frac": bench_line["roofline"]["frac"] if bench_line else None,
+                                   "avg_launch_ms": bench_line["roofline"]["avg_launch_ms"] if bench_line else None},
+           "source": os.path.relpath(dst, ROOT)}
+    with open(os.path.join(ROOT, "profiles", "traffic.json"), "w") as f:
+        json.dump(out, f, indent=1)
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 4 << 20)

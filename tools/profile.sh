@@ -1,6 +1,6 @@
 #!/bin/bash
 # rocprofv3 evidence for the dominant kernel (run on the GPU box via gpurun).
-#   1. kernel trace + stats of the bench command (average k_xxh64_quad duration)
+#   1. kernel trace + stats of the bench command (average duration of the dominant kernel)
 #   2. separate PMC passes: FETCH_SIZE, WRITE_SIZE (one bench step, one arena pass)
 #   3. FETCH_SIZE calibration on the probe (read-peak kernel with a known byte count)
 # Usage: tools/profile.sh <tag>
@@ -20,3 +20,4 @@ timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write"
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/calib" -o calib -- \
     "$R/tools/probe" 8 1 > "$OUT/calib.log" 2>&1 || { echo "calib failed rc=$?"; exit 1; }
 echo "profile done"
+# then, in the build container: python tools/collect_profile.py <tag>
