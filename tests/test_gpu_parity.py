@@ -683,7 +683,8 @@ def test_read_verify_o_direct_into_registered_slots(dev, tmp_path):
     image.tofile(path)
     n = 3000
     runs = np.concatenate([np.arange(100, 164), np.arange(2000, 2040), np.arange(4000, 4096)])
-    addresses = np.concatenate([runs, rng.choice(nblocks, size=n - runs.size, replace=False)]).astype(np.uint64)
+    rest = np.setdiff1d(np.arange(nblocks), runs)
+    addresses = np.concatenate([runs, rng.choice(rest, size=n - runs.size, replace=False)]).astype(np.uint64)
     lens = rng.choice([72, 28808, 30000, 31808, 32768], size=n).astype(np.uint32)
     expected = o.checksum_batch(image[addresses.astype(np.int64)], n, bs, lens=lens, threads=8)
     mm = mmap.mmap(-1, n * bs)  # page-aligned slots

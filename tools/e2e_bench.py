@@ -109,6 +109,46 @@ def main():
             res["read_verify_note"] = "parallel pread (16 threads) from page cache on a reader thread, 1 GiB ahead of the pipelined H2D + verify"
         finally:
             os.close(fd)
+    # f3 cold read from storage: the same image opened with O_DIRECT (no page cache),
+    # read into page-aligned registered slots (full blocks, no staging copy), random
+    # block order and in address order (runs of consecutive blocks: one pread per MiB)
+    import mmap
+    img = os.path.join(os.environ.get("E2E_IMAGE_DIR", os.getcwd()), f"e2e_odirect_{os.getpid()}.img")
+    host.tofile(img)
+    mm = mmap.mmap(-1, n * BLOCK)
+    slots_d = np.frombuffer(mm, dtype=np.uint8).reshape(n, BLOCK)
+    blocks.RegisterHostMemory(slots_d)
+    try:
+        fd = os.open(img, os.O_RDONLY | os.O_DIRECT)
+        try:
+            lens = np.full(n, BLOCK, dtype=np.uint32)
+            for name, addrs in (("random", np.random.default_rng(2).permutation(n).astype(np.uint64)),
+                                ("sequential", np.arange(n, dtype=np.uint64))):
+                exp = want[addrs.astype(np.int64)]
+                blocks.ReadVerifyBatch(fd, addrs[:256], lens[:256], exp[:256], slots_d, BLOCK)  # warm
+                t, r = timed(lambda: blocks.ReadVerifyBatch(fd, addrs, lens, exp, slots_d, BLOCK))
+                assert r == (n, 0), r
+                res[f"read_verify_odirect_{name}_gib_s"] = round(n * BLOCK / t / 2**30, 2)
+            # the storage alone: the same O_DIRECT reads with nothing verified (32 threads)
+            import concurrent.futures as cf
+            order = np.random.default_rng(3).permutation(n)
+
+            def raw_read(part):
+                for i in part:
+                    os.preadv(fd, [memoryview(mm)[int(i) * BLOCK:(int(i) + 1) * BLOCK]], int(order[i]) * BLOCK)
+
+            parts = np.array_split(np.arange(n), 32)
+            t0 = time.perf_counter()
+            with cf.ThreadPoolExecutor(32) as ex:
+                list(ex.map(raw_read, parts))
+            res["raw_odirect_random_read_gib_s"] = round(n * BLOCK / (time.perf_counter() - t0) / 2**30, 2)
+            res["odirect_note"] = ("image file on " + os.path.dirname(img) + "; see profiles/*fs_probe.txt for the "
+                                   "filesystem (overlay); O_DIRECT bypasses the page cache")
+        finally:
+            os.close(fd)
+    finally:
+        blocks.UnregisterHostMemory(slots_d)
+        os.unlink(img)
     # f1 commit on a registered HOST arena (storm's cache.data in place, kernels over
     # PCIe via stormck_host_device_pointer), and the zero-copy device-entry hash rate
     from storm_amd import commit as sc
