@@ -1,0 +1,270 @@
+// Host-side sanitizer driver for libstormck (ASan + UBSan, or TSan).
+//
+// Built by tests/sanitize/build.sh against a copy of libstormck whose HOST code is
+// instrumented (hipcc -Xarch_host -fsanitize=...; device code is untouched, GPU
+// sanitizers are not used). It drives the library's host orchestration through the
+// C ABI:
+//   * the single-call leg stormck_xxh64 / stormck_checksum on every length 0..4100 at
+//     every start offset mod 8, against the oracle (out-of-bounds reads show up here);
+//   * argument validation of every entry point (EINVAL before any device work);
+//   * f1 commit planning: validation, the threaded height walk-up (ForkJoin pool),
+//     cycle / range / alignment errors, on shuffled forests up to 300K records;
+//   * with a gfx950 device (GPU box): the same commits run to completion on a device
+//     arena and are compared with the oracle's serial commit; the host pipeline
+//     (pageable and registered sources, parallel staging copies, both stages), the
+//     batched verify and the file read-verify reader threads.
+// Exit status 0 = every check passed and the sanitizer reported nothing (sanitizer
+// reports abort the process: halt_on_error / -fno-sanitize-recover).
+#include <fcntl.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <numeric>
+#include <random>
+#include <string>
+#include <vector>
+
+#include <hip/hip_runtime_api.h>
+
+#include "stormck.h"
+
+extern "C" {
+uint64_t oracle_xxh64(const void* data, size_t n);
+int oracle_commit(uint8_t* arena, stormck_dirty_block* blocks, size_t n, uint64_t revision, uint64_t* last_allocated,
+                  uint64_t* out_cs);
+}
+
+static int g_fail = 0;
+#define CHECK(cond)                                                                                  \
+    do {                                                                                             \
+        if (!(cond)) {                                                                               \
+            std::fprintf(stderr, "FAIL %s:%d: %s (%s)\n", __FILE__, __LINE__, #cond, stormck_last_error()); \
+            ++g_fail;                                                                                \
+        }                                                                                            \
+    } while (0)
+
+static void single_calls() {
+    std::mt19937_64 rng(7);
+    std::vector<uint8_t> buf(4100 + 16);
+    for (auto& c : buf) c = static_cast<uint8_t>(rng());
+    for (size_t n = 0; n <= 4100; ++n) {
+        for (size_t off = 0; off < 8; ++off) {
+            // an exact-size heap copy, so a read past the end is a heap overflow
+            std::vector<uint8_t> exact(buf.begin() + off, buf.begin() + off + n);
+            const uint64_t want = oracle_xxh64(n ? exact.data() : buf.data(), n);
+            CHECK(stormck_xxh64(exact.data(), n) == want);
+            uint64_t out = 0;
+            CHECK(stormck_checksum(n ? exact.data() : nullptr, n, &out) == STORMCK_OK && out == want);
+        }
+    }
+    CHECK(stormck_xxh64(nullptr, 0) == 0xEF46DB3751D8E999ULL);
+}
+
+static void argument_errors() {
+    uint64_t out = 0, fb = 0, nb = 0;
+    uint8_t small[64] = {};
+    CHECK(stormck_checksum("abc", 3, nullptr) == STORMCK_EINVAL);
+    CHECK(stormck_checksum(nullptr, 3, &out) == STORMCK_EINVAL);
+    CHECK(stormck_checksum_gpu("abc", 3, nullptr) == STORMCK_EINVAL);
+    CHECK(stormck_checksum_gpu(small, (256ULL << 20) + 1, &out) == STORMCK_EINVAL);
+    CHECK(stormck_checksum_device(reinterpret_cast<void*>(1 << 20), 16, nullptr, 32, 2, &out, nullptr) == STORMCK_EINVAL);
+    CHECK(stormck_checksum_device(nullptr, 32, nullptr, 32, 2, &out, nullptr) == STORMCK_EINVAL);
+    CHECK(stormck_checksum_gather_device(small, nullptr, nullptr, 32, 2, &out, nullptr) == STORMCK_EINVAL);
+    CHECK(stormck_verify_device(small, 32, nullptr, 32, 2, &out, nullptr, nullptr) == STORMCK_EINVAL);
+    CHECK(stormck_pointer_level_device(&out, 5, 0, 1, 2, 0, &out, nullptr) == STORMCK_EINVAL);
+    CHECK(stormck_pointer_node_device(reinterpret_cast<stormck_pointer*>(small), small, 11, 10, &out, nullptr) ==
+          STORMCK_EINVAL);
+    CHECK(stormck_pack_pointer_blocks_device(&out, 5, 0, 1, 2, 10, small, 200, nullptr) == STORMCK_EINVAL);
+    CHECK(stormck_merkle_root_device(&out, 5000, 0, 5000, 1, 10, small, 8, reinterpret_cast<stormck_pointer*>(small),
+                                     small, nullptr) == STORMCK_EINVAL);
+    CHECK(stormck_fill_synthetic_device(small, 24, 4, 0, 1, nullptr) == STORMCK_EINVAL);
+    CHECK(stormck_host_register(nullptr, 0) == STORMCK_EINVAL);
+    CHECK(stormck_host_device_pointer(nullptr, nullptr) == STORMCK_EINVAL);
+    CHECK(stormck_key_tags_device(nullptr, 48, nullptr, nullptr, 48, 10, &out, nullptr) == STORMCK_EINVAL);
+    CHECK(stormck_checksum_host(nullptr, 32, nullptr, 32, 4, &out) == STORMCK_EINVAL);
+    const uint64_t addr_big[1] = {1ULL << 60}, addr0[1] = {0};
+    const uint32_t len100[1] = {100};
+    const uint64_t exp0[1] = {0};
+    const int devnull = open("/dev/null", O_RDONLY);
+    CHECK(stormck_read_verify_fd(devnull, addr_big, len100, 1, 32768, small, 64, exp0, 0, &fb, &nb) == STORMCK_EINVAL);
+    CHECK(stormck_read_verify_fd(devnull, addr0, len100, 1, 32768, small, 64, exp0, STORMCK_READ_FULL_BLOCK, &fb,
+                                 &nb) == STORMCK_EINVAL);
+    CHECK(stormck_read_verify_fd(devnull, addr0, len100, 1, 0, small, 64, exp0, 0, &fb, &nb) == STORMCK_EINVAL);
+    close(devnull);
+}
+
+// storm's dirty forest (storm_amd.commit.pointer_forest): leaves in slots 1..n, pointer
+// blocks level by level after them, the top block hanging off the singularity (slot 0).
+struct Forest {
+    std::vector<stormck_dirty_block> b;
+    uint64_t arena_bytes = 0, last = 0;
+};
+
+static Forest make_forest(uint64_t n_leaves, uint32_t fanout, uint64_t slot, uint64_t revision, std::mt19937_64& rng,
+                          bool shuffle) {
+    Forest f;
+    const uint32_t pbs = (fanout * 25u + 7u) & ~7u;
+    std::vector<uint64_t> levels;
+    for (uint64_t m = n_leaves; m > 1;) levels.push_back(m = (m + fanout - 1) / fanout);
+    const uint64_t total = n_leaves + std::accumulate(levels.begin(), levels.end(), uint64_t{0});
+    f.b.resize(total);
+    for (uint64_t i = 0; i < total; ++i) {
+        auto& r = f.b[i];
+        std::memset(&r, 0, sizeof r);
+        r.data_offset = (i + 1) * slot;
+        r.length = i < n_leaves ? static_cast<uint32_t>(std::min<uint64_t>(slot, 72 + rng() % slot)) : pbs;
+        r.type = i < n_leaves ? STORMCK_LEAF_BLOCK : STORMCK_POINTER_BLOCK;
+        r.address = i + 1;
+        r.birth_revision = rng() % 3 == 0 ? revision : revision + 1;  // a third relocate
+    }
+    uint64_t start = 0, count = n_leaves;
+    for (uint64_t lv : levels) {
+        const uint64_t ps = start + count;
+        for (uint64_t c = 0; c < count; ++c) {
+            const uint64_t p = ps + c / fanout, k = c % fanout;
+            f.b[start + c].parent = static_cast<int64_t>(p);
+            f.b[start + c].origin_pointer = f.b[p].data_offset + 24 * k;
+            f.b[start + c].origin_type = f.b[p].data_offset + 24ULL * fanout + k;
+        }
+        start = ps;
+        count = lv;
+    }
+    f.b[start].parent = STORMCK_NO_PARENT;
+    f.b[start].origin_pointer = 32;  // singularity SpacePointer / SpaceBlockType
+    f.b[start].origin_type = 56;
+    f.last = total;
+    f.arena_bytes = (total + 1) * slot;
+    if (shuffle) {  // parents before children in the caller's array
+        std::vector<uint64_t> perm(total), inv(total);
+        std::iota(perm.begin(), perm.end(), 0);
+        std::shuffle(perm.begin(), perm.end(), rng);
+        for (uint64_t i = 0; i < total; ++i) inv[perm[i]] = i;
+        std::vector<stormck_dirty_block> nb(total);
+        for (uint64_t i = 0; i < total; ++i) {
+            nb[i] = f.b[perm[i]];
+            if (nb[i].parent >= 0) nb[i].parent = static_cast<int64_t>(inv[nb[i].parent]);
+        }
+        f.b.swap(nb);
+    }
+    return f;
+}
+
+static bool has_device() {
+    int c = 0;
+    return stormck_device_count(&c) == STORMCK_OK && c > 0;
+}
+
+static void commit_planning(bool device) {
+    std::mt19937_64 rng(11);
+    const uint64_t sizes[] = {1, 2, 137, 5000, 70000, 300000};
+    for (uint64_t nl : sizes) {
+        for (bool shuffle : {false, true}) {
+            const uint32_t fanout = nl > 10000 ? 1200 : 10;
+            const uint64_t slot = nl > 10000 ? 32768 : 1024;
+            Forest f = make_forest(nl, fanout, slot, 5, rng, shuffle);
+            const uint64_t n = f.b.size();
+            std::vector<uint64_t> cs(n, 0);
+            uint64_t last = f.last;
+            if (!device) {
+                const auto before = f.b;
+                const int rc = stormck_commit_device(reinterpret_cast<void*>(1 << 20), f.b.data(), n, 5, &last,
+                                                     cs.data(), nullptr);
+                CHECK(rc == STORMCK_ENODEV);
+                CHECK(last == f.last && std::memcmp(before.data(), f.b.data(), n * sizeof(stormck_dirty_block)) == 0);
+                continue;
+            }
+            if (f.arena_bytes > (6ULL << 30)) continue;  // keep the host copy small
+            std::vector<uint8_t> host(f.arena_bytes, 0);
+            for (uint64_t i = 0; i < n; ++i)
+                if (f.b[i].type == STORMCK_LEAF_BLOCK)
+                    for (uint32_t k = 0; k < f.b[i].length; k += 8) host[f.b[i].data_offset + k] = static_cast<uint8_t>(rng());
+            void* d_arena = nullptr;
+            CHECK(hipMalloc(&d_arena, f.arena_bytes) == hipSuccess);
+            CHECK(hipMemcpy(d_arena, host.data(), f.arena_bytes, hipMemcpyHostToDevice) == hipSuccess);
+            auto ref = f.b;
+            uint64_t ref_last = f.last;
+            std::vector<uint64_t> ref_cs(n, 0);
+            CHECK(oracle_commit(host.data(), ref.data(), n, 5, &ref_last, ref_cs.data()) == 0);
+            CHECK(stormck_commit_device(d_arena, f.b.data(), n, 5, &last, cs.data(), nullptr) == STORMCK_OK);
+            CHECK(last == ref_last && cs == ref_cs);
+            CHECK(std::memcmp(ref.data(), f.b.data(), n * sizeof(stormck_dirty_block)) == 0);
+            std::vector<uint8_t> back(f.arena_bytes);
+            CHECK(hipMemcpy(back.data(), d_arena, f.arena_bytes, hipMemcpyDeviceToHost) == hipSuccess);
+            CHECK(back == host);
+            CHECK(hipFree(d_arena) == hipSuccess);
+        }
+    }
+    // planning errors, with or without a device: parent range, origin alignment, cycle
+    Forest f = make_forest(25, 10, 1024, 1, rng, false);
+    std::vector<uint64_t> cs(f.b.size());
+    uint64_t last = f.last;
+    auto bad = f.b;
+    bad[3].parent = 1000000;
+    CHECK(stormck_commit_device(reinterpret_cast<void*>(1 << 20), bad.data(), bad.size(), 1, &last, cs.data(), nullptr) ==
+          STORMCK_EINVAL);
+    bad = f.b;
+    bad[3].origin_pointer += 4;
+    CHECK(stormck_commit_device(reinterpret_cast<void*>(1 << 20), bad.data(), bad.size(), 1, &last, cs.data(), nullptr) ==
+          STORMCK_EINVAL);
+    bad = f.b;
+    bad[bad.size() - 1].parent = 0;  // root -> leaf 0 -> ... -> root
+    CHECK(stormck_commit_device(reinterpret_cast<void*>(1 << 20), bad.data(), bad.size(), 1, &last, cs.data(), nullptr) ==
+          STORMCK_EINVAL);
+}
+
+static void host_pipeline_paths() {
+    std::mt19937_64 rng(3);
+    const uint64_t n = 12000, stride = 32768;  // 375 MiB: two 256 MiB pipeline chunks
+    std::vector<uint8_t> buf(n * stride);
+    for (size_t i = 0; i < buf.size(); i += 8) buf[i] = static_cast<uint8_t>(rng());
+    std::vector<uint32_t> lens(n);
+    for (auto& l : lens) l = static_cast<uint32_t>(rng() % (stride + 1));
+    std::vector<uint64_t> want(n), got(n);
+    for (uint64_t i = 0; i < n; ++i) want[i] = oracle_xxh64(buf.data() + i * stride, lens[i]);
+    CHECK(stormck_checksum_host(buf.data(), stride, lens.data(), 0, n, got.data()) == STORMCK_OK && got == want);
+    uint64_t fb = 0, nb = 0;
+    CHECK(stormck_verify_host(buf.data(), stride, lens.data(), 0, n, want.data(), &fb, &nb) == STORMCK_OK && nb == 0);
+    auto bad = want;
+    bad[7777] ^= 1;
+    CHECK(stormck_verify_host(buf.data(), stride, lens.data(), 0, n, bad.data(), &fb, &nb) == STORMCK_EMISMATCH &&
+          fb == 7777 && nb == 1);
+    CHECK(stormck_host_register(buf.data(), buf.size()) == STORMCK_OK);
+    std::fill(got.begin(), got.end(), 0);
+    CHECK(stormck_checksum_host(buf.data(), stride, lens.data(), 0, n, got.data()) == STORMCK_OK && got == want);
+    CHECK(stormck_host_unregister(buf.data()) == STORMCK_OK);
+    uint64_t one = 0;
+    CHECK(stormck_checksum_gpu(buf.data() + 3, 70000, &one) == STORMCK_OK && one == oracle_xxh64(buf.data() + 3, 70000));
+    // file read-verify: reader threads, pipelined verify
+    char path[] = "/tmp/stormck_sanitize_XXXXXX";
+    const int fd = mkstemp(path);
+    CHECK(fd >= 0);
+    CHECK(write(fd, buf.data(), 4096 * stride) == static_cast<ssize_t>(4096 * stride));
+    std::vector<uint64_t> addrs(3000), exp(3000);
+    std::vector<uint32_t> l2(3000);
+    for (uint64_t i = 0; i < 3000; ++i) {
+        addrs[i] = rng() % 4096;
+        l2[i] = lens[addrs[i]];
+        exp[i] = want[addrs[i]];
+    }
+    std::vector<uint8_t> slots(3000 * stride);
+    CHECK(stormck_read_verify_fd(fd, addrs.data(), l2.data(), 3000, stride, slots.data(), stride, exp.data(), 0, &fb,
+                                 &nb) == STORMCK_OK && nb == 0);
+    close(fd);
+    unlink(path);
+}
+
+int main() {
+    single_calls();
+    argument_errors();
+    const bool device = has_device();
+    std::printf("device: %s\n", device ? "yes" : "no (planning up to the device check)");
+    if (device) CHECK(stormck_init(0) == STORMCK_OK);
+    commit_planning(device);
+    if (device) host_pipeline_paths();
+    stormck_shutdown();
+    std::printf("%s: %d failure(s)\n", g_fail ? "FAILED" : "ok", g_fail);
+    return g_fail ? 1 : 0;
+}
