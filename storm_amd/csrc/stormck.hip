@@ -1360,7 +1360,7 @@ int stormck_commit_device(void* d_arena, stormck_dirty_block* blocks, uint64_t n
         // level_start[h] = commit position of height h's first block (h >= 1)
         std::vector<uint64_t> level_start(static_cast<size_t>(max_h) + 2, 0);
         for (const Part& P : part)
-            for (size_t l = 1; l < P.hist.size(); ++l) level_start[l + 1] += P.hist[l];
+            for (size_t l = 1; l < P.hist.size() && l <= max_h; ++l) level_start[l + 1] += P.hist[l];
         level_start[1] = n0;
         for (uint32_t l = 1; l <= max_h; ++l) level_start[l + 1] += level_start[l];
         if (!sorted || !upper.empty()) {

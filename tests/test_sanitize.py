@@ -16,8 +16,10 @@ SOURCES = [os.path.join(ROOT, "storm_amd", "csrc", f) for f in ("stormck.hip", "
 SOURCES += [os.path.join(SAN, "host_paths.cpp"), os.path.join(SAN, "build.sh"), os.path.join(ROOT, "include", "stormck.h"),
             os.path.join(ROOT, "oracle", "xxh64_oracle.c")]
 ENV = {"asan": {"ASAN_OPTIONS": "detect_leaks=1:halt_on_error=1:abort_on_error=0",
+                "LSAN_OPTIONS": "suppressions=" + os.path.join(SAN, "lsan.supp"),
                 "UBSAN_OPTIONS": "halt_on_error=1:print_stacktrace=1"},
-       "tsan": {"TSAN_OPTIONS": "halt_on_error=1:second_deadlock_stack=1"}}
+       "tsan": {"TSAN_OPTIONS": "halt_on_error=1:second_deadlock_stack=1:suppressions="
+                                + os.path.join(SAN, "tsan.supp")}}
 
 
 def built(kind):
