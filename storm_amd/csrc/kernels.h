@@ -958,43 +958,49 @@ __global__ __launch_bounds__(256) void k_pointer_level(const uint64_t* __restric
 // order. The type bytes (37 stripes + the 16-byte tail at F = 1200) are the constant
 // type byte for full nodes; only the level's last node can be partial, and the one
 // wave that holds it takes the masked variant (FULL = false) of the same code.
-constexpr uint32_t kRingTileStripes = 15;  // stripes of one node per tile (odd: conflict-free reads)
-constexpr uint32_t kRingTileSlots = 20;    // child slots per tile (60 words)
+// A tile is TS stripes of every node = TS·4/3 child slots. A node's row in LDS is an
+// odd number of stripes (TS, or TS+1 for even TS), so the 8 quads of a 32-lane
+// ds_read_b64 group hit 8 distinct 32-byte bank groups.
+template <uint32_t TS>
+struct RingShape {
+    static_assert(TS % 3 == 0, "whole child slots per tile");
+    static constexpr uint32_t SL = TS * 4 / 3;        // child slots per tile
+    static constexpr uint32_t RS = (TS | 1u) * 4;     // words per node row in LDS
+};
 
-template <uint32_t F, int D, bool FULL>
-__device__ __forceinline__ void pointer_level_ring_body(const uint64_t* __restrict__ cs, uint64_t m, uint64_t pm,
-                                                        uint64_t node0, uint64_t addr_base, uint64_t rev, uint8_t type,
-                                                        uint64_t* __restrict__ parent_cs,
-                                                        uint64_t (*ring)[16][kRingTileStripes * 4]) {
-    constexpr uint32_t TS = kRingTileStripes, SL = kRingTileSlots, NT = F / SL, IT = 16 * SL / 64;
-    constexpr uint32_t kSize = (F * 25u + 7u) & ~7u, kWords = kSize / 8, kNst = kSize / 32;
-    constexpr uint32_t kPtrStripes = 3 * F / 4;
-    static_assert(F % SL == 0 && NT % D == 0 && IT * 64 == 16 * SL, "tile shape");
-    const uint32_t lane = threadIdx.x, q = lane >> 2, j = lane & 3;
-    const uint64_t rep = 0x0101010101010101ULL * type;
-    const uint64_t rev_pm = rev * kP2, step_pm = static_cast<uint64_t>(SL) * kP2;
-
-    // producer items: item r of this lane is slot pu[r] of node pq[r] in every tile
+// The producer side of one wave's 16 nodes: lane `lane` owns IT (node, slot) items of
+// every tile, loads their child checksums and writes the premultiplied words.
+template <uint32_t F, uint32_t TS_, bool FULL, uint32_t NODES = 16>
+struct RingProducer {
+    static constexpr uint32_t TS = TS_, SL = RingShape<TS_>::SL, RS = RingShape<TS_>::RS, NT = F / SL,
+                              IT = NODES * SL / 64;
+    static_assert(F % SL == 0 && IT * 64 == NODES * SL, "tile shape");
     uint32_t pq[IT], pu[IT], cnt_i[IT];
     const uint64_t* gp[IT];
     uint64_t addr_pm[IT];
+    uint64_t rev_pm, step_pm;
+
+    __device__ __forceinline__ RingProducer(const uint64_t* __restrict__ cs, uint64_t m, uint64_t pm, uint64_t node0,
+                                            uint64_t addr_base, uint64_t rev, uint32_t lane) {
+        rev_pm = rev * kP2;
+        step_pm = static_cast<uint64_t>(SL) * kP2;
 #pragma unroll
-    for (uint32_t r = 0; r < IT; ++r) {
-        const uint32_t item = lane + 64 * r;
-        pq[r] = item / SL;
-        pu[r] = item % SL;
-        uint64_t node = node0 + pq[r];
-        if (!FULL) {
-            if (node >= pm) node = pm - 1;  // idle quads of the last wave: hash a copy, store nothing
-            const uint64_t left = m - node * F;
-            cnt_i[r] = static_cast<uint32_t>(left < F ? left : F);
+        for (uint32_t r = 0; r < IT; ++r) {
+            const uint32_t item = lane + 64 * r;
+            pq[r] = item / SL;
+            pu[r] = item % SL;
+            uint64_t node = node0 + pq[r];
+            if (!FULL) {
+                if (node >= pm) node = pm - 1;  // idle quads of the last wave: hash a copy, store nothing
+                const uint64_t left = m - node * F;
+                cnt_i[r] = static_cast<uint32_t>(left < F ? left : F);
+            }
+            const uint64_t g = node * F + pu[r];
+            gp[r] = cs + g;
+            addr_pm[r] = (addr_base + g) * kP2;
         }
-        const uint64_t g = node * F + pu[r];
-        gp[r] = cs + g;
-        addr_pm[r] = (addr_base + g) * kP2;
     }
-    uint64_t raw[D][IT];
-    auto load_tile = [&](uint32_t t, uint64_t* dst) {
+    __device__ __forceinline__ void load(uint32_t t, uint64_t* dst) const {
 #pragma unroll
         for (uint32_t r = 0; r < IT; ++r) {
             if (FULL) {
@@ -1004,12 +1010,11 @@ __device__ __forceinline__ void pointer_level_ring_body(const uint64_t* __restri
                 dst[r] = slot < cnt_i[r] ? gp[r][t * SL] : 0;
             }
         }
-    };
-    auto produce = [&](uint32_t t, const uint64_t* src, int slot) {
-        uint64_t* row_base = &ring[slot][0][0];
+    }
+    __device__ __forceinline__ void produce(uint32_t t, const uint64_t* src, uint64_t (*tile)[RS]) const {
 #pragma unroll
         for (uint32_t r = 0; r < IT; ++r) {
-            uint64_t* w = row_base + pq[r] * (TS * 4) + 3 * pu[r];
+            uint64_t* w = &tile[pq[r]][3 * pu[r]];
             const uint64_t a = addr_pm[r] + t * step_pm;
             if (FULL) {
                 w[0] = src[r] * kP2;
@@ -1022,36 +1027,17 @@ __device__ __forceinline__ void pointer_level_ring_body(const uint64_t* __restri
                 w[2] = valid ? rev_pm : 0;
             }
         }
-    };
-
-    uint64_t acc = acc_seed(j);
-#pragma unroll
-    for (int d = 0; d < D; ++d) load_tile(d, raw[d]);
-    produce(0, raw[0], 0);
-    load_tile(D, raw[0]);
-    // Tile t: produce tile t+1 into ring slot (t+1)&1 and refill its registers with
-    // tile t+1+D, then walk the 15 chain rounds of tile t (slot t&1). D is even and t0
-    // a multiple of D, so the slots are compile-time constants. (Merging the three
-    // into one basic block so the scheduler interleaves them measured 6 % slower.)
-    static_assert(D % 2 == 0, "static ring slots");
-    for (uint32_t t0 = 0; t0 < NT; t0 += D) {
-#pragma unroll
-        for (int d = 0; d < D; ++d) {
-            const uint32_t t = t0 + d;
-            const int nb = (d + 1) % D;
-            if (t + 1 < NT) {
-                produce(t + 1, raw[nb], (d + 1) & 1);
-                if (t + 1 + D < NT) load_tile(t + 1 + D, raw[nb]);
-            }
-            __builtin_amdgcn_wave_barrier();
-            const uint64_t* row = &ring[d & 1][q][j];
-#pragma unroll
-            for (uint32_t s = 0; s < TS; ++s) acc = round_pm(acc, row[4 * s]);
-            __builtin_amdgcn_wave_barrier();
-        }
     }
-    // type bytes: stripes kPtrStripes .. kNst-1, then the tail words
-    const uint64_t node = node0 + q;
+};
+
+// After the pointer tiles: the type bytes (stripes 3F/4 .. nst-1, then the tail
+// words), the merge and the avalanche; lane 0 of the quad stores the node's checksum.
+template <uint32_t F, bool FULL>
+__device__ __forceinline__ void ring_finish(uint64_t acc, uint32_t j, uint64_t node, uint64_t pm, uint64_t m,
+                                            uint8_t type, uint64_t* __restrict__ parent_cs) {
+    constexpr uint32_t kSize = (F * 25u + 7u) & ~7u, kWords = kSize / 8, kNst = kSize / 32;
+    constexpr uint32_t kPtrStripes = 3 * F / 4;
+    const uint64_t rep = 0x0101010101010101ULL * type;
     uint32_t cnt = F;
     if (!FULL) {
         const uint64_t nn = node < pm ? node : pm - 1;
@@ -1081,17 +1067,125 @@ __device__ __forceinline__ void pointer_level_ring_body(const uint64_t* __restri
     if (j == 0 && node < pm) parent_cs[node] = h;
 }
 
-template <uint32_t F, int D>
+// One wave produces and consumes (k_pointer_level_ring).
+template <uint32_t F, uint32_t TS_, int D, bool FULL>
+__device__ __forceinline__ void pointer_level_ring_body(const uint64_t* __restrict__ cs, uint64_t m, uint64_t pm,
+                                                        uint64_t node0, uint64_t addr_base, uint64_t rev, uint8_t type,
+                                                        uint64_t* __restrict__ parent_cs,
+                                                        uint64_t (*ring)[16][RingShape<TS_>::RS]) {
+    using P = RingProducer<F, TS_, FULL>;
+    constexpr uint32_t TS = P::TS, NT = P::NT, IT = P::IT;
+    static_assert(NT % D == 0, "tile shape");
+    const uint32_t lane = threadIdx.x, q = lane >> 2, j = lane & 3;
+    const P prod(cs, m, pm, node0, addr_base, rev, lane);
+    uint64_t raw[D][IT];
+    uint64_t acc = acc_seed(j);
+#pragma unroll
+    for (int d = 0; d < D; ++d) prod.load(d, raw[d]);
+    prod.produce(0, raw[0], ring[0]);
+    prod.load(D, raw[0]);
+    // Tile t: produce tile t+1 into ring slot (t+1)&1 and refill its registers with
+    // tile t+1+D, then walk the 15 chain rounds of tile t (slot t&1). D is even and t0
+    // a multiple of D, so the slots are compile-time constants. (Merging the three
+    // into one basic block so the scheduler interleaves them measured 6 % slower.)
+    static_assert(D % 2 == 0, "static ring slots");
+    for (uint32_t t0 = 0; t0 < NT; t0 += D) {
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            const uint32_t t = t0 + d;
+            const int nb = (d + 1) % D;
+            if (t + 1 < NT) {
+                prod.produce(t + 1, raw[nb], ring[(d + 1) & 1]);
+                if (t + 1 + D < NT) prod.load(t + 1 + D, raw[nb]);
+            }
+            __builtin_amdgcn_wave_barrier();
+            const uint64_t* row = &ring[d & 1][q][j];
+#pragma unroll
+            for (uint32_t s = 0; s < TS; ++s) acc = round_pm(acc, row[4 * s]);
+            __builtin_amdgcn_wave_barrier();
+        }
+    }
+    ring_finish<F, FULL>(acc, j, node0 + q, pm, m, type, parent_cs);
+}
+
+template <uint32_t F, uint32_t TS, int D>
 __global__ __launch_bounds__(64) void k_pointer_level_ring(const uint64_t* __restrict__ cs, uint64_t m,
                                                            uint64_t addr_base, uint64_t rev, uint8_t type,
                                                            uint64_t* __restrict__ parent_cs) {
-    __shared__ uint64_t ring[2][16][kRingTileStripes * 4];  // 15 KiB: two tiles of 16 nodes
+    __shared__ uint64_t ring[2][16][RingShape<TS>::RS];  // two tiles of 16 nodes (15 KiB at TS = 15)
     const uint64_t pm = (m + F - 1) / F;
     const uint64_t node0 = static_cast<uint64_t>(blockIdx.x) * 16;
     if (node0 + 16 <= m / F)  // every node of this wave has F children (wave-uniform branch)
-        pointer_level_ring_body<F, D, true>(cs, m, pm, node0, addr_base, rev, type, parent_cs, ring);
+        pointer_level_ring_body<F, TS, D, true>(cs, m, pm, node0, addr_base, rev, type, parent_cs, ring);
     else
-        pointer_level_ring_body<F, D, false>(cs, m, pm, node0, addr_base, rev, type, parent_cs, ring);
+        pointer_level_ring_body<F, TS, D, false>(cs, m, pm, node0, addr_base, rev, type, parent_cs, ring);
+}
+
+// Producer / consumer waves (k_pointer_level_pc): C chain waves and C producer waves
+// per workgroup; producer wave C+i writes the premultiplied tiles of chain wave i's
+// 16 nodes, and the quads of the chain waves walk them, so a chain wave's instruction
+// stream holds only the LDS reads and the add / rotate / P1 multiply. One barrier per
+// tile: tile t+1 is written (slot (t+1)&1) while tile t is read (slot t&1); the
+// barrier after both orders the next reuse of each slot.
+template <uint32_t F, uint32_t TS_, int D, int C, bool FULL>
+__device__ __forceinline__ void pointer_level_pc_body(const uint64_t* __restrict__ cs, uint64_t m, uint64_t pm,
+                                                      uint64_t node0, uint64_t addr_base, uint64_t rev, uint8_t type,
+                                                      uint64_t* __restrict__ parent_cs,
+                                                      uint64_t (*ring)[16 * C][RingShape<TS_>::RS]) {
+    using P = RingProducer<F, TS_, FULL>;
+    constexpr uint32_t TS = P::TS, NT = P::NT, IT = P::IT;
+    static_assert(NT % D == 0 && D % 2 == 0, "tile shape / static ring slots");
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (wave >= C) {  // producer wave for chain wave (wave - C)
+        const uint32_t pair = wave - C;
+        const P prod(cs, m, pm, node0 + 16 * pair, addr_base, rev, lane);
+        uint64_t raw[D][IT];
+        auto tile = [&](int slot) { return reinterpret_cast<uint64_t(*)[P::RS]>(&ring[slot][16 * pair][0]); };
+#pragma unroll
+        for (int d = 0; d < D; ++d) prod.load(d, raw[d]);
+        prod.produce(0, raw[0], tile(0));
+        prod.load(D, raw[0]);
+        __syncthreads();
+        for (uint32_t t0 = 0; t0 < NT; t0 += D) {
+#pragma unroll
+            for (int d = 0; d < D; ++d) {
+                const uint32_t t = t0 + d;
+                const int nb = (d + 1) % D;
+                if (t + 1 < NT) {
+                    prod.produce(t + 1, raw[nb], tile((d + 1) & 1));
+                    if (t + 1 + D < NT) prod.load(t + 1 + D, raw[nb]);
+                }
+                __syncthreads();
+            }
+        }
+    } else {  // chain wave
+        const uint32_t q = wave * 16 + (lane >> 2), j = lane & 3;
+        uint64_t acc = acc_seed(j);
+        __syncthreads();
+        for (uint32_t t0 = 0; t0 < NT; t0 += D) {
+#pragma unroll
+            for (int d = 0; d < D; ++d) {
+                const uint64_t* row = &ring[d & 1][q][j];
+#pragma unroll
+                for (uint32_t s = 0; s < TS; ++s) acc = round_pm(acc, row[4 * s]);
+                __syncthreads();
+            }
+        }
+        ring_finish<F, FULL>(acc, j, node0 + q, pm, m, type, parent_cs);
+    }
+}
+
+template <uint32_t F, uint32_t TS, int D, int C>
+__global__ __launch_bounds__(128 * C) void k_pointer_level_pc(const uint64_t* __restrict__ cs, uint64_t m,
+                                                              uint64_t addr_base, uint64_t rev, uint8_t type,
+                                                              uint64_t* __restrict__ parent_cs) {
+    __shared__ uint64_t ring[2][16 * C][RingShape<TS>::RS];  // two tiles per chain wave
+    const uint64_t pm = (m + F - 1) / F;
+    const uint64_t node0 = static_cast<uint64_t>(blockIdx.x) * 16 * C;
+    if (node0 + 16 * C <= m / F)  // workgroup-uniform
+        pointer_level_pc_body<F, TS, D, C, true>(cs, m, pm, node0, addr_base, rev, type, parent_cs, ring);
+    else
+        pointer_level_pc_body<F, TS, D, C, false>(cs, m, pm, node0, addr_base, rev, type, parent_cs, ring);
 }
 
 // Small levels (a handful of nodes, e.g. the top of a shard tree): one workgroup per

@@ -152,9 +152,11 @@ constexpr uint32_t kMaxFanout = 1u << 16;
 // a node is then about one XXH64 chain (~26 us for 30,000 B); larger levels put a quad
 // on each node, 64 nodes per workgroup, to keep every CU busy.
 constexpr uint64_t kWideNodes = 256;
-// k_pointer_level_ring: child-checksum tiles loaded this many tiles ahead of the LDS
-// tile being produced (each tile is 15 rounds of the chain).
-constexpr int kRingPrefetch = 4;
+// k_pointer_level_pc: tiles of 15 stripes (20 child slots) per node; the producer wave
+// loads child checksums 6 tiles (90 chain rounds) ahead of the tile it writes
+// (profiles/r02_merkle/: 38 us for 13,982 nodes against 41 at 4 tiles and 52 at 12).
+constexpr uint32_t kRingTile = 15;
+constexpr int kRingPrefetch = 6;
 
 // Skewed persistent streaming kernel (k_xxh64_glds_skew): wave v starts kSkewTiles*v
 // tiles late, 4 KiB apart at 16-stripe tiles (profiles/r01_probe_phase_skew.txt). Its
@@ -793,17 +795,28 @@ int stormck_pointer_level_device(const uint64_t* d_child_cs, uint64_t m, uint64_
         HIP_TRY(hipGetLastError());
         return STORMCK_OK;
     }
-    static const bool ring_on = [] {
-        const char* e = std::getenv("STORMCK_POINTER_RING");  // probe knob: "0" = the register-quad kernel
-        return !(e && e[0] == '0');
+    // probe knob STORMCK_POINTER_RING: "0" = the register-quad kernel, "1" = one wave
+    // producing and hashing (k_pointer_level_ring); default: the producer / chain wave
+    // pair (k_pointer_level_pc). Measured alternatives (30- and 45-stripe tiles, prefetch
+    // 4 and 12 tiles, two pairs per workgroup, one producer for two chain waves):
+    // DESIGN.md §5, profiles/r02_merkle/.
+    static const int ring_mode = [] {
+        const char* e = std::getenv("STORMCK_POINTER_RING");
+        return e ? std::atoi(e) : 2;
     }();
-    if (ring_on && fanout == STORMCK_POINTERS_PER_BLOCK) {
-        // storm's fan-out: one wave per 16 nodes, premultiplied words staged in LDS
-        const uint64_t waves = (pm + 15) / 16;
-        if (waves > 0x7fffffffULL) return fail(STORMCK_EINVAL, "level too large");
-        hipLaunchKernelGGL((k_pointer_level_ring<STORMCK_POINTERS_PER_BLOCK, kRingPrefetch>),
-                           dim3(static_cast<unsigned>(waves)), dim3(64), 0, static_cast<hipStream_t>(stream),
-                           d_child_cs, m, child_addr_base, rev, child_type, d_parent_cs);
+    if (ring_mode != 0 && fanout == STORMCK_POINTERS_PER_BLOCK) {
+        // storm's fan-out: 16 nodes per workgroup, premultiplied words staged in LDS
+        constexpr uint32_t F = STORMCK_POINTERS_PER_BLOCK;
+        const uint64_t groups = (pm + 15) / 16;
+        if (groups > 0x7fffffffULL) return fail(STORMCK_EINVAL, "level too large");
+        const dim3 grid(static_cast<unsigned>(groups));
+        hipStream_t st = static_cast<hipStream_t>(stream);
+        if (ring_mode == 1)
+            hipLaunchKernelGGL((k_pointer_level_ring<F, kRingTile, 4>), grid, dim3(64), 0, st, d_child_cs, m,
+                               child_addr_base, rev, child_type, d_parent_cs);
+        else
+            hipLaunchKernelGGL((k_pointer_level_pc<F, kRingTile, kRingPrefetch, 1>), grid, dim3(128), 0, st, d_child_cs,
+                               m, child_addr_base, rev, child_type, d_parent_cs);
         HIP_TRY(hipGetLastError());
         return STORMCK_OK;
     }

@@ -12,7 +12,7 @@ from storm_amd import engine  # noqa: E402
 dev = torch.device("cuda", 0)
 torch.cuda.set_device(dev)
 st = torch.cuda.current_stream(dev)
-kind = "register-quad" if os.environ.get("STORMCK_POINTER_RING") == "0" else "ring"
+kind = {"0": "register-quad", "1": "ring (1 wave)"}.get(os.environ.get("STORMCK_POINTER_RING", ""), "ring (wave pair)")
 cs = torch.randint(-2**62, 2**62, (16 << 20,), dtype=torch.int64, device=dev)
 par = torch.empty(16384, dtype=torch.int64, device=dev)
 for m in (16 << 20, 8 << 20, 1 << 20, 300 * 1200):
