@@ -16,7 +16,6 @@ this file alone (independent of oracle/oracle.py and storm_amd/).
 """
 from __future__ import annotations
 
-import ctypes
 import json
 import os
 import struct

@@ -5,7 +5,6 @@ oracle as the per-shard hasher), the roots are all-gathered and combined, and ev
 rank must hold the same global root as the libxxhash combine fixture."""
 import json
 import os
-import sys
 import time
 
 import numpy as np

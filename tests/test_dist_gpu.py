@@ -5,7 +5,6 @@ rank's global root must equal the oracle's. RCCL itself runs in
 import os
 import socket
 
-import numpy as np
 import pytest
 
 pytestmark = pytest.mark.gpu

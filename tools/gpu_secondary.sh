@@ -1,7 +1,8 @@
-# secondary workloads (c5, f4 key tags) + kernel stats (run on the GPU box from the repo root)
+# The secondary workloads' bench lines (f1 commit, c5 mixed batch, f4 key tags)
 set -o pipefail
-mkdir -p gpurun_out/sec
-export TMPDIR=/tmp
-timeout -k 10 200 python bench.py --workload c5 --steps 50 > gpurun_out/sec/c5.log 2>&1 && echo c5-ok && tail -1 gpurun_out/sec/c5.log &&
-timeout -k 10 200 python bench.py --workload keytags --no-cpu > gpurun_out/sec/keytags.log 2>&1 && echo keytags-ok && tail -1 gpurun_out/sec/keytags.log &&
-timeout -k 10 200 rocprofv3 --kernel-trace --stats -d gpurun_out/sec/c5prof -o run -- python3 bench.py --workload c5 --steps 20 --no-cpu > gpurun_out/sec/c5prof.log 2>&1 && echo prof-ok
+out=gpurun_out/${1:-secondary}
+mkdir -p $out
+for w in commit c5 keytags; do
+  timeout -k 10 240 python bench.py --workload $w > $out/bench_$w.log 2>&1 || exit 1
+  tail -1 $out/bench_$w.log
+done
