@@ -57,6 +57,7 @@ def build_oracle(force: bool = False) -> str:
 
 
 PROBES = ("probe", "probe_keys", "probe_small", "alloc_probe", "phase_probe")  # tools/<name>.hip: design probes
+SANITIZE = os.path.join(ROOT, "tests", "sanitize")
 READPEAK = os.path.join(ROOT, "tools", "libreadpeak.so")  # bench.py's measured read peak (not product)
 
 
@@ -81,7 +82,22 @@ def build_probe(force: bool = False) -> str:
         if force or not _newer(out, srcs):
             subprocess.run([hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-o", out, srcs[0]], check=True)
         built.append(out)
+    # tools/single_call_probe.cpp: host leg vs device single call, in C (links the library)
+    out = os.path.join(ROOT, "tools", "single_call_probe")
+    src = os.path.join(ROOT, "tools", "single_call_probe.cpp")
+    if force or not _newer(out, [src, LIB]):
+        subprocess.run(["g++", "-O2", "-std=c++17", "-I", os.path.join(ROOT, "include"), src, "-L", LIB_DIR,
+                        "-lstormck", "-Wl,-rpath,$ORIGIN/../storm_amd/lib", "-o", out], check=True)
+    built.append(out)
     return " ".join(built)
+
+
+def build_sanitizers() -> str:
+    """tests/sanitize/build/host_paths_{asan,tsan}: the host code under ASan+UBSan and
+    TSan (tests/sanitize/build.sh; device code unchanged, no GPU sanitizer)."""
+    for kind in ("asan", "tsan"):
+        subprocess.run(["bash", os.path.join(SANITIZE, "build.sh"), kind], check=True, capture_output=True)
+    return os.path.join(SANITIZE, "build")
 
 
 if __name__ == "__main__":
