@@ -154,11 +154,10 @@ int main(int argc, char** argv) {
     const dim3 g(cus), blk(512);
     std::vector<V> vs = {
         {"shipped skew 8w T=16 R=2", [&](uint8_t* d, uint64_t* o) { hipLaunchKernelGGL((k_xxh64_glds_skew<16, 2, false, 8, 8, true>), g, blk, 0, 0, d, L, (uint32_t)L, n, o, nullptr, nullptr, nullptr); }},
-        {"4w T=32 (1 KiB rows) R=2", [&](uint8_t* d, uint64_t* o) { hipLaunchKernelGGL((k_xxh64_glds_rs<32, 2, 4, 4>), g, dim3(256), 0, 0, d, L, (uint32_t)L, n, o); }},
-        {"2w T=32 R=2, 2 WG/CU", [&](uint8_t* d, uint64_t* o) { hipLaunchKernelGGL((k_xxh64_glds_rs<32, 2, 4, 2>), dim3(2 * cus), dim3(128), 0, 0, d, L, (uint32_t)L, n, o); }},
-        {"2w T=64 (2 KiB rows) R=2", [&](uint8_t* d, uint64_t* o) { hipLaunchKernelGGL((k_xxh64_glds_rs<64, 2, 2, 2>), g, dim3(128), 0, 0, d, L, (uint32_t)L, n, o); }},
-        {"2w T=32 R=3", [&](uint8_t* d, uint64_t* o) { hipLaunchKernelGGL((k_xxh64_glds_rs<32, 3, 4, 2>), dim3(cus), dim3(128), 0, 0, d, L, (uint32_t)L, n, o); }},
-        {"4w T=16 R=2, 2 WG/CU", [&](uint8_t* d, uint64_t* o) { hipLaunchKernelGGL((k_xxh64_glds_rs<16, 2, 8, 4>), dim3(2 * cus), dim3(256), 0, 0, d, L, (uint32_t)L, n, o); }},
+        {"9w T=16 R=2 (144 blocks/CU)", [&](uint8_t* d, uint64_t* o) { hipLaunchKernelGGL((k_xxh64_glds_rs<16, 2, 8, 9>), g, dim3(576), 0, 0, d, L, (uint32_t)L, n, o); }},
+        {"10w T=16 R=2 (160 blocks/CU)", [&](uint8_t* d, uint64_t* o) { hipLaunchKernelGGL((k_xxh64_glds_rs<16, 2, 8, 10>), g, dim3(640), 0, 0, d, L, (uint32_t)L, n, o); }},
+        {"10w T=16 R=2 skew 6", [&](uint8_t* d, uint64_t* o) { hipLaunchKernelGGL((k_xxh64_glds_rs<16, 2, 6, 10>), g, dim3(640), 0, 0, d, L, (uint32_t)L, n, o); }},
+        {"8w T=20 R=2 (640 B rows)", [&](uint8_t* d, uint64_t* o) { hipLaunchKernelGGL((k_xxh64_glds_rs<20, 2, 6, 8>), g, blk, 0, 0, d, L, (uint32_t)L, n, o); }},
     };
     std::vector<std::vector<float>> ms(vs.size() * 2);
     for (int a = 0; a < 2; ++a) {
