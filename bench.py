@@ -184,6 +184,24 @@ def cpu_commit_baseline(seconds: float):
                       f"oracle/xxh64_oracle.c oracle_commit (serial Cache.Commit loop, 1 thread)"}
 
 
+def golden(name: str):
+    """A committed libxxhash fixture (tests/golden/, oracle/gen_golden.py), or None."""
+    path = os.path.join(ROOT, "tests", "golden", name)
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        return json.load(f)
+
+
+def check_against(got: int, want_hex, what: str):
+    """(root_check text, exit code) for a printed result against its fixture value."""
+    if want_hex is None:
+        return "no fixture for this workload", 0
+    if got == int(want_hex, 16):
+        return f"match ({what})", 0
+    return f"MISMATCH vs {what} {want_hex}", 3
+
+
 def commit_workload(a):
     """f1: one step = commit of a dirty forest of `commit_leaves` 32 KiB leaves under
     fan-out-1200 pointer blocks held in HBM (level-synchronous, stormck_commit_device:
@@ -228,9 +246,13 @@ def commit_workload(a):
                         "unit": "GB/s", "frac": round(blocks_bytes / (el / a.steps) / 1e9 / HBM_PEAK_GBS, 4),
                         "traffic": None, "kernel": "k_commit_level_glds<16,nt,8w> (whole call: host planning, record and checksum transfers included)"},
            "root": "0x%016x" % int(cs[-1])}
+    fx = golden("c3c4_roots.json")
+    want = fx["f1_commit_1m"]["root"][0] if fx and "f1_commit_1m" in fx and n == fx["f1_commit_1m"]["leaves"] else None
+    res["root_check"], rc = check_against(int(cs[-1]), want, "f1_commit_1m, tests/golden/c3c4_roots.json")
     if not a.no_cpu:
         res["cpu_baseline"] = cpu_commit_baseline(a.cpu_seconds)
     print(json.dumps(res), flush=True)
+    return rc
 
 
 def c5_workload(a):
@@ -290,6 +312,15 @@ def c5_workload(a):
            "batch_us": round(el / a.steps * 1e6, 1),
            "commit_forest_us": round(commit_us, 1),
            "commit_root": "0x%016x" % int(cs[-1])}
+    # the batch's checksums and the commit root against tests/golden/c5.json; the digest
+    # is XXH64 of the checksum array, taken with the library's single-call host leg
+    from storm_amd import blocks
+    fx = golden("c5.json")
+    digest = blocks.Checksum(out.cpu().numpy().view(np.uint64).astype("<u8"))
+    c1, rc1 = check_against(digest, fx and fx["batch_digest"], "c5 batch digest, tests/golden/c5.json")
+    c2, rc2 = check_against(int(cs[-1]), fx and fx["commit_root"], "c5 commit root, tests/golden/c5.json")
+    res["root_check"] = f"batch: {c1}; commit: {c2}"
+    rc = rc1 or rc2
     if not a.no_cpu:
         from oracle import oracle as o
         host = buf.cpu().numpy()
@@ -302,6 +333,7 @@ def c5_workload(a):
                                "sample": f"the same {n}-block batch hashed {reps}x in {el:.1f} s by oracle/xxh64_oracle.c",
                                "batch_us": round(el / reps * 1e6, 1)}
     print(json.dumps(res), flush=True)
+    return rc
 
 
 def keytags_workload(a):
@@ -341,6 +373,11 @@ def keytags_workload(a):
                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(n * (klen + 8) / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
                         "kernel": "k_key_tags_ring<nt,3,4,8> (per-wave 4-slot LDS-DMA ring)", "avg_launch_ms": round(kms, 4)}}
+    # all 64M tags against tests/golden/keytags.json (digest by the library's host leg)
+    from storm_amd import blocks
+    fx = golden("keytags.json")
+    digest = blocks.Checksum(out.cpu().numpy().view(np.uint64).astype("<u8"))
+    res["root_check"], rc = check_against(digest, fx and fx["digest"], "f4 tag digest, tests/golden/keytags.json")
     if not a.no_cpu:
         from oracle import oracle as o
         m = 1 << 20
@@ -353,6 +390,7 @@ def keytags_workload(a):
         res["cpu_baseline"] = {"value": round(reps * m / el / 1e9, 4), "unit": "Gkeys/s", "cores": 1, "kind": "port",
                                "sample": f"{m} 48-byte keys hashed {reps}x in {el:.1f} s by oracle/xxh64_oracle.c"}
     print(json.dumps(res), flush=True)
+    return rc
 
 
 def host_cpu_info():
@@ -462,12 +500,13 @@ def main():
         # no launcher: one rank process per GPU, started before this process touches a GPU
         sys.exit(spawn_ranks(a.gpus, sys.argv))
     if a.workload == "commit":
-        return commit_workload(a)
-    if a.workload == "keytags":
-        return keytags_workload(a)
-    if a.workload == "c5":
-        return c5_workload(a)
-    rc = block_checksum_workload(a)
+        rc = commit_workload(a)
+    elif a.workload == "keytags":
+        rc = keytags_workload(a)
+    elif a.workload == "c5":
+        rc = c5_workload(a)
+    else:
+        rc = block_checksum_workload(a)
     if rc:
         sys.exit(rc)
 

@@ -285,6 +285,55 @@ def gen_commit() -> None:
     })
 
 
+def gen_c5() -> None:
+    """c5 (BASELINE.json configs[4]) as bench.py --workload c5 runs it: synthetic
+    32 KiB-stride blocks 0..1201 hashed at storm's mixed lengths (1200 objectlist leaves
+    of 31,808 B, one 30,000 B pointer block, the 72 B singularity), and the same 1200
+    leaves committed as a forest under one fan-out-1200 pointer block rooted at the
+    singularity (storm_amd.commit.pointer_forest: leaf i has address 1 + i and
+    BirthRevision 2, nothing relocates), whose root checksum is the pointer block's."""
+    n_ol, rev = 1200, 1
+    lens = [31808] * n_ol + [30000, 72]
+    blocks = synth_blocks(0, len(lens), 32768)
+    cs = np.array([xx(blocks[i][:lens[i]]) for i in range(len(lens))], dtype=np.uint64)
+    leaf = [(int(cs[i]), 1 + i, rev + 1, 2) for i in range(n_ol)]
+    root = xx(pack_pointer_block(leaf, 1200))
+    write("c5.json", {
+        "config": "c5: bench.py --workload c5 (keystore/benchmark_test.go commit batch)", "seed": h(SEED),
+        "lens": {"31808": n_ol, "30000": 1, "72": 1}, "batch_digest": h(xx(cs.astype("<u8").tobytes())),
+        "first4": [h(int(v)) for v in cs[:4]], "last2": [h(int(v)) for v in cs[-2:]],
+        "commit_root": h(root), "commit_root_address": 1 + n_ol, "commit_revision": rev,
+    })
+
+
+def _keytags_worker(args):
+    first, count, klen = args
+    sys.path.insert(0, ROOT)
+    from oracle import oracle as o  # generator only; hashing stays libxxhash
+    per = 48 * 1024 // klen  # keys per 48 KiB synthetic block
+    buf = o.fill_synthetic(count // per, 48 * 1024, first // per)
+    mv = memoryview(buf)
+    return first, np.array([xxhash.xxh64_intdigest(mv[k * klen:(k + 1) * klen]) for k in range(count)],
+                           dtype=np.uint64)
+
+
+def gen_keytags() -> None:
+    """f4 as bench.py --workload keytags runs it: 64M keys of 48 B, packed (key i at byte
+    48 i of synthetic 48 KiB blocks 0..65535), each tagged with xxhash.Sum64; the digest
+    is XXH64 of the 64M tags (about a minute on every core)."""
+    import multiprocessing as mp
+    n, klen, chunk = 1 << 26, 48, 1 << 20
+    tags = np.empty(n, dtype=np.uint64)
+    with mp.get_context("fork").Pool(max(1, (os.cpu_count() or 2) - 1)) as pool:
+        for first, t in pool.imap_unordered(_keytags_worker, [(f, chunk, klen) for f in range(0, n, chunk)]):
+            tags[first:first + chunk] = t
+    write("keytags.json", {
+        "config": "f4: bench.py --workload keytags, 64M packed 48-byte keys", "seed": h(SEED), "keys": n,
+        "key_bytes": klen, "digest": h(xx(tags.astype("<u8").tobytes())),
+        "first4": [h(int(v)) for v in tags[:4]], "every_1048576th": [h(int(v)) for v in tags[::1 << 20]],
+    })
+
+
 def gen_big() -> None:
     """Digests (XXH64 of the little-endian checksum array) of the c2 (1M) and c3 (16M)
     synthetic 32 KiB block sets. Blocks are generated with the C oracle's generator
@@ -399,11 +448,17 @@ def gen_c4() -> None:
         groot = (xx(pack_pointer_block(table, f)), 2 * n_total, rev, 1)
         worlds[str(world)] = {"shard_roots": [[h(v) for v in r_[:3]] + [r_[3]] for r_ in table],
                               "global_root": [h(v) for v in groot[:3]] + [groot[3]]}
+    # f1: bench.py --workload commit commits the first 1M of these blocks as 32 KiB leaves
+    # under fan-out-1200 pointer blocks (storm_amd.commit.pointer_forest: leaves get
+    # addresses 1.., pointer blocks the next addresses level by level, BirthRevision 2
+    # everywhere, nothing relocates); the commit's root is the top pointer block's
+    f1 = tree_root_np(cs[:1 << 20], 1, (1 << 20) + 1, 2, f)
     write("c3c4_roots.json", {
         "rule": "synth_c1.json rule, stride = length = 32768, fan-out 1200, BirthRevision 1; see gen_c4",
         "seed": h(SEED),
         "c3": {"n": 1 << 24, "leaf_addr_base": 0, "node_addr_base": 1 << 24,
                "root": [h(v) for v in c3[:3]] + [c3[3]]},
+        "f1_commit_1m": {"leaves": 1 << 20, "root": [h(v) for v in f1[:3]] + [f1[3]]},
         "c4": {"n_total": n_total, "digest": h(xx(np.ascontiguousarray(cs).astype("<u8").tobytes())),
                "every_1048576th": [h(int(v)) for v in cs[::1 << 20]], "worlds": worlds},
     })
@@ -414,11 +469,15 @@ if __name__ == "__main__":
     if "--c4" in sys.argv:  # only the c3/c4 roots (several minutes on every core)
         gen_c4()
         sys.exit(0)
+    if "--keytags" in sys.argv:  # only the f4 digest (about a minute on every core)
+        gen_keytags()
+        sys.exit(0)
     gen_kat()
     gen_synth_c1()
     gen_mixed()
     gen_layouts()
     gen_merkle()
     gen_commit()
+    gen_c5()
     if "--big" in sys.argv:
         gen_big()
