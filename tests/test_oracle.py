@@ -85,3 +85,30 @@ def test_pointer_block_pack_matches_python():
     leaf = np.array([e[0] for e in entries], dtype=np.uint64)
     root = o.merkle_root(leaf, 1000, 5000, 7, 10)
     assert root == (o.xxh64_py(b), 5000, 7, 1)
+
+
+def test_c5_fixture_against_oracle():
+    """tests/golden/c5.json (libxxhash) = the C oracle on the same synthetic batch, and
+    the commit root = the oracle's packer + XXH64 over the leaves' pointers."""
+    import numpy as np
+    from oracle import oracle as o
+    g = load_golden("c5.json")
+    lens = [31808] * 1200 + [30000, 72]
+    buf = o.fill_synthetic(len(lens), 32768, 0)
+    cs = o.checksum_batch(buf, len(lens), 32768, lens=lens, threads=8)
+    assert o.xxh64(cs.astype("<u8")) == hx(g["batch_digest"])
+    leaf = [(int(cs[i]), 1 + i, 2, 2) for i in range(1200)]
+    assert o.xxh64(o.pack_pointer_block_py(leaf, 1200)) == hx(g["commit_root"])
+
+
+def test_keytags_fixture_samples_against_oracle():
+    """tests/golden/keytags.json samples (every 1,048,576th of 64M packed 48-byte keys)
+    = the C oracle on the same synthetic bytes."""
+    import numpy as np
+    from oracle import oracle as o
+    g = load_golden("keytags.json")
+    for s, want in enumerate(g["every_1048576th"]):
+        key = s << 20  # key index; 1024 keys per 48 KiB synthetic block
+        blk = o.fill_synthetic(1, 48 * 1024, key // 1024)
+        off = (key % 1024) * 48
+        assert o.xxh64(blk[off:off + 48]) == hx(want), s
