@@ -1537,7 +1537,10 @@ __global__ __launch_bounds__(256) void k_key_tags(const uint8_t* __restrict__ ke
 // at stride 48), so the stripe count and the tail fold into straight-line code; the
 // kernel is VALU-bound (about 28 64-bit multiplies per 48-byte key) and the generic tail
 // costs about a third of its instructions. KLEN = 0: the runtime `len`.
-template <int AUX, int P, int RING, int PW, int KLEN = 0>
+// SM (how the tags reach HBM): 0 = one 8-byte store per lane per batch; 1 = the same,
+// non-temporal; 2 = none (read-only probe); 3 = staged in the wave's LDS, then 16-byte
+// stores (4 KiB contiguous per wave); 4 = 3, non-temporal.
+template <int AUX, int P, int RING, int PW, int KLEN = 0, int SM = 0>
 __global__ __launch_bounds__(256) void k_key_tags_ring(const uint8_t* __restrict__ keys, uint32_t len_rt,
                                                         uint64_t batches, uint64_t* __restrict__ out) {
     static_assert(RING >= 2 && PW >= RING, "ring");
@@ -1607,8 +1610,30 @@ __global__ __launch_bounds__(256) void k_key_tags_ring(const uint8_t* __restrict
         }
         return;
     }
+    if constexpr (SM == 3 || SM == 4) {
+        static_assert(PW % 2 == 0 && PW * 64 * 8 <= RING * kRegion, "tags fit in the wave's ring");
+        wait_lgkm0();  // the last batch's LDS reads are done: the ring is free
+        uint64_t* tl = reinterpret_cast<uint64_t*>(buf);
 #pragma unroll
-    for (int i = 0; i < PW; ++i) out[(b0 + i) * 64 + lane] = h[i];
+        for (int i = 0; i < PW; ++i) tl[i * 64 + lane] = h[i];
+        u64x2* dst = reinterpret_cast<u64x2*>(out + b0 * 64);
+#pragma unroll
+        for (int k = 0; k < PW / 2; ++k) {
+            const u64x2 v = reinterpret_cast<const u64x2*>(tl)[k * 64 + lane];
+            if constexpr (SM == 4) __builtin_nontemporal_store(v, dst + k * 64 + lane);
+            else dst[k * 64 + lane] = v;
+        }
+    } else if constexpr (SM != 2) {
+#pragma unroll
+        for (int i = 0; i < PW; ++i) {
+            if constexpr (SM == 1) __builtin_nontemporal_store(h[i], out + (b0 + i) * 64 + lane);
+            else out[(b0 + i) * 64 + lane] = h[i];
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < PW; ++i)
+            if (h[i] == 0x5354524d5354524dULL) out[(b0 + i) * 64 + lane] = h[i];  // keeps the hash live
+    }
 #undef STORMCK_RING_ISSUE
 }
 

@@ -1047,6 +1047,10 @@ int stormck_key_tags_device(const void* d_keys, uint64_t stride, const uint64_t*
         const uint64_t batches = n / 64;
         constexpr uint32_t kPerWave = 8;
         constexpr int kKeyRing = 4;
+        // tags leave by non-temporal stores: the 8 B-per-key write stream costs the
+        // read stream about a quarter of the rate, nt stores recover ~3 %
+        // (tools/probe_keys.hip, profiles/r02_keys/)
+        constexpr int kKeyStore = 1;
         const uint64_t waves = (batches + kPerWave - 1) / kPerWave;
         const uint64_t wgs = (waves + 3) / 4;
         if (wgs > 0x7fffffffULL) return fail(STORMCK_EINVAL, "batch too large for one launch");
@@ -1055,34 +1059,34 @@ int stormck_key_tags_device(const void* d_keys, uint64_t stride, const uint64_t*
         switch (stride) {
             case 16:
                 if (len == 16)
-                    hipLaunchKernelGGL((k_key_tags_ring<kAuxNT, 1, kKeyRing, kPerWave, 16>), grid_k, dim3(kThreads), ring_lds,
+                    hipLaunchKernelGGL((k_key_tags_ring<kAuxNT, 1, kKeyRing, kPerWave, 16, kKeyStore>), grid_k, dim3(kThreads), ring_lds,
                                        st, k, len, batches, d_out);
                 else
-                    hipLaunchKernelGGL((k_key_tags_ring<kAuxNT, 1, kKeyRing, kPerWave>), grid_k, dim3(kThreads), ring_lds, st,
+                    hipLaunchKernelGGL((k_key_tags_ring<kAuxNT, 1, kKeyRing, kPerWave, 0, kKeyStore>), grid_k, dim3(kThreads), ring_lds, st,
                                        k, len, batches, d_out);
                 break;
             case 32:
                 if (len == 32)
-                    hipLaunchKernelGGL((k_key_tags_ring<kAuxNT, 2, kKeyRing, kPerWave, 32>), grid_k, dim3(kThreads), ring_lds,
+                    hipLaunchKernelGGL((k_key_tags_ring<kAuxNT, 2, kKeyRing, kPerWave, 32, kKeyStore>), grid_k, dim3(kThreads), ring_lds,
                                        st, k, len, batches, d_out);
                 else
-                    hipLaunchKernelGGL((k_key_tags_ring<kAuxNT, 2, kKeyRing, kPerWave>), grid_k, dim3(kThreads), ring_lds, st,
+                    hipLaunchKernelGGL((k_key_tags_ring<kAuxNT, 2, kKeyRing, kPerWave, 0, kKeyStore>), grid_k, dim3(kThreads), ring_lds, st,
                                        k, len, batches, d_out);
                 break;
             case 48:
                 if (len == 48)
-                    hipLaunchKernelGGL((k_key_tags_ring<kAuxNT, 3, kKeyRing, kPerWave, 48>), grid_k, dim3(kThreads), ring_lds,
+                    hipLaunchKernelGGL((k_key_tags_ring<kAuxNT, 3, kKeyRing, kPerWave, 48, kKeyStore>), grid_k, dim3(kThreads), ring_lds,
                                        st, k, len, batches, d_out);
                 else
-                    hipLaunchKernelGGL((k_key_tags_ring<kAuxNT, 3, kKeyRing, kPerWave>), grid_k, dim3(kThreads), ring_lds, st,
+                    hipLaunchKernelGGL((k_key_tags_ring<kAuxNT, 3, kKeyRing, kPerWave, 0, kKeyStore>), grid_k, dim3(kThreads), ring_lds, st,
                                        k, len, batches, d_out);
                 break;
             case 64:
                 if (len == 64)
-                    hipLaunchKernelGGL((k_key_tags_ring<kAuxNT, 4, kKeyRing, kPerWave, 64>), grid_k, dim3(kThreads), ring_lds,
+                    hipLaunchKernelGGL((k_key_tags_ring<kAuxNT, 4, kKeyRing, kPerWave, 64, kKeyStore>), grid_k, dim3(kThreads), ring_lds,
                                        st, k, len, batches, d_out);
                 else
-                    hipLaunchKernelGGL((k_key_tags_ring<kAuxNT, 4, kKeyRing, kPerWave>), grid_k, dim3(kThreads), ring_lds, st,
+                    hipLaunchKernelGGL((k_key_tags_ring<kAuxNT, 4, kKeyRing, kPerWave, 0, kKeyStore>), grid_k, dim3(kThreads), ring_lds, st,
                                        k, len, batches, d_out);
                 break;
             default:
