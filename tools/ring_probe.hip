@@ -34,7 +34,9 @@
     } while (0)
 
 namespace stormck {
-template <int T, int R, int SKEW, int WAVES = 8>
+// PERM 1: wave v hashes the group's blocks v, v+8, v+16, ... instead of 16v..16v+15.
+// PHASE k: wave v starts (k*v mod WAVES)*SKEW tiles late (k = 1: shipped order).
+template <int T, int R, int SKEW, int WAVES = 8, int PERM = 0, int PHASE = 1>
 __global__ __launch_bounds__(64 * WAVES) void k_xxh64_glds_rs(const uint8_t* __restrict__ base, uint64_t stride,
                                                               uint32_t len, uint64_t n, uint64_t* __restrict__ out) {
     constexpr int BPW = 16 * WAVES;
@@ -52,7 +54,8 @@ __global__ __launch_bounds__(64 * WAVES) void k_xxh64_glds_rs(const uint8_t* __r
     if (blockIdx.x >= ngroups) return;
     const uint32_t nst = len >> 5, ntiles = nst / T;
     const uint64_t total = ((ngroups - blockIdx.x + G - 1) / G) * ntiles;
-    const int64_t ph = static_cast<int64_t>(wave) * SKEW;
+    const int64_t ph = static_cast<int64_t>((PHASE * wave) % WAVES) * SKEW;
+    auto perm = [](uint32_t bb) -> uint32_t { return PERM ? (bb % 16) * WAVES + bb / 16 : bb; };
     const uint64_t steps = total + static_cast<uint64_t>(WAVES - 1) * SKEW;
 
     uint32_t prow[PER_WAVE], pofs[PER_WAVE];
@@ -70,7 +73,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_xxh64_glds_rs(const uint8_t* __r
         if (it == 0) {
 #pragma unroll
             for (int k = 0; k < PER_WAVE; ++k) {
-                uint64_t gb = ig * BPW + prow[k];
+                uint64_t gb = ig * BPW + perm(prow[k]);
                 if (gb >= n) gb = n - 1;
                 src[k] = base + gb * stride + pofs[k];
             }
@@ -104,7 +107,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_xxh64_glds_rs(const uint8_t* __r
                 acc = round(acc, *reinterpret_cast<const uint64_t*>(row + q * 16));
             }
             if (++ht == ntiles) {
-                const uint64_t gbk = hg * BPW + b;
+                const uint64_t gbk = hg * BPW + perm(b);
                 const uint64_t gb = gbk < n ? gbk : n - 1;
                 const uint8_t* blk_src = base + gb * stride;
                 for (uint32_t s = ntiles * T; s < nst; ++s)
@@ -154,10 +157,10 @@ int main(int argc, char** argv) {
     const dim3 g(cus), blk(512);
     std::vector<V> vs = {
         {"shipped skew 8w T=16 R=2", [&](uint8_t* d, uint64_t* o) { hipLaunchKernelGGL((k_xxh64_glds_skew<16, 2, false, 8, 8, true>), g, blk, 0, 0, d, L, (uint32_t)L, n, o, nullptr, nullptr, nullptr); }},
-        {"9w T=16 R=2 (144 blocks/CU)", [&](uint8_t* d, uint64_t* o) { hipLaunchKernelGGL((k_xxh64_glds_rs<16, 2, 8, 9>), g, dim3(576), 0, 0, d, L, (uint32_t)L, n, o); }},
-        {"10w T=16 R=2 (160 blocks/CU)", [&](uint8_t* d, uint64_t* o) { hipLaunchKernelGGL((k_xxh64_glds_rs<16, 2, 8, 10>), g, dim3(640), 0, 0, d, L, (uint32_t)L, n, o); }},
-        {"10w T=16 R=2 skew 6", [&](uint8_t* d, uint64_t* o) { hipLaunchKernelGGL((k_xxh64_glds_rs<16, 2, 6, 10>), g, dim3(640), 0, 0, d, L, (uint32_t)L, n, o); }},
-        {"8w T=20 R=2 (640 B rows)", [&](uint8_t* d, uint64_t* o) { hipLaunchKernelGGL((k_xxh64_glds_rs<20, 2, 6, 8>), g, blk, 0, 0, d, L, (uint32_t)L, n, o); }},
+        {"blocks v+8k, phases 3v", [&](uint8_t* d, uint64_t* o) { hipLaunchKernelGGL((k_xxh64_glds_rs<16, 2, 8, 8, 1, 3>), g, blk, 0, 0, d, L, (uint32_t)L, n, o); }},
+        {"blocks v+8k, phases 5v", [&](uint8_t* d, uint64_t* o) { hipLaunchKernelGGL((k_xxh64_glds_rs<16, 2, 8, 8, 1, 5>), g, blk, 0, 0, d, L, (uint32_t)L, n, o); }},
+        {"blocks v+8k, phases 7v", [&](uint8_t* d, uint64_t* o) { hipLaunchKernelGGL((k_xxh64_glds_rs<16, 2, 8, 8, 1, 7>), g, blk, 0, 0, d, L, (uint32_t)L, n, o); }},
+        {"shipped again", [&](uint8_t* d, uint64_t* o) { hipLaunchKernelGGL((k_xxh64_glds_skew<16, 2, false, 8, 8, true>), g, blk, 0, 0, d, L, (uint32_t)L, n, o, nullptr, nullptr, nullptr); }},
     };
     std::vector<std::vector<float>> ms(vs.size() * 2);
     for (int a = 0; a < 2; ++a) {
