@@ -18,7 +18,7 @@
 //   * k_commit_level*: f1 commit levels; k_pointer_level / _node: Merkle nodes
 //   * k_key_tags*    : f4, one lane per short key
 // (A lane-per-block mapping was measured and rejected: 0.59-0.66 of HBM peak,
-// profiles/r01_probe*.txt)
+// profiles/r01_probe*.txt; DESIGN.md §4. Its kernel left the library in round 2.)
 // The per-block sizes (stride / explicit offsets) and lengths (uniform / per-block)
 // cover storm's block types: 72, 28808, 30000, 31808, 32768 bytes.
 #pragma once
@@ -765,72 +765,6 @@ __global__ __launch_bounds__(64 * WAVES) void k_xxh64_glds_skew(const uint8_t* _
             ++hc;
         }
     }
-}
-
-// ---------------------------------------------------------------------------
-template <int U, bool NT = false>
-__global__ __launch_bounds__(256) void k_xxh64_lane(const uint8_t* __restrict__ base, uint64_t stride,
-                                                      uint32_t len, uint64_t n, uint64_t* __restrict__ out) {
-    const uint64_t blk = static_cast<uint64_t>(blockIdx.x) * 256 + threadIdx.x;
-    if (blk >= n) return;
-    const uint8_t* src = base + blk * stride;
-    const uint32_t nst = len >> 5;
-    const u64x2* p = reinterpret_cast<const u64x2*>(src);
-    uint64_t v1 = kV1, v2 = kV2, v3 = kV3, v4 = kV4;
-    const uint32_t ngroups = nst / U;
-    uint32_t s = 0;
-    if (ngroups > 0) {
-        u64x2 a[2 * U], b[2 * U];
-#pragma unroll
-        for (int u = 0; u < 2 * U; ++u) a[u] = ldg<NT>(p + u);
-        uint32_t g = 1;
-        for (; g + 1 < ngroups; g += 2) {
-            const u64x2* q = p + 2 * U * g;
-#pragma unroll
-            for (int u = 0; u < 2 * U; ++u) b[u] = ldg<NT>(q + u);
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                v1 = round(v1, a[2 * u].x); v2 = round(v2, a[2 * u].y);
-                v3 = round(v3, a[2 * u + 1].x); v4 = round(v4, a[2 * u + 1].y);
-            }
-            q += 2 * U;
-#pragma unroll
-            for (int u = 0; u < 2 * U; ++u) a[u] = ldg<NT>(q + u);
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                v1 = round(v1, b[2 * u].x); v2 = round(v2, b[2 * u].y);
-                v3 = round(v3, b[2 * u + 1].x); v4 = round(v4, b[2 * u + 1].y);
-            }
-        }
-        if (g < ngroups) {
-            const u64x2* q = p + 2 * U * g;
-#pragma unroll
-            for (int u = 0; u < 2 * U; ++u) b[u] = ldg<NT>(q + u);
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                v1 = round(v1, a[2 * u].x); v2 = round(v2, a[2 * u].y);
-                v3 = round(v3, a[2 * u + 1].x); v4 = round(v4, a[2 * u + 1].y);
-            }
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                v1 = round(v1, b[2 * u].x); v2 = round(v2, b[2 * u].y);
-                v3 = round(v3, b[2 * u + 1].x); v4 = round(v4, b[2 * u + 1].y);
-            }
-        } else {
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                v1 = round(v1, a[2 * u].x); v2 = round(v2, a[2 * u].y);
-                v3 = round(v3, a[2 * u + 1].x); v4 = round(v4, a[2 * u + 1].y);
-            }
-        }
-        s = ngroups * U;
-    }
-    for (; s < nst; ++s) {
-        const u64x2 x = p[2 * s], y = p[2 * s + 1];
-        v1 = round(v1, x.x); v2 = round(v2, x.y); v3 = round(v3, y.x); v4 = round(v4, y.y);
-    }
-    const uint64_t h0 = (len >= 32) ? converge(v1, v2, v3, v4) : kP5;
-    out[blk] = finish_fast(h0, len, src + 32 * static_cast<uint64_t>(nst), len & 31);
 }
 
 // ---------------------------------------------------------------------------
