@@ -108,6 +108,44 @@ __global__ __launch_bounds__(256) void k_read_nt(const u64x2* __restrict__ p, ui
     for (; i < n16; i += stride) acc ^= ldg<true>(p + i);
     if ((acc.x ^ acc.y) == 0x1234567) out[0] = acc.x;
 }
+// The traffic of the key-tag pass without its hash: each lane reads one 48-byte key
+// (3 x 16 B, non-temporal) and writes one 8-byte word, grid-stride. Its rate is the
+// ceiling of a read-48 / write-8 stream on this HBM, the bound f4 is measured against.
+template <bool NTS>
+__global__ __launch_bounds__(256) void k_copy_fold(const u64x2* __restrict__ p, uint64_t n, uint64_t* __restrict__ out) {
+    const uint64_t stride = (uint64_t)gridDim.x * 256;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
+        const u64x2 a = ldg<true>(p + 3 * i), b = ldg<true>(p + 3 * i + 1), c = ldg<true>(p + 3 * i + 2);
+        const u64x2 f = a ^ b ^ c;
+        if (NTS) __builtin_nontemporal_store(f.x ^ f.y, out + i);
+        else out[i] = f.x ^ f.y;
+    }
+}
+// The same traffic fully coalesced: a wave reads a batch's 3 KiB as 3 contiguous
+// 1 KiB loads (16 B per lane) and writes 512 B (8 B per lane), grid-stride over
+// batches, U batches per wave-iteration in flight. No hash; the values are not tags.
+template <int U>
+__global__ __launch_bounds__(256) void k_stream_rw(const u64x2* __restrict__ p, uint64_t batches, uint64_t* __restrict__ out) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t waves = (uint64_t)gridDim.x * 4;
+    uint64_t w = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    for (; w + (U - 1) * waves < batches; w += U * waves) {
+        u64x2 v[U][3];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int k = 0; k < 3; ++k) v[u][k] = ldg<true>(p + (w + u * waves) * 192 + k * 64 + lane);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const u64x2 f = v[u][0] ^ v[u][1] ^ v[u][2];
+            __builtin_nontemporal_store(f.x ^ f.y, out + (w + u * waves) * 64 + lane);
+        }
+    }
+    for (; w < batches; w += waves) {
+        const u64x2 f = ldg<true>(p + w * 192 + lane) ^ ldg<true>(p + w * 192 + 64 + lane) ^ ldg<true>(p + w * 192 + 128 + lane);
+        __builtin_nontemporal_store(f.x ^ f.y, out + w * 64 + lane);
+    }
+}
 }  // namespace stormck
 
 struct Timer {
@@ -164,6 +202,20 @@ int main(int argc, char** argv) {
     SMV(4, "ring klen=48, LDS-staged x4 nt");
     vs.push_back({"grid-stride read nt, no hash", [&] {
         hipLaunchKernelGGL(k_read_nt, dim3(16384), dim3(256), 0, 0, (const u64x2*)keys, n * klen / 16, out); }});
+    vs.push_back({"read 48 / write 8, no hash", [&] {
+        hipLaunchKernelGGL(k_copy_fold<false>, dim3(16384), dim3(256), 0, 0, (const u64x2*)keys, n, out); }});
+    vs.push_back({"read 48 / write 8 nt, no hash", [&] {
+        hipLaunchKernelGGL(k_copy_fold<true>, dim3(16384), dim3(256), 0, 0, (const u64x2*)keys, n, out); }});
+    vs.push_back({"r48/w8 nt, no hash, 64K WGs", [&] {
+        hipLaunchKernelGGL(k_copy_fold<true>, dim3(65536), dim3(256), 0, 0, (const u64x2*)keys, n, out); }});
+    vs.push_back({"coalesced r3K/w512 U=1, no hash", [&] {
+        hipLaunchKernelGGL(k_stream_rw<1>, dim3(16384), dim3(256), 0, 0, (const u64x2*)keys, batches, out); }});
+    vs.push_back({"coalesced r3K/w512 U=2, no hash", [&] {
+        hipLaunchKernelGGL(k_stream_rw<2>, dim3(8192), dim3(256), 0, 0, (const u64x2*)keys, batches, out); }});
+    vs.push_back({"coalesced r3K/w512 U=4, no hash", [&] {
+        hipLaunchKernelGGL(k_stream_rw<4>, dim3(4096), dim3(256), 0, 0, (const u64x2*)keys, batches, out); }});
+    vs.push_back({"coalesced r3K/w512 U=4, 1K WGs", [&] {
+        hipLaunchKernelGGL(k_stream_rw<4>, dim3(1024), dim3(256), 0, 0, (const u64x2*)keys, batches, out); }});
     hipDeviceProp_t prop; CK(hipGetDeviceProperties(&prop, 0));
     const unsigned cus = (unsigned)prop.multiProcessorCount;
 #define WG(BW, MULT)                                                                                        \
