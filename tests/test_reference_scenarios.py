@@ -241,3 +241,43 @@ def test_store_validation_on_device(gpu, tmp_path):
     assert [int(v) for v in got] == [o.xxh64(bytes(buf[i, :size])) for i in range(len(cases))]
     assert [blocks.VerifyChecksum(0, bytes(buf[i, :size]), expected[i]) is None for i in range(4)] == \
         [True, False, False, True]
+
+
+# keystore/keystore_test.go:38-47 (TestSetGet): "Key intentionally takes 2.5 chunks."
+SETGET_KEY = bytes(range(0x50))
+
+
+def test_keystore_set_get_tag():
+    """The tree tag of TestSetGet's 80-byte key, xxhash.Sum64(key)
+    (keystore/keystore.go:33,66), on the host leg that keyTag binds
+    (integration/go/keystore/keytag_stormck.go)."""
+    assert blocks.Checksum(SETGET_KEY) == o.xxh64(SETGET_KEY)
+
+
+@pytest.mark.gpu
+def test_keystore_storing_batches_tags(gpu):
+    """keystore_test.go:74-140 (TestStoringBatches): 1,500 batches of 5 random 48-byte
+    keys. Their tags on the device, at a fixed stride and packed with TestSetGet's key
+    and ragged neighbours, match xxhash.Sum64 of each key."""
+    from storm_amd import engine
+    torch = gpu
+    rng = np.random.default_rng(74)
+    keys = rng.integers(0, 256, size=(1500 * 5, 48), dtype=np.uint8)
+    d_keys = torch.from_numpy(keys.reshape(-1)).cuda()
+    out = torch.zeros(len(keys), dtype=torch.int64, device="cuda")
+    engine.key_tags_device(d_keys.data_ptr(), len(keys), out.data_ptr(), stride=48, length=48)
+    torch.cuda.synchronize()
+    got = out.cpu().numpy().view(np.uint64)
+    assert [int(v) for v in got] == [o.xxh64(bytes(k)) for k in keys]
+
+    packed = [SETGET_KEY] + [bytes(keys[i, :1 + i % 48]) for i in range(300)] + [bytes(256 * [0xAB])]
+    offs = np.cumsum([0] + [len(k) for k in packed[:-1]]).astype(np.uint64)
+    lens = np.array([len(k) for k in packed], dtype=np.uint32)
+    d_buf = torch.from_numpy(np.frombuffer(b"".join(packed), dtype=np.uint8).copy()).cuda()
+    d_offs = torch.from_numpy(offs.view(np.int64)).cuda()
+    d_lens = torch.from_numpy(lens.view(np.int32)).cuda()
+    out2 = torch.zeros(len(packed), dtype=torch.int64, device="cuda")
+    engine.key_tags_device(d_buf.data_ptr(), len(packed), out2.data_ptr(), d_offsets=d_offs.data_ptr(),
+                           d_lens=d_lens.data_ptr())
+    torch.cuda.synchronize()
+    assert [int(v) for v in out2.cpu().numpy().view(np.uint64)] == [o.xxh64(k) for k in packed]
