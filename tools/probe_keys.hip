@@ -240,6 +240,7 @@ int main(int argc, char** argv) {
             for (int k = 0; k < reps; ++k) { t.start(); vs[v].f(); gks[v].push_back(n / (t.stop() * 1e-3) / 1e9); }
         }
     printf("keys %llu x %u B (%.2f GB + %.2f GB out)\n", (unsigned long long)n, klen, n * klen / 1e9, n * 8 / 1e9);
+    printf("GB/s counts %u B per key (key read + tag written); the read-only variants move %u B\n", klen + 8, klen);
     for (size_t v = 0; v < vs.size(); ++v) {
         auto g = gks[v]; std::sort(g.begin(), g.end());
         const double med = g[g.size() / 2];
