@@ -58,6 +58,9 @@ def parse():
     p.add_argument("--settle", type=float, default=1.0,
                    help="before the W warmup steps, run untimed steps for at least this many seconds so the "
                         "GPU clocks settle (short workloads otherwise time a ramping clock)")
+    p.add_argument("--c5-mix", default="keystore", choices=["keystore", "storm"],
+                   help="c5 batch: BenchmarkKeyStore's commit (objectlist leaves) or BenchmarkStorm's (blob leaves "
+                        "and a spacelist block)")
     p.add_argument("--workload", default="c3", choices=["c3", "commit", "keytags", "c5"],
                    help="c3 = BASELINE metric (default); commit = f1 level-synchronous Cache.Commit of a dirty "
                         "forest; keytags = f4 xxhash.Sum64 of 48-byte keys")
@@ -272,7 +275,9 @@ def c5_workload(a):
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     n_ol = 1200
-    lens = np.array([31808] * n_ol + [30000, 72], dtype=np.uint32)
+    storm_mix = a.c5_mix == "storm"
+    leaf_len = 32768 if storm_mix else 31808  # blob leaves (BenchmarkStorm) or objectlist leaves (BenchmarkKeyStore)
+    lens = np.array([leaf_len] * n_ol + ([28808] if storm_mix else []) + [30000, 72], dtype=np.uint32)
     n = len(lens)
     buf = torch.empty((n, BLOCK), dtype=torch.uint8, device=dev)
     engine.fill_synthetic_device(buf.data_ptr(), BLOCK, n, 0, 0x53544F524D)
@@ -280,7 +285,7 @@ def c5_workload(a):
     out = torch.empty(n, dtype=torch.int64, device=dev)
     st = torch.cuda.current_stream(dev).cuda_stream
     # the commit form: 1200 objectlist leaves under one pointer block (fan-out 1200), rooted at the singularity
-    b0, size, last = sc.pointer_forest(n_ol, 31808, FANOUT, slot=BLOCK, revision=REV)
+    b0, size, last = sc.pointer_forest(n_ol, leaf_len, FANOUT, slot=BLOCK, revision=REV)
     arena = torch.zeros(size, dtype=torch.uint8, device=dev)
     engine.fill_synthetic_device(arena.data_ptr() + BLOCK, BLOCK, n_ol, 0, 0x53544F524D)
 
@@ -307,8 +312,11 @@ def c5_workload(a):
            "unit": "GiB/s", "n_gpus": 1, "steps": a.steps, "warmup": a.warmup,
            "ms_per_step": round(el / a.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
            "vs_baseline": None, "dtype": "u64", "data": "synthetic",
-           "config": {"workload": "c5: 1200 x 31808 B objectlist + 1 x 30000 B pointer + 1 x 72 B singularity "
-                                  "(keystore/benchmark_test.go commit), per-block lengths", "blocks": n,
+           "config": {"workload": ("c5 (storm mix): 1200 x 32768 B blob + 1 x 28808 B spacelist + 1 x 30000 B pointer "
+                                   "+ 1 x 72 B singularity (benchmark_test.go BenchmarkStorm commit), per-block lengths"
+                                   if storm_mix else
+                                   "c5: 1200 x 31808 B objectlist + 1 x 30000 B pointer + 1 x 72 B singularity "
+                                   "(keystore/benchmark_test.go commit), per-block lengths"), "blocks": n,
                       "hashed_bytes": hashed},
            "batch_us": round(el / a.steps * 1e6, 1),
            "commit_forest_us": round(commit_us, 1),
@@ -317,6 +325,8 @@ def c5_workload(a):
     # is XXH64 of the checksum array, taken with the library's single-call host leg
     from storm_amd import blocks
     fx = golden("c5.json")
+    if fx and storm_mix:
+        fx = fx.get("storm")
     digest = blocks.Checksum(out.cpu().numpy().view(np.uint64).astype("<u8"))
     c1, rc1 = check_against(digest, fx and fx["batch_digest"], "c5 batch digest, tests/golden/c5.json")
     c2, rc2 = check_against(int(cs[-1]), fx and fx["commit_root"], "c5 commit root, tests/golden/c5.json")

@@ -298,11 +298,23 @@ def gen_c5() -> None:
     cs = np.array([xx(blocks[i][:lens[i]]) for i in range(len(lens))], dtype=np.uint64)
     leaf = [(int(cs[i]), 1 + i, rev + 1, 2) for i in range(n_ol)]
     root = xx(pack_pointer_block(leaf, 1200))
+    # the BenchmarkStorm mix (/root/reference/benchmark_test.go): storm.Set
+    # adds blob leaves of 32,768 B and a spacelist block of 28,808 B to the same commit
+    n_bl = 1200
+    lens_s = [32768] * n_bl + [28808, 30000, 72]
+    blocks_s = synth_blocks(0, len(lens_s), 32768)
+    cs_s = np.array([xx(blocks_s[i][:lens_s[i]]) for i in range(len(lens_s))], dtype=np.uint64)
+    root_s = xx(pack_pointer_block([(int(cs_s[i]), 1 + i, rev + 1, 2) for i in range(n_bl)], 1200))
     write("c5.json", {
         "config": "c5: bench.py --workload c5 (keystore/benchmark_test.go commit batch)", "seed": h(SEED),
         "lens": {"31808": n_ol, "30000": 1, "72": 1}, "batch_digest": h(xx(cs.astype("<u8").tobytes())),
         "first4": [h(int(v)) for v in cs[:4]], "last2": [h(int(v)) for v in cs[-2:]],
         "commit_root": h(root), "commit_root_address": 1 + n_ol, "commit_revision": rev,
+        "storm": {"config": "bench.py --workload c5 --c5-mix storm (benchmark_test.go BenchmarkStorm commit batch)",
+                  "lens": {"32768": n_bl, "28808": 1, "30000": 1, "72": 1},
+                  "batch_digest": h(xx(cs_s.astype("<u8").tobytes())),
+                  "first4": [h(int(v)) for v in cs_s[:4]], "last3": [h(int(v)) for v in cs_s[-3:]],
+                  "commit_root": h(root_s), "commit_root_address": 1 + n_bl},
     })
 
 

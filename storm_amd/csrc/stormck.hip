@@ -935,26 +935,45 @@ int stormck_read_verify_fd(int fd, const uint64_t* addresses, const uint32_t* le
     }
     int rc = device_check();
     if (rc) return rc;
-    // Reads (Store.ReadBlock: Seek(address*BlockSize) + Read) run on a reader thread
-    // one super-chunk ahead of the GPU verify of the previous super-chunk. Runs of
-    // consecutive addresses whose slots are contiguous (full blocks, dst_stride ==
-    // block_size) are read with one pread of up to kRunBytes. An O_DIRECT descriptor
-    // reaches the device, whose rate needs queue depth: 32 reader threads instead of 16
-    // (STORMCK_READ_THREADS overrides).
+    // Reads (Store.ReadBlock: Seek(address*BlockSize) + Read) run on a pool of reader
+    // threads that take pieces of the batch in index order from one shared counter, so
+    // the pool streams across super-chunk boundaries without joining; the GPU verifies
+    // each 1 GiB super-chunk as soon as its last piece has landed. Runs of consecutive
+    // addresses whose slots are contiguous (full blocks, dst_stride == block_size) are
+    // read with one pread of up to kRunBytes. An O_DIRECT descriptor reaches the device,
+    // whose rate needs queue depth: 32 reader threads instead of 16 (STORMCK_READ_THREADS
+    // overrides; on the test boxes' overlay filesystem, counts from 8 to 64 measured the
+    // same within its run-to-run noise).
     constexpr uint64_t kRunBytes = 1ULL << 20;
     const uint64_t max_run = full && dst_stride == block_size ? std::max<uint64_t>(1, kRunBytes / block_size) : 1;
     unsigned nt = direct ? 32u : std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
     if (const char* e = std::getenv("STORMCK_READ_THREADS")) nt = std::max(1, std::atoi(e));
-    const uint64_t per_super = std::max<uint64_t>(1, (1ULL << 30) / std::max<uint64_t>(dst_stride, 1));
+    uint64_t super_bytes = 1ULL << 30;  // STORMCK_READ_SUPER_BYTES: smaller super-chunks, for tests
+    if (const char* e = std::getenv("STORMCK_READ_SUPER_BYTES")) super_bytes = std::max(1LL, std::atoll(e));
+    const uint64_t per_super = std::max<uint64_t>(1, super_bytes / std::max<uint64_t>(dst_stride, 1));
     const uint64_t nsuper = (n + per_super - 1) / per_super;
+    const uint64_t piece = std::max<uint64_t>(max_run, 16);  // blocks per work item
+    const uint64_t pps = (per_super + piece - 1) / piece;     // pieces per full super-chunk
+    auto pieces_in = [&](uint64_t sc) {
+        const uint64_t lo = sc * per_super, hi = std::min(n, lo + per_super);
+        return (hi - lo + piece - 1) / piece;
+    };
+    const uint64_t npieces = (nsuper - 1) * pps + pieces_in(nsuper - 1);
+    std::unique_ptr<std::atomic<uint64_t>[]> landed(new std::atomic<uint64_t>[nsuper]);
+    for (uint64_t sc = 0; sc < nsuper; ++sc) landed[sc].store(0);
+    std::atomic<uint64_t> next{0};
     std::atomic<int> err{0}, err_no{0};
     std::atomic<uint64_t> bad_index{n};
-    std::atomic<uint64_t> ready{0};  // super-chunks fully read
     std::atomic<bool> stop{false};
     std::mutex mu;
     std::condition_variable cv;
+    auto note_bad = [&](uint64_t idx) {  // the lowest failing index wins
+        uint64_t cur = bad_index.load();
+        while (idx < cur && !bad_index.compare_exchange_weak(cur, idx)) {
+        }
+    };
     auto read_range = [&](uint64_t lo, uint64_t hi) {
-        for (uint64_t i = lo; i < hi && !err.load(std::memory_order_relaxed);) {
+        for (uint64_t i = lo; i < hi;) {
             uint64_t k = i + 1;
             while (k < hi && k - i < max_run && addresses[k] == addresses[k - 1] + 1) ++k;
             uint8_t* d = static_cast<uint8_t*>(dst) + i * dst_stride;
@@ -966,44 +985,39 @@ int stormck_read_verify_fd(int fd, const uint64_t* addresses, const uint32_t* le
                 if (r <= 0) {
                     if (r < 0) err_no.store(errno);
                     err.store(r < 0 ? 1 : 2);
-                    bad_index.store(i + (full ? got / block_size : 0));
-                    return;
+                    note_bad(i + (full ? got / block_size : 0));
+                    return false;
                 }
                 got += static_cast<uint64_t>(r);
             }
             i = k;
         }
+        return true;
     };
-    std::thread reader([&] {
-        for (uint64_t s = 0; s < nsuper && !stop.load() && !err.load(); ++s) {
-            const uint64_t lo = s * per_super, hi = std::min(n, lo + per_super);
-            const unsigned k = static_cast<unsigned>(std::min<uint64_t>(nt, (hi - lo + 63) / 64));
-            if (k <= 1) {
-                read_range(lo, hi);
-            } else {
-                std::vector<std::thread> th;
-                for (unsigned t = 0; t < k; ++t)
-                    th.emplace_back(read_range, lo + (hi - lo) * t / k, lo + (hi - lo) * (t + 1) / k);
-                for (auto& x : th) x.join();
+    auto reader = [&] {
+        while (!stop.load(std::memory_order_relaxed) && !err.load(std::memory_order_relaxed)) {
+            const uint64_t p = next.fetch_add(1);
+            if (p >= npieces) return;
+            const uint64_t sc = p / pps, lo = sc * per_super + (p % pps) * piece;
+            const uint64_t hi = std::min({n, (sc + 1) * per_super, lo + piece});
+            const bool ok = read_range(lo, hi);
+            if (!ok || landed[sc].fetch_add(1) + 1 == pieces_in(sc)) {
+                std::lock_guard<std::mutex> g(mu);  // pairs with the verifier's predicate check
+                cv.notify_all();
             }
-            {
-                std::lock_guard<std::mutex> g(mu);
-                ready.store(s + 1);
-            }
-            cv.notify_all();
+            if (!ok) return;
         }
-        std::lock_guard<std::mutex> g(mu);
-        stop.store(true);
-        cv.notify_all();
-    });
+    };
+    std::vector<std::thread> pool;
+    for (unsigned t = 0; t < std::min<uint64_t>(nt, npieces); ++t) pool.emplace_back(reader);
     rc = STORMCK_OK;
-    for (uint64_t s = 0; s < nsuper; ++s) {
+    for (uint64_t sc = 0; sc < nsuper; ++sc) {
         {
             std::unique_lock<std::mutex> g(mu);
-            cv.wait(g, [&] { return ready.load() > s || stop.load() || err.load(); });
+            cv.wait(g, [&] { return landed[sc].load() == pieces_in(sc) || err.load(); });
         }
-        if (err.load() || ready.load() <= s) break;
-        const uint64_t lo = s * per_super, hi = std::min(n, lo + per_super);
+        if (err.load()) break;
+        const uint64_t lo = sc * per_super, hi = std::min(n, lo + per_super);
         uint64_t fb = 0, nb = 0;
         rc = host_pipeline(static_cast<uint8_t*>(dst) + lo * dst_stride, dst_stride, lens + lo, 0, hi - lo, nullptr,
                            expected + lo, &fb, &nb);
@@ -1014,7 +1028,7 @@ int stormck_read_verify_fd(int fd, const uint64_t* addresses, const uint32_t* le
         }
     }
     stop.store(true);
-    reader.join();
+    for (auto& t : pool) t.join();
     if (err.load()) {
         const std::string what = err.load() == 1 ? std::string("pread failed (") + std::strerror(err_no.load()) + ")"
                                                  : std::string("short read (block beyond end of device)");

@@ -255,6 +255,21 @@ static void host_pipeline_paths() {
     std::vector<uint8_t> slots(3000 * stride);
     CHECK(stormck_read_verify_fd(fd, addrs.data(), l2.data(), 3000, stride, slots.data(), stride, exp.data(), 0, &fb,
                                  &nb) == STORMCK_OK && nb == 0);
+    // many small super-chunks: the reader pool runs ahead of the verifier across them;
+    // then a mismatch and a read past the end of the file, both in a later super-chunk
+    setenv("STORMCK_READ_SUPER_BYTES", "200000", 1);
+    CHECK(stormck_read_verify_fd(fd, addrs.data(), l2.data(), 3000, stride, slots.data(), stride, exp.data(), 0, &fb,
+                                 &nb) == STORMCK_OK && nb == 0);
+    exp[2500] ^= 1;
+    CHECK(stormck_read_verify_fd(fd, addrs.data(), l2.data(), 3000, stride, slots.data(), stride, exp.data(), 0, &fb,
+                                 &nb) == STORMCK_EMISMATCH && fb == 2500 && nb == 1);
+    exp[2500] ^= 1;
+    addrs[2600] = 5000;  // beyond the 4096 blocks written
+    l2[2600] = 64;
+    CHECK(stormck_read_verify_fd(fd, addrs.data(), l2.data(), 3000, stride, slots.data(), stride, exp.data(), 0, &fb,
+                                 &nb) == STORMCK_EINVAL &&
+          std::string(stormck_last_error()).find("block index 2600") != std::string::npos);
+    unsetenv("STORMCK_READ_SUPER_BYTES");
     close(fd);
     unlink(path);
 }

@@ -3,8 +3,9 @@
 
 * f1: storm's Cache.Commit of 1M dirty 32 KiB leaves under fan-out-1200 pointer blocks
   (cache/cache.go:87-137) -- the commit's root, which covers every leaf and pointer;
-* c5 (BASELINE.json configs[4]): the mixed batch of one keystore commit -- every
-  checksum (digest) and the root of the same leaves committed as a forest;
+* c5 (BASELINE.json configs[4]): the mixed batch of one keystore commit, and of one
+  BenchmarkStorm commit (blob leaves, a spacelist block) -- every checksum (digest)
+  and the root of the same leaves committed as a forest;
 * f4: xxhash.Sum64 of 64M packed 48-byte keys (keystore/keystore.go:33,66) -- the
   digest of all tags.
 """
@@ -61,6 +62,30 @@ def test_c5_batch_and_commit(dev):
     torch.cuda.synchronize()
     assert _digest(out) == hx(fx["batch_digest"])
     b0, size, last = sc.pointer_forest(1200, 31808, 1200, slot=32768, revision=1)
+    arena = torch.zeros(size, dtype=torch.uint8, device=dev)
+    engine.fill_synthetic_device(arena.data_ptr() + 32768, 32768, 1200, 0, o.SYNTH_SEED)
+    torch.cuda.synchronize()
+    cs, _ = sc.commit_device(arena.data_ptr(), b0, 1, last)
+    assert int(cs[-1]) == hx(fx["commit_root"])
+    assert np.array_equal(cs[:1200], out[:1200].cpu().numpy().view(np.uint64))
+
+
+def test_c5_storm_mix_batch_and_commit(dev):
+    """c5, BenchmarkStorm's mix (/root/reference/benchmark_test.go): 1200 blob leaves of
+    32,768 B, a 28,808 B spacelist block, the pointer block and the singularity, as
+    bench.py --workload c5 --c5-mix storm runs it."""
+    from storm_amd import commit as sc
+    from storm_amd import engine
+    from oracle import oracle as o
+    fx = load_golden("c5.json")["storm"]
+    lens = np.array([32768] * 1200 + [28808, 30000, 72], dtype=np.uint32)
+    n = len(lens)
+    buf = torch.empty((n, 32768), dtype=torch.uint8, device=dev)
+    engine.fill_synthetic_device(buf.data_ptr(), 32768, n, 0, o.SYNTH_SEED)
+    out = engine.checksum_tensor(buf, lens=torch.from_numpy(lens.view(np.int32)).to(dev))
+    torch.cuda.synchronize()
+    assert _digest(out) == hx(fx["batch_digest"])
+    b0, size, last = sc.pointer_forest(1200, 32768, 1200, slot=32768, revision=1)
     arena = torch.zeros(size, dtype=torch.uint8, device=dev)
     engine.fill_synthetic_device(arena.data_ptr() + 32768, 32768, 1200, 0, o.SYNTH_SEED)
     torch.cuda.synchronize()

@@ -99,6 +99,15 @@ def test_c5_fixture_against_oracle():
     assert o.xxh64(cs.astype("<u8")) == hx(g["batch_digest"])
     leaf = [(int(cs[i]), 1 + i, 2, 2) for i in range(1200)]
     assert o.xxh64(o.pack_pointer_block_py(leaf, 1200)) == hx(g["commit_root"])
+    # the BenchmarkStorm mix: blob leaves and a spacelist block join the commit
+    gs = g["storm"]
+    lens = [32768] * 1200 + [28808, 30000, 72]
+    buf = o.fill_synthetic(len(lens), 32768, 0)
+    cs = o.checksum_batch(buf, len(lens), 32768, lens=lens, threads=8)
+    assert o.xxh64(cs.astype("<u8")) == hx(gs["batch_digest"])
+    assert [int(v) for v in cs[-3:]] == [hx(v) for v in gs["last3"]]
+    leaf = [(int(cs[i]), 1 + i, 2, 2) for i in range(1200)]
+    assert o.xxh64(o.pack_pointer_block_py(leaf, 1200)) == hx(gs["commit_root"])
 
 
 def test_keytags_fixture_samples_against_oracle():

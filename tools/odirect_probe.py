@@ -36,15 +36,19 @@ try:
     for name, addrs in (("random", np.random.default_rng(2).permutation(n).astype(np.uint64)),
                         ("in order", np.arange(n, dtype=np.uint64))):
         exp = cs[addrs.astype(np.int64)]
-        for threads in (16, 32, 64, 128):
-            os.environ["STORMCK_READ_THREADS"] = str(threads)
+        for threads in [int(t) for t in os.environ.get("ODIRECT_THREADS", "1,2,4,8,16,32,64").split(",")]:
+            if threads:
+                os.environ["STORMCK_READ_THREADS"] = str(threads)
+            else:  # 0: the library's own choice
+                os.environ.pop("STORMCK_READ_THREADS", None)
             best = 1e9
             for _ in range(2):
                 t0 = time.perf_counter()
                 r = blocks.ReadVerifyBatch(fd, addrs, lens, exp, host, BLOCK)
                 best = min(best, time.perf_counter() - t0)
                 assert r == (n, 0), r
-            print(f"O_DIRECT read+verify, {name:8s}, {threads:3d} readers: {n * BLOCK / best / 2**30:6.2f} GiB/s",
+            label = f"{threads:4d}" if threads else "auto"
+            print(f"O_DIRECT read+verify, {name:8s}, {label} readers: {n * BLOCK / best / 2**30:6.2f} GiB/s",
                   flush=True)
     blocks.UnregisterHostMemory(host)
 finally:
