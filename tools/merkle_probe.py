@@ -7,15 +7,19 @@ import sys
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from storm_amd import _lib  # noqa: E402
+
+if os.environ.get("MERKLE_PROBE_LIB"):  # A/B: a variant build of the library
+    _lib.LIB_PATH = os.path.abspath(os.environ["MERKLE_PROBE_LIB"])
 from storm_amd import engine  # noqa: E402
 
 dev = torch.device("cuda", 0)
 torch.cuda.set_device(dev)
 st = torch.cuda.current_stream(dev)
-kind = {"0": "register-quad", "1": "ring (1 wave)"}.get(os.environ.get("STORMCK_POINTER_RING", ""), "ring (wave pair)")
+kind = os.environ.get("MERKLE_PROBE_LIB", "") + " " + {"0": "register-quad", "1": "ring (1 wave)"}.get(os.environ.get("STORMCK_POINTER_RING", ""), "ring (wave pair)")
 cs = torch.randint(-2**62, 2**62, (16 << 20,), dtype=torch.int64, device=dev)
 par = torch.empty(16384, dtype=torch.int64, device=dev)
-for m in (16 << 20, 8 << 20, 1 << 20, 300 * 1200):
+for m in (16 << 20, 8 << 20, 1 << 20, 300 * 1200, 12 * 1200, 1200):
     for _ in range(20):
         engine.pointer_level_device(cs.data_ptr(), m, 0, 1, 2, 1200, par.data_ptr(), st.cuda_stream)
     ts = []
