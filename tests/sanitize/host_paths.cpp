@@ -12,19 +12,22 @@
 //   * with a gfx950 device (GPU box): the same commits run to completion on a device
 //     arena and are compared with the oracle's serial commit; the host pipeline
 //     (pageable and registered sources, parallel staging copies, both stages), the
-//     batched verify and the file read-verify reader threads.
+//     batched verify and the file read-verify reader threads, and four host threads
+//     calling the library at once.
 // Exit status 0 = every check passed and the sanitizer reported nothing (sanitizer
 // reports abort the process: halt_on_error / -fno-sanitize-recover).
 #include <fcntl.h>
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <numeric>
 #include <random>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include <hip/hip_runtime_api.h>
@@ -37,7 +40,7 @@ int oracle_commit(uint8_t* arena, stormck_dirty_block* blocks, size_t n, uint64_
                   uint64_t* out_cs);
 }
 
-static int g_fail = 0;
+static std::atomic<int> g_fail{0};
 #define CHECK(cond)                                                                                  \
     do {                                                                                             \
         if (!(cond)) {                                                                               \
@@ -274,6 +277,61 @@ static void host_pipeline_paths() {
     unlink(path);
 }
 
+// Several host threads on one device at once, as cgo callers on many goroutines would
+// be (stormck.h: the library is safe for concurrent callers; host pipelines sharing a
+// device are serialised inside). Each thread hashes and verifies its own batch, makes
+// single calls on both legs, and provokes an error whose thread-local message must be
+// its own.
+static void concurrent_callers() {
+    constexpr int kThreads = 4;
+    constexpr uint64_t n = 600, stride = 32768;
+    std::vector<std::vector<uint8_t>> bufs(kThreads);
+    std::vector<std::vector<uint32_t>> lens(kThreads);
+    std::vector<std::vector<uint64_t>> want(kThreads);
+    for (int t = 0; t < kThreads; ++t) {
+        std::mt19937_64 rng(100 + t);
+        bufs[t].resize(n * stride);
+        for (size_t i = 0; i < bufs[t].size(); i += 8) bufs[t][i] = static_cast<uint8_t>(rng());
+        lens[t].resize(n);
+        for (auto& l : lens[t]) l = static_cast<uint32_t>(rng() % (stride + 1));
+        want[t].resize(n);
+        for (uint64_t i = 0; i < n; ++i) want[t][i] = oracle_xxh64(bufs[t].data() + i * stride, lens[t][i]);
+    }
+    const int devnull = open("/dev/null", O_RDONLY);
+    CHECK(devnull >= 0);
+    std::vector<std::thread> th;
+    for (int t = 0; t < kThreads; ++t)
+        th.emplace_back([&, t] {
+            CHECK(stormck_init(0) == STORMCK_OK);
+            const uint8_t* b = bufs[t].data();
+            std::vector<uint64_t> got(n), bad = want[t];
+            bad[(t + 1) * 100] ^= 1;
+            for (int it = 0; it < 5; ++it) {
+                std::fill(got.begin(), got.end(), 0);
+                CHECK(stormck_checksum_host(b, stride, lens[t].data(), 0, n, got.data()) == STORMCK_OK &&
+                      got == want[t]);
+                uint64_t fb = 0, nb = 0;
+                CHECK(stormck_verify_host(b, stride, lens[t].data(), 0, n, bad.data(), &fb, &nb) == STORMCK_EMISMATCH &&
+                      fb == static_cast<uint64_t>((t + 1) * 100) && nb == 1);
+                uint64_t one = 0;
+                CHECK(stormck_checksum_gpu(b + 8 * t, 5000 + t, &one) == STORMCK_OK &&
+                      one == oracle_xxh64(b + 8 * t, 5000 + t));
+                CHECK(stormck_xxh64(b + it * stride, lens[t][it]) == want[t][it]);
+                // an argument error naming this thread's own block index
+                std::vector<uint64_t> addr(t + 1, 0), exp(t + 1, 0);
+                std::vector<uint32_t> l(t + 1, 64);
+                addr[t] = UINT64_MAX;
+                std::vector<uint8_t> slots((t + 1) * 64);
+                CHECK(stormck_read_verify_fd(devnull, addr.data(), l.data(), t + 1, 32768, slots.data(), 64, exp.data(),
+                                             0, &fb, &nb) == STORMCK_EINVAL &&
+                      std::string(stormck_last_error()).find("of block index " + std::to_string(t) + " ") !=
+                          std::string::npos);
+            }
+        });
+    for (auto& x : th) x.join();
+    close(devnull);
+}
+
 int main() {
     std::setvbuf(stdout, nullptr, _IONBF, 0);  // progress lines reach a log file at once
     single_calls();
@@ -285,7 +343,9 @@ int main() {
     commit_planning(device);
     std::printf("commit planning: done\n");
     if (device) host_pipeline_paths();
+    if (device) concurrent_callers();
+    if (device) std::printf("concurrent callers: done\n");
     stormck_shutdown();
-    std::printf("%s: %d failure(s)\n", g_fail ? "FAILED" : "ok", g_fail);
+    std::printf("%s: %d failure(s)\n", g_fail.load() ? "FAILED" : "ok", g_fail.load());
     return g_fail ? 1 : 0;
 }
