@@ -125,6 +125,99 @@ __global__ __launch_bounds__(64 * WAVES) void k_xxh64_glds_rs(const uint8_t* __r
         }
     }
 }
+// Per-block phases (round 2, placement): every block of a wave also starts E(b) tiles
+// late, E(b) in [0, 8), on top of the wave's 8-tile skew, so the 128 blocks of a
+// workgroup read 64 different 512 B rows at any moment and concurrent addresses differ
+// in bits 9..14 too, not only in the bits the page mapping decides. Addresses are
+// computed per step from (step - phase): no per-lane counters. MODE 1: E = b mod 8
+// (the two blocks of one DMA instruction differ); MODE 2: E = (b mod 16) / 2 (they
+// share a phase).
+template <int MODE>
+__global__ __launch_bounds__(512) void k_xxh64_glds_qs(const uint8_t* __restrict__ base, uint64_t stride,
+                                                       uint32_t len, uint64_t n, uint64_t* __restrict__ out) {
+    constexpr int T = 16, WAVES = 8, BPW = 128, ROW = 32 * T, TILE = BPW * ROW, PER_WAVE = TILE / 1024 / WAVES;
+    constexpr int SKEW = 8;
+    __shared__ __attribute__((aligned(16))) uint8_t lds[2 * TILE];
+    const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const uint64_t ngroups = (n + BPW - 1) / BPW, G = gridDim.x;
+    if (blockIdx.x >= ngroups) return;
+    const uint32_t nst = len >> 5;
+    constexpr uint32_t NT = 64;  // 32 KiB blocks only (probe): divisions by NT are shifts
+    if (nst / T != NT) return;
+    const int64_t tiles = static_cast<int64_t>((ngroups - blockIdx.x + G - 1) / G) * NT;  // per block
+    auto phase = [&](uint32_t b) -> int64_t {
+        const uint32_t e = MODE == 1 ? (b % 8) : ((b % 16) / 2);
+        return static_cast<int64_t>((b / 16) * SKEW + e);
+    };
+    const int64_t steps = tiles + 7 * SKEW + 7;
+    uint32_t prow[PER_WAVE], pofs[PER_WAVE];
+    int64_t pph[PER_WAVE];
+#pragma unroll
+    for (int k = 0; k < PER_WAVE; ++k) {
+        const uint32_t off = (wave * PER_WAVE + k) * 1024 + lane * 16;
+        const uint32_t b = off / ROW, q = (off % ROW) / 16;
+        prow[k] = b;
+        pofs[k] = ((q + glds_rot<T>(b)) % (2 * T)) * 16;
+        pph[k] = phase(b);
+    }
+    // per piece: the source of its next row, advanced one row per issue and moved to
+    // the block's next group after its last row (no per-step address arithmetic)
+    const uint8_t* src[PER_WAVE];
+    uint64_t gbk[PER_WAVE];
+#pragma unroll
+    for (int k = 0; k < PER_WAVE; ++k) {
+        gbk[k] = blockIdx.x * BPW + prow[k];
+        src[k] = base + (gbk[k] < n ? gbk[k] : n - 1) * stride + pofs[k];
+    }
+    auto issue = [&](int64_t v) {  // the pieces of virtual step v into slot v & 1
+        uint8_t* dst = lds + (v & 1) * TILE + wave * PER_WAVE * 1024;
+#pragma unroll
+        for (int k = 0; k < PER_WAVE; ++k) {
+            const int64_t r = v - pph[k];
+            if (r >= 0 && r < tiles) {
+                __builtin_amdgcn_global_load_lds(src[k], dst + k * 1024, 16, 0, 2);
+                if ((r & (NT - 1)) == NT - 1) {
+                    gbk[k] += G * BPW;
+                    src[k] = base + (gbk[k] < n ? gbk[k] : n - 1) * stride + pofs[k];
+                } else {
+                    src[k] += ROW;
+                }
+            }
+        }
+    };
+    const uint32_t b = tid >> 2, j = tid & 3;
+    const uint32_t rot = glds_rot<T>(b);
+    const int64_t ph = phase(b);
+    uint64_t acc = acc_seed(j);
+    issue(0);
+    for (int64_t u = 0; u < steps; ++u) {
+        wait_vmcnt<0>();
+        __builtin_amdgcn_s_barrier();
+        if (u + 1 < steps) issue(u + 1);
+        const int64_t r = u - ph;
+        if (r >= 0 && r < tiles) {
+            const uint8_t* row = lds + (u & 1) * TILE + b * ROW + (j & 1) * 8;
+#pragma unroll
+            for (int s = 0; s < T; ++s) {
+                const uint32_t q = (2 * s + (j >> 1) + 2 * T - rot) % (2 * T);
+                acc = round(acc, *reinterpret_cast<const uint64_t*>(row + q * 16));
+            }
+            if (static_cast<uint64_t>(r) % NT == NT - 1) {
+                const uint64_t grp = static_cast<uint64_t>(r) / NT;
+                const uint64_t gbk = (blockIdx.x + grp * G) * BPW + b;
+                const uint64_t gb = gbk < n ? gbk : n - 1;
+                const uint8_t* blk_src = base + gb * stride;
+                for (uint32_t s = NT * T; s < nst; ++s) acc = round(acc, reinterpret_cast<const uint64_t*>(blk_src)[4 * s + j]);
+                const uint64_t v1 = quad_bcast<0>(acc), v2 = quad_bcast<1>(acc), v3 = quad_bcast<2>(acc),
+                               v4 = quad_bcast<3>(acc);
+                if (j == 0 && gbk < n)
+                    out[gbk] = finish_fast(converge(v1, v2, v3, v4), len, blk_src + 32 * static_cast<uint64_t>(nst),
+                                           len & 31);
+                acc = acc_seed(j);
+            }
+        }
+    }
+}
 }  // namespace stormck
 
 using namespace stormck;
@@ -157,9 +250,8 @@ int main(int argc, char** argv) {
     const dim3 g(cus), blk(512);
     std::vector<V> vs = {
         {"shipped skew 8w T=16 R=2", [&](uint8_t* d, uint64_t* o) { hipLaunchKernelGGL((k_xxh64_glds_skew<16, 2, false, 8, 8, true>), g, blk, 0, 0, d, L, (uint32_t)L, n, o, nullptr, nullptr, nullptr); }},
-        {"blocks v+8k, phases 3v", [&](uint8_t* d, uint64_t* o) { hipLaunchKernelGGL((k_xxh64_glds_rs<16, 2, 8, 8, 1, 3>), g, blk, 0, 0, d, L, (uint32_t)L, n, o); }},
-        {"blocks v+8k, phases 5v", [&](uint8_t* d, uint64_t* o) { hipLaunchKernelGGL((k_xxh64_glds_rs<16, 2, 8, 8, 1, 5>), g, blk, 0, 0, d, L, (uint32_t)L, n, o); }},
-        {"blocks v+8k, phases 7v", [&](uint8_t* d, uint64_t* o) { hipLaunchKernelGGL((k_xxh64_glds_rs<16, 2, 8, 8, 1, 7>), g, blk, 0, 0, d, L, (uint32_t)L, n, o); }},
+        {"block phases b mod 8", [&](uint8_t* d, uint64_t* o) { hipLaunchKernelGGL((k_xxh64_glds_qs<1>), g, blk, 0, 0, d, L, (uint32_t)L, n, o); }},
+        {"block phases (b mod 16)/2", [&](uint8_t* d, uint64_t* o) { hipLaunchKernelGGL((k_xxh64_glds_qs<2>), g, blk, 0, 0, d, L, (uint32_t)L, n, o); }},
         {"shipped again", [&](uint8_t* d, uint64_t* o) { hipLaunchKernelGGL((k_xxh64_glds_skew<16, 2, false, 8, 8, true>), g, blk, 0, 0, d, L, (uint32_t)L, n, o, nullptr, nullptr, nullptr); }},
     };
     std::vector<std::vector<float>> ms(vs.size() * 2);
