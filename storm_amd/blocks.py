@@ -165,6 +165,8 @@ def ReadVerifyBatch(fd: int, addresses, lens, expected, dst, dst_stride: int, bl
     ad = np.ascontiguousarray(np.asarray(addresses, dtype=np.uint64))
     la = np.ascontiguousarray(np.asarray(lens, dtype=np.uint32))
     ex = np.ascontiguousarray(np.asarray(expected, dtype=np.uint64))
+    if isinstance(dst, np.ndarray) and not dst.flags.c_contiguous:
+        raise ValueError("dst must be C-contiguous (a strided view would be read into a temporary copy)")
     d = _as_u8(dst)
     if not d.flags.writeable:
         raise ValueError("dst must be writable (the blocks are read into it)")
