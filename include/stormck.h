@@ -101,6 +101,20 @@ int stormck_checksum_host(const void* base, uint64_t stride, const uint32_t* len
  * *n_bad = mismatch count. Returns STORMCK_EMISMATCH if n_bad > 0. */
 int stormck_verify_host(const void* base, uint64_t stride, const uint32_t* lens, uint32_t len, uint64_t n,
                         const uint64_t* expected, uint64_t* first_bad, uint64_t* n_bad);
+/* The same two calls spread over several devices from one process (storm is one Go
+ * process; each device has its own PCIe link): the n blocks split into n_devices
+ * contiguous ranges whose sizes differ by at most one, and range k runs on
+ * devices[k] in its own host thread. Results are as from the single-device calls
+ * (first_bad is the lowest mismatching index of the whole batch, n_bad the total).
+ * A device may be listed more than once; its ranges then run one after another.
+ * Memory registered with stormck_host_register is pinned for every device. The
+ * calling thread's current device is left as it was. On failure the message names
+ * the device and block range of the lowest failing range. */
+int stormck_checksum_host_multi(const void* base, uint64_t stride, const uint32_t* lens, uint32_t len, uint64_t n,
+                                uint64_t* out, const int* devices, int n_devices);
+int stormck_verify_host_multi(const void* base, uint64_t stride, const uint32_t* lens, uint32_t len, uint64_t n,
+                              const uint64_t* expected, uint64_t* first_bad, uint64_t* n_bad, const int* devices,
+                              int n_devices);
 /* ---- single calls (Go blocks.Checksum / BlockChecksum / VerifyChecksum, one block)
  * stormck_xxh64: XXH64 seed 0 of p[0..n_bytes) on the calling host thread; cannot
  * fail (p may be NULL only when n_bytes == 0). What the Go shim's Checksum calls.

@@ -85,6 +85,25 @@ func ChecksumBatch(data []byte, n, stride, length int, out []Hash) error {
 	return nil
 }
 
+// ChecksumBatchDevices is ChecksumBatch spread over several GPUs of this process
+// (stormck_checksum_host_multi): contiguous ranges, one per entry of devices, each
+// over its own device's PCIe link. storm is one process, so this is how one commit
+// batch uses every GPU of a node.
+func ChecksumBatchDevices(data []byte, n, stride, length int, out []Hash, devices []int32) error {
+	if n == 0 {
+		return nil
+	}
+	if len(out) < n || len(data) < (n-1)*stride+length || len(devices) == 0 {
+		return errors.New("ChecksumBatchDevices: argument sizes")
+	}
+	rc := C.stormck_checksum_host_multi(bytesPtr(data), C.uint64_t(stride), nil, C.uint32_t(length), C.uint64_t(n),
+		(*C.uint64_t)(unsafe.Pointer(&out[0])), (*C.int)(unsafe.Pointer(&devices[0])), C.int(len(devices)))
+	if rc != C.STORMCK_OK {
+		return stormckError(rc)
+	}
+	return nil
+}
+
 // VerifyChecksumBatch verifies n blocks; it returns the first mismatching index
 // (n when all match) and the number of mismatches.
 func VerifyChecksumBatch(data []byte, n, stride, length int, expected []Hash) (firstBad, nBad int, err error) {

@@ -51,6 +51,10 @@ SIGNATURES = {
     "stormck_verify_device": (c_int, [c_void_p, c_uint64, c_void_p, c_uint32, c_uint64, c_void_p, c_void_p, c_void_p]),
     "stormck_checksum_host": (c_int, [c_void_p, c_uint64, c_void_p, c_uint32, c_uint64, c_void_p]),
     "stormck_verify_host": (c_int, [c_void_p, c_uint64, c_void_p, c_uint32, c_uint64, c_void_p, c_void_p, c_void_p]),
+    "stormck_checksum_host_multi": (
+        c_int, [c_void_p, c_uint64, c_void_p, c_uint32, c_uint64, c_void_p, c_void_p, c_int]),
+    "stormck_verify_host_multi": (
+        c_int, [c_void_p, c_uint64, c_void_p, c_uint32, c_uint64, c_void_p, c_void_p, c_void_p, c_void_p, c_int]),
     "stormck_xxh64": (c_uint64, [c_void_p, c_uint64]),
     "stormck_checksum": (c_int, [c_void_p, c_uint64, POINTER(c_uint64)]),
     "stormck_checksum_gpu": (c_int, [c_void_p, c_uint64, POINTER(c_uint64)]),

@@ -118,10 +118,19 @@ def _lens_arg(n: int, length: Optional[int], lens: Optional[Sequence[int]]):
     return None, int(length)
 
 
+def _devices_arg(devices: Optional[Sequence[int]]):
+    if devices is None:
+        return None
+    d = (ctypes.c_int * len(devices))(*[int(x) for x in devices])
+    return d
+
+
 def ChecksumBatch(buf, n: int, stride: int, length: Optional[int] = None,
-                  lens: Optional[Sequence[int]] = None) -> np.ndarray:
+                  lens: Optional[Sequence[int]] = None, devices: Optional[Sequence[int]] = None) -> np.ndarray:
     """Checksums of ``n`` host blocks at ``buf + i*stride`` (``length`` bytes each or
-    ``lens[i]``). H2D -> gfx950 kernel -> D2H. Returns uint64[n]."""
+    ``lens[i]``). H2D -> gfx950 kernel -> D2H. Returns uint64[n]. ``devices``: spread
+    the batch over these devices in contiguous ranges, one host thread each
+    (stormck_checksum_host_multi); default: the current device."""
     a = _as_u8(buf)
     la, ln = _lens_arg(n, length, lens)
     if n and a.size < (n - 1) * stride + (int(la.max()) if la is not None else ln):
@@ -129,14 +138,20 @@ def ChecksumBatch(buf, n: int, stride: int, length: Optional[int] = None,
     out = np.zeros(n, dtype=np.uint64)
     if n == 0:
         return out
-    _lib.check(_lib.lib.stormck_checksum_host(a.ctypes.data, stride, la.ctypes.data if la is not None else None, ln, n,
-                                              out.ctypes.data))
+    lp = la.ctypes.data if la is not None else None
+    d = _devices_arg(devices)
+    if d is None:
+        _lib.check(_lib.lib.stormck_checksum_host(a.ctypes.data, stride, lp, ln, n, out.ctypes.data))
+    else:
+        _lib.check(_lib.lib.stormck_checksum_host_multi(a.ctypes.data, stride, lp, ln, n, out.ctypes.data, d, len(d)))
     return out
 
 
 def VerifyChecksumBatch(buf, n: int, stride: int, expected: Sequence[int], length: Optional[int] = None,
-                        lens: Optional[Sequence[int]] = None) -> Tuple[int, int]:
-    """Batched VerifyChecksum. Returns (first_bad, n_bad); first_bad == n when all match."""
+                        lens: Optional[Sequence[int]] = None,
+                        devices: Optional[Sequence[int]] = None) -> Tuple[int, int]:
+    """Batched VerifyChecksum. Returns (first_bad, n_bad); first_bad == n when all match.
+    ``devices`` as in ChecksumBatch."""
     a = _as_u8(buf)
     la, ln = _lens_arg(n, length, lens)
     exp = np.ascontiguousarray(np.asarray(expected, dtype=np.uint64))
@@ -145,8 +160,14 @@ def VerifyChecksumBatch(buf, n: int, stride: int, expected: Sequence[int], lengt
     if n == 0:
         return 0, 0
     fb, nb = ctypes.c_uint64(0), ctypes.c_uint64(0)
-    rc = _lib.lib.stormck_verify_host(a.ctypes.data, stride, la.ctypes.data if la is not None else None, ln, n,
-                                      exp.ctypes.data, ctypes.byref(fb), ctypes.byref(nb))
+    lp = la.ctypes.data if la is not None else None
+    d = _devices_arg(devices)
+    if d is None:
+        rc = _lib.lib.stormck_verify_host(a.ctypes.data, stride, lp, ln, n, exp.ctypes.data, ctypes.byref(fb),
+                                          ctypes.byref(nb))
+    else:
+        rc = _lib.lib.stormck_verify_host_multi(a.ctypes.data, stride, lp, ln, n, exp.ctypes.data, ctypes.byref(fb),
+                                                ctypes.byref(nb), d, len(d))
     if rc != _lib.EMISMATCH:
         _lib.check(rc)
     return fb.value, nb.value

@@ -603,6 +603,97 @@ int host_pipeline(const void* base, uint64_t stride, const uint32_t* lens, uint3
     return STORMCK_OK;
 }
 
+// One host batch over several devices from one process (storm is one Go process): the
+// blocks split into contiguous ranges whose sizes differ by at most one (as the ranks of
+// storm_amd/dist.py shard_range), and range k runs host_pipeline on devices[k] in its
+// own host thread, so each device's PCIe link carries its own range. A device may be
+// listed more than once; its ranges then share its staging (per-device mutex) and run
+// one after another. Returns the failing status of the lowest-numbered range, with its
+// message, or STORMCK_OK.
+int host_pipeline_multi(const void* base, uint64_t stride, const uint32_t* lens, uint32_t len, uint64_t n,
+                        uint64_t* out, const uint64_t* expected, uint64_t* first_bad, uint64_t* n_bad,
+                        const int* devices, int n_devices) {
+    if (!devices || n_devices <= 0 || n_devices > 64) return fail(STORMCK_EINVAL, "devices: 1..64 entries");
+    if (n == 0) {
+        if (first_bad) *first_bad = 0;
+        if (n_bad) *n_bad = 0;
+        return STORMCK_OK;
+    }
+    int rc = device_check();
+    if (rc) return rc;
+    int count = 0;
+    HIP_TRY(hipGetDeviceCount(&count));
+    for (int k = 0; k < n_devices; ++k) {
+        if (devices[k] < 0 || devices[k] >= count)
+            return fail(STORMCK_EINVAL, "devices[" + std::to_string(k) + "] = " + std::to_string(devices[k]) +
+                                            " is not a visible device");
+        hipDeviceProp_t prop;
+        HIP_TRY(hipGetDeviceProperties(&prop, devices[k]));
+        if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+            return fail(STORMCK_ENODEV, "devices[" + std::to_string(k) + "] is not gfx950: " + prop.gcnArchName);
+    }
+    const uint64_t parts = std::min<uint64_t>(static_cast<uint64_t>(n_devices), std::max<uint64_t>(n, 1));
+    if (parts == 1 || n <= 1) {
+        int prev = 0;
+        HIP_TRY(hipGetDevice(&prev));
+        HIP_TRY(hipSetDevice(devices[0]));
+        rc = host_pipeline(base, stride, lens, len, n, out, expected, first_bad, n_bad);
+        const std::string msg = g_last_error;
+        (void)hipSetDevice(prev);
+        g_last_error = msg;
+        return rc;
+    }
+    if (!base) return fail(STORMCK_EINVAL, "base is null");
+    struct Part {
+        uint64_t lo = 0, hi = 0, fb = 0, nb = 0;
+        int rc = STORMCK_OK;
+        std::string err;
+    };
+    std::vector<Part> part(parts);
+    const uint64_t q = n / parts, r = n % parts;
+    for (uint64_t k = 0; k < parts; ++k) {
+        part[k].lo = k * q + std::min(k, r);
+        part[k].hi = part[k].lo + q + (k < r ? 1 : 0);
+    }
+    const uint8_t* b8 = static_cast<const uint8_t*>(base);
+    auto work = [&](uint64_t k) {
+        Part& P = part[k];
+        if (hipSetDevice(devices[k]) != hipSuccess) {
+            P.rc = STORMCK_EHIP;
+            P.err = "hipSetDevice failed";
+            return;
+        }
+        const uint64_t cnt = P.hi - P.lo;
+        P.rc = host_pipeline(b8 + P.lo * stride, stride, lens ? lens + P.lo : nullptr, len, cnt,
+                             out ? out + P.lo : nullptr, expected ? expected + P.lo : nullptr, &P.fb, &P.nb);
+        if (P.rc) P.err = g_last_error;  // this worker thread's message
+    };
+    std::vector<std::thread> threads;
+    threads.reserve(parts - 1);
+    for (uint64_t k = 1; k < parts; ++k) threads.emplace_back(work, k);
+    {
+        // range 0 on the calling thread, which keeps its own current device
+        int prev = 0;
+        HIP_TRY(hipGetDevice(&prev));
+        work(0);
+        (void)hipSetDevice(prev);
+    }
+    for (std::thread& t : threads) t.join();
+    uint64_t fb = n, nb = 0;
+    for (uint64_t k = 0; k < parts; ++k) {
+        const Part& P = part[k];
+        if (P.rc) return fail(P.rc, "device " + std::to_string(devices[k]) + " (blocks " + std::to_string(P.lo) +
+                                        ".." + std::to_string(P.hi) + "): " + P.err);
+        if (expected && P.nb) {
+            nb += P.nb;
+            fb = std::min(fb, P.lo + P.fb);
+        }
+    }
+    if (first_bad) *first_bad = fb;
+    if (n_bad) *n_bad = nb;
+    return STORMCK_OK;
+}
+
 }  // namespace
 
 // ============================================================================
@@ -705,6 +796,25 @@ int stormck_verify_host(const void* base, uint64_t stride, const uint32_t* lens,
     return STORMCK_OK;
 }
 
+int stormck_checksum_host_multi(const void* base, uint64_t stride, const uint32_t* lens, uint32_t len, uint64_t n,
+                                uint64_t* out, const int* devices, int n_devices) {
+    if (n > 0 && !out) return fail(STORMCK_EINVAL, "out is null");
+    return host_pipeline_multi(base, stride, lens, len, n, out, nullptr, nullptr, nullptr, devices, n_devices);
+}
+
+int stormck_verify_host_multi(const void* base, uint64_t stride, const uint32_t* lens, uint32_t len, uint64_t n,
+                              const uint64_t* expected, uint64_t* first_bad, uint64_t* n_bad, const int* devices,
+                              int n_devices) {
+    if (!expected || !first_bad || !n_bad) return fail(STORMCK_EINVAL, "null argument");
+    int rc = host_pipeline_multi(base, stride, lens, len, n, nullptr, expected, first_bad, n_bad, devices, n_devices);
+    if (rc) return rc;
+    if (*n_bad > 0) {
+        g_last_error = "checksum mismatch";
+        return STORMCK_EMISMATCH;
+    }
+    return STORMCK_OK;
+}
+
 uint64_t stormck_xxh64(const void* p, uint64_t n_bytes) {
     static const uint8_t empty = 0;
     return host::xxh64(n_bytes ? p : &empty, n_bytes);
@@ -760,7 +870,9 @@ int stormck_host_register(void* p, uint64_t bytes) {
     if (!p || bytes == 0) return fail(STORMCK_EINVAL, "empty range");
     int rc = device_check();
     if (rc) return rc;
-    HIP_TRY(hipHostRegister(p, bytes, hipHostRegisterMapped));
+    // portable: pinned for every device of the process (stormck_checksum_host_multi DMAs
+    // ranges of one registered buffer to several devices)
+    HIP_TRY(hipHostRegister(p, bytes, hipHostRegisterMapped | hipHostRegisterPortable));
     return STORMCK_OK;
 }
 

@@ -88,6 +88,7 @@ static void argument_errors() {
     CHECK(stormck_host_device_pointer(nullptr, nullptr) == STORMCK_EINVAL);
     CHECK(stormck_key_tags_device(nullptr, 48, nullptr, nullptr, 48, 10, &out, nullptr) == STORMCK_EINVAL);
     CHECK(stormck_checksum_host(nullptr, 32, nullptr, 32, 4, &out) == STORMCK_EINVAL);
+    CHECK(stormck_checksum_host_multi(small, 32, nullptr, 32, 2, &out, nullptr, 0) == STORMCK_EINVAL);
     const uint64_t addr_big[1] = {1ULL << 60}, addr0[1] = {0};
     const uint32_t len100[1] = {100};
     const uint64_t exp0[1] = {0};
@@ -240,6 +241,17 @@ static void host_pipeline_paths() {
     CHECK(stormck_host_register(buf.data(), buf.size()) == STORMCK_OK);
     std::fill(got.begin(), got.end(), 0);
     CHECK(stormck_checksum_host(buf.data(), stride, lens.data(), 0, n, got.data()) == STORMCK_OK && got == want);
+    // one batch over several devices from one process (worker thread per listed device;
+    // the box has one GPU, so device 0 is listed three times): ranges, offsets, merge
+    const int devs[3] = {0, 0, 0};
+    std::fill(got.begin(), got.end(), 0);
+    CHECK(stormck_checksum_host_multi(buf.data(), stride, lens.data(), 0, n, got.data(), devs, 3) == STORMCK_OK &&
+          got == want);
+    bad[11111] ^= 1;
+    CHECK(stormck_verify_host_multi(buf.data(), stride, lens.data(), 0, n, bad.data(), &fb, &nb, devs, 3) ==
+              STORMCK_EMISMATCH &&
+          fb == 7777 && nb == 2);
+    bad[11111] ^= 1;
     CHECK(stormck_host_unregister(buf.data()) == STORMCK_OK);
     uint64_t one = 0;
     CHECK(stormck_checksum_gpu(buf.data() + 3, 70000, &one) == STORMCK_OK && one == oracle_xxh64(buf.data() + 3, 70000));

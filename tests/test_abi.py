@@ -75,6 +75,8 @@ def test_no_device_fails_loudly():
         blocks.VerifyChecksumBatch(bytes(64), 2, 32, [0, 0], 32)
     with pytest.raises(_lib.NoDeviceError):
         engine.checksum_device(1 << 20, 32, 1, 1 << 21, 32)
+    with pytest.raises(_lib.NoDeviceError):
+        blocks.ChecksumBatch(bytes(64), 2, 32, 32, devices=[0, 0])
     assert "no HIP device" in _lib.last_error() or "gfx950" in _lib.last_error()
 
 
@@ -107,6 +109,12 @@ def test_argument_errors_precede_the_device_check():
         ("device pointer null", lambda: L.stormck_host_device_pointer(None, None)),
         ("key tags null", lambda: L.stormck_key_tags_device(None, 48, None, None, 48, 10, 1 << 20, None)),
         ("host null base", lambda: L.stormck_checksum_host(None, 32, None, 32, 4, ctypes.addressof(out))),
+        ("multi no devices", lambda: L.stormck_checksum_host_multi(1 << 20, 32, None, 32, 4, ctypes.addressof(out),
+                                                                   None, 0)),
+        ("multi null out", lambda: L.stormck_checksum_host_multi(1 << 20, 32, None, 32, 4, None,
+                                                                 (ctypes.c_int * 1)(0), 1)),
+        ("verify multi null", lambda: L.stormck_verify_host_multi(1 << 20, 32, None, 32, 4, None, None, None,
+                                                                  (ctypes.c_int * 1)(0), 1)),
         ("read-verify slot", lambda: L.stormck_read_verify_fd(0, (ctypes.c_uint64 * 1)(0), (ctypes.c_uint32 * 1)(100),
                                                               1, 32768, (ctypes.c_uint8 * 64)(), 64,
                                                               (ctypes.c_uint64 * 1)(0), 1, ctypes.byref(out),
