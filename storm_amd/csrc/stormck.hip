@@ -12,6 +12,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <system_error>
 #include <functional>
 #include <thread>
 #include <vector>
@@ -668,16 +669,19 @@ int host_pipeline_multi(const void* base, uint64_t stride, const uint32_t* lens,
                              out ? out + P.lo : nullptr, expected ? expected + P.lo : nullptr, &P.fb, &P.nb);
         if (P.rc) P.err = g_last_error;  // this worker thread's message
     };
+    int prev = 0;  // the calling thread runs range 0 and then gets its own device back
+    HIP_TRY(hipGetDevice(&prev));
     std::vector<std::thread> threads;
     threads.reserve(parts - 1);
-    for (uint64_t k = 1; k < parts; ++k) threads.emplace_back(work, k);
-    {
-        // range 0 on the calling thread, which keeps its own current device
-        int prev = 0;
-        HIP_TRY(hipGetDevice(&prev));
-        work(0);
-        (void)hipSetDevice(prev);
+    uint64_t spawned = 1;
+    try {
+        for (; spawned < parts; ++spawned) threads.emplace_back(work, spawned);
+    } catch (const std::system_error&) {
+        // no more threads: the calling thread runs the ranges that have none
     }
+    for (uint64_t k = 0; k < parts; ++k)
+        if (k == 0 || k >= spawned) work(k);
+    (void)hipSetDevice(prev);
     for (std::thread& t : threads) t.join();
     uint64_t fb = n, nb = 0;
     for (uint64_t k = 0; k < parts; ++k) {
