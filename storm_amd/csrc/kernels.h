@@ -399,43 +399,42 @@ __global__ __launch_bounds__(256) void k_xxh64_wide(const uint8_t* __restrict__ 
 // walk block b's chain. The chain wave is issue-bound, so BPW blocks cost about what
 // one costs; at BPW = 5 a storm commit batch (~1,200 blocks) is one workgroup per CU.
 // Blocks that cannot be staged (other starts, larger covers) hash from memory in the
-// same lanes.
+// same lanes. multi_stage_hash is the body; k_xxh64_wide_multi (batches) and
+// k_commit_level_multi (f1 levels) differ only in where a block is and what happens to
+// its checksum.
 // ---------------------------------------------------------------------------
-template <bool LENS, bool OFFS, bool VERIFY, int BPW>
-__global__ __launch_bounds__(256) void k_xxh64_wide_multi(const uint8_t* __restrict__ base, uint64_t stride,
-                                                            const uint32_t* __restrict__ lens, uint32_t len,
-                                                            const uint64_t* __restrict__ offs, uint64_t n,
-                                                            uint64_t* __restrict__ out,
-                                                            const uint64_t* __restrict__ expected,
-                                                            unsigned long long* __restrict__ first_bad,
-                                                            unsigned long long* __restrict__ n_bad) {
-    // Block slots are kPieces 16-byte pieces apart: 2034 = 2 (mod 16), so slot b starts
-    // 32 * b bytes into the 256-byte bank period and the chain's ds_read_b64 of the BPW
-    // blocks (4 lanes x 8 B each) hit distinct banks (a 32 KiB stride would put them all
-    // on the same 8 banks). 5 slots of 32,544 B fit the CU's 160 KiB.
-    constexpr uint32_t kPieces = 2034;
-    static_assert(BPW * kPieces * 16 <= 160 * 1024, "LDS");
-    __shared__ uint4 buf[BPW * kPieces];
-    const uint64_t first = static_cast<uint64_t>(blockIdx.x) * BPW;
+// Block slots are kMultiPieces 16-byte pieces apart: 2034 = 2 (mod 16), so slot b starts
+// 32 * b bytes into the 256-byte bank period and the chain's ds_read_b64 of the BPW
+// blocks (4 lanes x 8 B each) hit distinct banks (a 32 KiB stride would put them all on
+// the same 8 banks). 5 slots of 32,544 B fit the CU's 160 KiB.
+constexpr uint32_t kMultiPieces = 2034;
+
+struct BlockRef {
+    const uint8_t* p;
+    uint32_t len;
+};
+
+// buf: BPW * kMultiPieces LDS pieces. src_of(b) -> BlockRef of block b < nlive (called by
+// every thread; nlive >= 1). emit(b, h) runs on lane 0 of quad b for b < nlive.
+template <int BPW, class Src, class Emit>
+__device__ __forceinline__ void multi_stage_hash(uint4* buf, uint32_t nlive, Src src_of, Emit emit) {
     const uint4* cover[BPW];
     uint32_t words[BPW], shift8[BPW], nw[BPW];
 #pragma unroll
     for (int b = 0; b < BPW; ++b) {
-        const uint64_t blk = first + b;
         words[b] = 0;
         cover[b] = nullptr;
         shift8[b] = 0;
         nw[b] = 0;
-        if (blk < n) {
-            const uint8_t* src = base + (OFFS ? offs[blk] : blk * stride);
-            const uint32_t L = LENS ? lens[blk] : len;
-            const uint32_t shift = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(src) & 15);
-            const uint32_t w = (shift + L + 15) / 16;
-            if ((shift & 7) == 0 && w <= kPieces) {
+        if (static_cast<uint32_t>(b) < nlive) {
+            const BlockRef r = src_of(static_cast<uint32_t>(b));
+            const uint32_t shift = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(r.p) & 15);
+            const uint32_t w = (shift + r.len + 15) / 16;
+            if ((shift & 7) == 0 && w <= kMultiPieces) {
                 words[b] = w;
-                cover[b] = reinterpret_cast<const uint4*>(src - shift);
+                cover[b] = reinterpret_cast<const uint4*>(r.p - shift);
                 shift8[b] = shift / 8;
-                nw[b] = 4 * (L >> 5);
+                nw[b] = 4 * (r.len >> 5);
             }
         }
     }
@@ -471,23 +470,22 @@ __global__ __launch_bounds__(256) void k_xxh64_wide_multi(const uint8_t* __restr
                 const uint32_t wa = 2 * idx - shift8[b];
                 if (wa < nw[b]) a *= kP2;
                 if (wa + 1 < nw[b]) c *= kP2;
-                buf[b * kPieces + idx] = make_uint4(static_cast<uint32_t>(a), static_cast<uint32_t>(a >> 32),
-                                                    static_cast<uint32_t>(c), static_cast<uint32_t>(c >> 32));
+                buf[b * kMultiPieces + idx] = make_uint4(static_cast<uint32_t>(a), static_cast<uint32_t>(a >> 32),
+                                                         static_cast<uint32_t>(c), static_cast<uint32_t>(c >> 32));
             }
         }
     }
     __syncthreads();
     if (threadIdx.x >= 4 * BPW) return;
     const uint32_t b = threadIdx.x >> 2, j = threadIdx.x & 3;
-    const uint64_t blk = first + b;
-    const bool live = blk < n;
-    const uint64_t bk = live ? blk : n - 1;
-    const uint8_t* src = base + (OFFS ? offs[bk] : bk * stride);
-    const uint32_t L = LENS ? lens[bk] : len;
+    const bool live = b < nlive;
+    const BlockRef r = src_of(live ? b : nlive - 1);
+    const uint8_t* src = r.p;
+    const uint32_t L = r.len;
     const uint32_t nst = L >> 5;
     const uint32_t shift = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(src) & 15);
-    const bool staged = (shift & 7) == 0 && (shift + L + 15) / 16 <= kPieces;
-    const uint8_t* s = staged ? reinterpret_cast<const uint8_t*>(buf + b * kPieces) + shift : src;
+    const bool staged = (shift & 7) == 0 && (shift + L + 15) / 16 <= kMultiPieces;
+    const uint8_t* s = staged ? reinterpret_cast<const uint8_t*>(buf + b * kMultiPieces) + shift : src;
     uint64_t acc = acc_seed(j);
     if (staged)
         acc = quad_stripes_aligned<16, false, true>(reinterpret_cast<const uint64_t*>(s) + j, nst, acc);
@@ -498,16 +496,39 @@ __global__ __launch_bounds__(256) void k_xxh64_wide_multi(const uint8_t* __restr
     const uint64_t v1 = quad_bcast<0>(acc), v2 = quad_bcast<1>(acc), v3 = quad_bcast<2>(acc), v4 = quad_bcast<3>(acc);
     if (j == 0 && live) {
         const uint64_t h0 = (L >= 32) ? converge(v1, v2, v3, v4) : kP5;
-        const uint64_t h = finish_fast(h0, L, s + 32 * static_cast<uint64_t>(nst), L & 31);
-        if (VERIFY) {
-            if (h != expected[blk]) {
-                atomicMin(first_bad, static_cast<unsigned long long>(blk));
-                atomicAdd(n_bad, 1ULL);
-            }
-        } else {
-            out[blk] = h;
-        }
+        emit(b, finish_fast(h0, L, s + 32 * static_cast<uint64_t>(nst), L & 31));
     }
+}
+
+template <bool LENS, bool OFFS, bool VERIFY, int BPW>
+__global__ __launch_bounds__(256) void k_xxh64_wide_multi(const uint8_t* __restrict__ base, uint64_t stride,
+                                                            const uint32_t* __restrict__ lens, uint32_t len,
+                                                            const uint64_t* __restrict__ offs, uint64_t n,
+                                                            uint64_t* __restrict__ out,
+                                                            const uint64_t* __restrict__ expected,
+                                                            unsigned long long* __restrict__ first_bad,
+                                                            unsigned long long* __restrict__ n_bad) {
+    static_assert(BPW * kMultiPieces * 16 <= 160 * 1024, "LDS");
+    __shared__ uint4 buf[BPW * kMultiPieces];
+    const uint64_t first = static_cast<uint64_t>(blockIdx.x) * BPW;
+    const uint32_t nlive = static_cast<uint32_t>(min<uint64_t>(BPW, n - first));
+    multi_stage_hash<BPW>(
+        buf, nlive,
+        [&](uint32_t b) {
+            const uint64_t blk = first + b;
+            return BlockRef{base + (OFFS ? offs[blk] : blk * stride), LENS ? lens[blk] : len};
+        },
+        [&](uint32_t b, uint64_t h) {
+            const uint64_t blk = first + b;
+            if (VERIFY) {
+                if (h != expected[blk]) {
+                    atomicMin(first_bad, static_cast<unsigned long long>(blk));
+                    atomicAdd(n_bad, 1ULL);
+                }
+            } else {
+                out[blk] = h;
+            }
+        });
 }
 
 // ---------------------------------------------------------------------------
@@ -1252,6 +1273,41 @@ __global__ __launch_bounds__(256) void k_commit_level_wide(uint8_t* __restrict__
             arena[b.origin_type] = b.type;
         }
     }
+}
+
+// Mid-size f1 levels (a storm commit's ~1,200 leaves): the wide-multi scheme, BPW dirty
+// blocks per workgroup staged premultiplied in one round trip, one chain wave. The
+// workgroup's BPW records (56 B each, possibly in pinned host memory) cross the bus
+// once, into LDS, before any block address is known.
+template <int BPW>
+__global__ __launch_bounds__(256) void k_commit_level_multi(uint8_t* __restrict__ arena,
+                                                             const stormck_dirty_block* __restrict__ blocks,
+                                                             uint64_t lo, uint64_t cnt,
+                                                             uint64_t* __restrict__ out_cs) {
+    constexpr uint32_t RW = sizeof(stormck_dirty_block) / 8;  // 7 words per record
+    static_assert(BPW * kMultiPieces * 16 + BPW * RW * 8 <= 160 * 1024, "LDS");
+    static_assert(BPW * RW <= 256, "one record word per thread");
+    __shared__ uint4 buf[BPW * kMultiPieces];
+    __shared__ uint64_t rec_w[BPW * RW];
+    const uint64_t first = static_cast<uint64_t>(blockIdx.x) * BPW;
+    const uint32_t nlive = static_cast<uint32_t>(min<uint64_t>(BPW, cnt - first));
+    if (threadIdx.x < nlive * RW)
+        rec_w[threadIdx.x] = reinterpret_cast<const uint64_t*>(blocks + lo + first)[threadIdx.x];
+    __syncthreads();
+    const stormck_dirty_block* rec = reinterpret_cast<const stormck_dirty_block*>(rec_w);
+    multi_stage_hash<BPW>(
+        buf, nlive, [&](uint32_t b) { return BlockRef{arena + rec[b].data_offset, rec[b].length}; },
+        [&](uint32_t b, uint64_t h) {
+            const stormck_dirty_block& r = rec[b];
+            out_cs[lo + first + b] = h;
+            if (r.origin_pointer != STORMCK_NO_ORIGIN) {
+                uint64_t* p = reinterpret_cast<uint64_t*>(arena + r.origin_pointer);
+                p[0] = h;
+                p[1] = r.address;
+                p[2] = r.birth_revision;
+                arena[r.origin_type] = r.type;
+            }
+        });
 }
 
 template <int U>

@@ -135,10 +135,10 @@ constexpr unsigned kGldsThreads = 64 * kGldsWaves;
 constexpr unsigned kGldsBlocks = 16 * kGldsWaves;
 constexpr int kAuxNT = 2;
 constexpr uint64_t kMultiBpw = 5;          // blocks per workgroup of k_xxh64_wide_multi
-constexpr uint64_t kMultiSlotPieces = 2034; // its LDS slot per block, 16-byte pieces (kernels.h)
 constexpr uint64_t kWideBatch = 128;      // batches up to this many blocks: k_xxh64_wide
 constexpr uint64_t kCommitWide = 256;     // f1 levels up to this many blocks: k_commit_level_wide
 constexpr uint64_t kStreamBatch = 16384;  // f1 commit levels from this many blocks: k_commit_level_glds
+constexpr uint64_t kCommitOnePiece = 4096; // f1 commits with at most this many leaves: one checksum copy-back
 // Uniform batches take the LDS-staged kernel from kMidBatch blocks. Below kBigBatch its
 // workgroups are 2 waves (32 blocks, 16 KiB of ring) rather than 8 (128 blocks, 128 KiB):
 // 16,384 blocks in 8-wave workgroups fill only 128 of the 256 CUs
@@ -255,7 +255,7 @@ int launch_checksum(const uint8_t* base, uint64_t stride, const uint32_t* lens, 
     if (multi_on && ncu > 0 && n <= kMultiBpw * ncu &&
         (offs || lens ||
          ((reinterpret_cast<uintptr_t>(base) & 7) == 0 && (stride & 7) == 0 &&
-          ((reinterpret_cast<uintptr_t>(base) & 15) + len + 15) / 16 <= kMultiSlotPieces))) {
+          ((reinterpret_cast<uintptr_t>(base) & 15) + len + 15) / 16 <= kMultiPieces))) {
         const dim3 grid(static_cast<unsigned>((n + kMultiBpw - 1) / kMultiBpw));
 #define STORMCK_MULTI(LENS, OFFS, VER)                                                                       \
     hipLaunchKernelGGL((k_xxh64_wide_multi<LENS, OFFS, VER, kMultiBpw>), grid, dim3(kThreads), 0, st, base, \
@@ -1377,6 +1377,11 @@ int stormck_commit_device(void* d_arena, stormck_dirty_block* blocks, uint64_t n
     hipStream_t st = static_cast<hipStream_t>(stream);
     uint64_t commit_wide = kCommitWide;
     if (const char* e = std::getenv("STORMCK_COMMIT_WIDE")) commit_wide = std::strtoull(e, nullptr, 10);  // probe knob
+    static const bool commit_multi = [] {
+        const char* e = std::getenv("STORMCK_COMMIT_MULTI");  // probe knob: "0" disables
+        return !(e && e[0] == '0');
+    }();
+    const uint64_t ncu = cu_count();
     auto launch_level = [&](uint64_t lo, uint64_t cnt) -> int {
         if (aligned16 && cnt >= kStreamBatch) {
             // LDS-DMA ring, 8 waves x 128 blocks per workgroup (as the uniform fast path)
@@ -1388,6 +1393,10 @@ int stormck_commit_device(void* d_arena, stormck_dirty_block* blocks, uint64_t n
             // one workgroup per block, premultiplied staging: the chain wave is alone on its SIMD
             hipLaunchKernelGGL(k_commit_level_wide, dim3(static_cast<unsigned>(cnt)), dim3(kThreads), 0, st,
                                static_cast<uint8_t*>(d_arena), d_blocks, lo, d_cs);
+        } else if (commit_multi && ncu > 0 && cnt <= kMultiBpw * ncu) {
+            // up to kMultiBpw blocks per CU (a storm commit's leaves): wide-multi staging
+            hipLaunchKernelGGL((k_commit_level_multi<kMultiBpw>), dim3(static_cast<unsigned>((cnt + kMultiBpw - 1) / kMultiBpw)),
+                               dim3(kThreads), 0, st, static_cast<uint8_t*>(d_arena), d_blocks, lo, cnt, d_cs);
         } else {
             dim3 grid;
             if (!grid_for(cnt * 4, &grid)) return fail(STORMCK_EINVAL, "level too large");
@@ -1461,14 +1470,23 @@ int stormck_commit_device(void* d_arena, stormck_dirty_block* blocks, uint64_t n
                 growth = gr;
             }
         }
+        // A small commit (storm's per-revision commit: ~1,200 leaves under one pointer
+        // block) returns its checksums in one piece after the last level: an event
+        // recorded between two launches holds the second one back by about 4 us
+        // (profiles/r02_c5_multi/), more than copying a few thousand checksums costs.
+        const bool one_piece = nu > 0 && n0 <= kCommitOnePiece;
+        uint64_t unsent = 0;  // first commit position not yet covered by `back`
         for (uint64_t lo = 0; lo < n0;) {
             uint64_t cnt = std::min(next, n0 - lo);
             if (n0 - lo - cnt < kStreamBatch) cnt = n0 - lo;  // no runt last chunk
             stage_records(lo, lo + cnt);
             int e = launch_level(lo, cnt);
             if (e) return e;
-            e = send_back(lo, cnt);
-            if (e) return e;
+            if (!one_piece) {
+                e = send_back(lo, cnt);
+                if (e) return e;
+                unsent = lo + cnt;
+            }
             lo += cnt;
             next = cnt * growth;
         }
@@ -1540,7 +1558,7 @@ int stormck_commit_device(void* d_arena, stormck_dirty_block* blocks, uint64_t n
             e = launch_level(lo, cnt);
             if (e) return e;
         }
-        return send_back(n0, nu);
+        return send_back(unsent, n - unsent);
     };
     rc = run();
     *last_allocated_block = last;  // the relocations applied to the caller's records so far
