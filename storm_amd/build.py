@@ -56,7 +56,7 @@ def build_oracle(force: bool = False) -> str:
     return out
 
 
-PROBES = ("probe", "probe_keys", "probe_small", "alloc_probe", "phase_probe", "span_probe")  # tools/<name>.hip: design probes
+PROBES = ("probe", "probe_keys", "probe_small", "alloc_probe", "phase_probe", "span_probe", "clock_probe")  # tools/<name>.hip: design probes
 SANITIZE = os.path.join(ROOT, "tests", "sanitize")
 READPEAK = os.path.join(ROOT, "tools", "libreadpeak.so")  # bench.py's measured read peak (not product)
 
