@@ -313,6 +313,18 @@ __global__ __launch_bounds__(256) void k_xxh64_single(const uint8_t* __restrict_
 // ---------------------------------------------------------------------------
 constexpr uint32_t kWideMax = 32 * 1024;
 
+// One block of a staged kernel: its first byte and its length.
+struct BlockRef {
+    const uint8_t* p;
+    uint32_t len;
+};
+
+// Pipelined staging (multi_stage_hash_pipe, below): chunks of 256 16-byte pieces per
+// block, an LDS counter per chunk, 3 stager waves.
+constexpr uint32_t kChunkPieces = 256;  // 4 KiB per block per chunk
+constexpr uint32_t kPipeChunks = 8;
+constexpr uint32_t kPipeStagers = 3;    // waves 1..3 of a 256-thread workgroup
+
 // Quad 0's part of k_xxh64_wide. Inlined once per branch, so the words are read with
 // ds_read from the staged copy and with global loads otherwise: through one generic
 // pointer both would be flat loads, which the compiler can only wait for all at once
@@ -409,11 +421,6 @@ __global__ __launch_bounds__(256) void k_xxh64_wide(const uint8_t* __restrict__ 
 // the same 8 banks). 5 slots of 32,544 B fit the CU's 160 KiB.
 constexpr uint32_t kMultiPieces = 2034;
 
-struct BlockRef {
-    const uint8_t* p;
-    uint32_t len;
-};
-
 // buf: BPW * kMultiPieces LDS pieces. src_of(b) -> BlockRef of block b < nlive (called by
 // every thread; nlive >= 1). emit(b, h) runs on lane 0 of quad b for b < nlive.
 template <int BPW, class Src, class Emit>
@@ -500,7 +507,148 @@ __device__ __forceinline__ void multi_stage_hash(uint4* buf, uint32_t nlive, Src
     }
 }
 
-template <bool LENS, bool OFFS, bool VERIFY, int BPW>
+// Pipelined form of multi_stage_hash. The whole-block staging above costs one full
+// round trip of BPW x 32 KiB per CU before the first chain round. Here the workgroup
+// stages only the first 4 KiB chunk of every block together, then wave 0 starts the
+// chains while waves 1-3 stage chunks 1.. in order; after each chunk a stager wave
+// adds 1 to that chunk's LDS counter, and the chain waits (s_sleep polls) for a
+// chunk's count to reach 3 before reading its stripes. A chain consumes a chunk in
+// ~3 us and the stagers fill one in about one memory round trip, so it rarely waits.
+// ready: kPipeChunks LDS words. Same contract as multi_stage_hash otherwise; the block
+// cover must fit PIECES (<= kPipeChunks chunks of 256 pieces).
+
+// Bounded: a chunk that never completes (a staging/chain disagreement would be a bug)
+// gives a wrong checksum after ~0.1 s of polling, which the parity tests report,
+// instead of a wave that never exits.
+__device__ __forceinline__ void pipe_wait(const uint32_t* ready, uint32_t c) {
+    for (uint32_t spin = 0;
+         __hip_atomic_load(ready + c, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < kPipeStagers &&
+         spin < (1u << 22);
+         ++spin)
+        __builtin_amdgcn_s_sleep(1);
+}
+
+template <int BPW, uint32_t PIECES, class Src, class Emit>
+__device__ __forceinline__ void multi_stage_hash_pipe(uint4* buf, uint32_t* ready, uint32_t nlive, Src src_of,
+                                                      Emit emit) {
+    static_assert(PIECES <= kPipeChunks * kChunkPieces, "cover exceeds the chunk counters");
+    constexpr uint32_t NCH = (PIECES + kChunkPieces - 1) / kChunkPieces;
+    const uint4* cover[BPW];
+    uint32_t words[BPW], shift8[BPW], nw[BPW];
+#pragma unroll
+    for (int b = 0; b < BPW; ++b) {
+        words[b] = 0;
+        cover[b] = nullptr;
+        shift8[b] = 0;
+        nw[b] = 0;
+        if (static_cast<uint32_t>(b) < nlive) {
+            const BlockRef r = src_of(static_cast<uint32_t>(b));
+            const uint32_t shift = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(r.p) & 15);
+            const uint32_t w = (shift + r.len + 15) / 16;
+            if ((shift & 7) == 0 && w <= PIECES) {
+                words[b] = w;
+                cover[b] = reinterpret_cast<const uint4*>(r.p - shift);
+                shift8[b] = shift / 8;
+                nw[b] = 4 * (r.len >> 5);
+            }
+        }
+    }
+    const uint4* safe = nullptr;
+#pragma unroll
+    for (int b = 0; b < BPW; ++b)
+        if (!safe && words[b]) safe = cover[b];
+    const uint4* cv[BPW];
+    uint32_t lim[BPW];
+#pragma unroll
+    for (int b = 0; b < BPW; ++b) {
+        cv[b] = words[b] ? cover[b] : safe;
+        lim[b] = words[b] ? words[b] - 1 : 0;
+    }
+    // piece idx of block b, premultiplied, into its slot (idx < words[b])
+    auto put = [&](int b, uint32_t idx, const uint4& v) {
+        uint64_t a = (static_cast<uint64_t>(v.y) << 32) | v.x;
+        uint64_t c = (static_cast<uint64_t>(v.w) << 32) | v.z;
+        const uint32_t wa = 2 * idx - shift8[b];
+        if (wa < nw[b]) a *= kP2;
+        if (wa + 1 < nw[b]) c *= kP2;
+        buf[b * PIECES + idx] = make_uint4(static_cast<uint32_t>(a), static_cast<uint32_t>(a >> 32),
+                                           static_cast<uint32_t>(c), static_cast<uint32_t>(c >> 32));
+    };
+    if (threadIdx.x < kPipeChunks) ready[threadIdx.x] = 0;
+    if (safe) {  // chunk 0, every thread one piece of each block (uniform over the workgroup)
+        uint4 r[BPW];
+#pragma unroll
+        for (int b = 0; b < BPW; ++b) r[b] = cv[b][min(threadIdx.x, lim[b])];
+#pragma unroll
+        for (int b = 0; b < BPW; ++b)
+            if (threadIdx.x < words[b]) put(b, threadIdx.x, r[b]);
+    }
+    __syncthreads();
+    if (threadIdx.x >= 64) {
+        if (!safe) return;
+        // stagers: chunk c's 256 pieces per block over 192 threads, t and t + 192 (< 256);
+        // the second load of threads t >= 64 repeats a clamped address and is not stored
+        const uint32_t t = threadIdx.x - 64;
+        for (uint32_t c = 1; c < NCH; ++c) {
+            uint4 r[BPW][2];
+#pragma unroll
+            for (int b = 0; b < BPW; ++b)
+#pragma unroll
+                for (int q = 0; q < 2; ++q)
+                    r[b][q] = cv[b][min(c * kChunkPieces + min(t + 192u * q, kChunkPieces - 1), lim[b])];
+#pragma unroll
+            for (int b = 0; b < BPW; ++b)
+#pragma unroll
+                for (int q = 0; q < 2; ++q) {
+                    const uint32_t k = t + 192u * q, idx = c * kChunkPieces + k;
+                    if (k < kChunkPieces && idx < words[b]) put(b, idx, r[b][q]);
+                }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            if ((threadIdx.x & 63) == 0)
+                __hip_atomic_fetch_add(ready + c, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        return;
+    }
+    if (threadIdx.x >= 4 * BPW) return;
+    const uint32_t b = threadIdx.x >> 2, j = threadIdx.x & 3;
+    const bool live = b < nlive;
+    const BlockRef r = src_of(live ? b : nlive - 1);
+    const uint8_t* src = r.p;
+    const uint32_t L = r.len;
+    const uint32_t nst = L >> 5;
+    const uint32_t shift = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(src) & 15);
+    // exactly the staging condition above (an empty block at a 16-byte boundary has no
+    // pieces, is not staged, and must not wait for chunks that nobody stages)
+    const uint32_t w = (shift + L + 15) / 16;
+    const bool staged = safe && (shift & 7) == 0 && w > 0 && w <= PIECES;
+    const uint8_t* s = staged ? reinterpret_cast<const uint8_t*>(buf + b * PIECES) + shift : src;
+    uint64_t acc = acc_seed(j);
+    if (staged) {
+        // stripes that end inside chunks 0..c, then wait for chunk c + 1
+        const uint64_t* w = reinterpret_cast<const uint64_t*>(s) + j;
+        uint32_t done = 0;
+        for (uint32_t c = 0; c < NCH; ++c) {
+            if (c > 0) pipe_wait(ready, c);
+            const uint32_t end = min(nst, (kChunkPieces * 16 * (c + 1) - shift) / 32);
+            if (end > done) {
+                acc = quad_stripes_aligned<16, false, true>(w + 4 * done, end - done, acc);
+                done = end;
+            }
+        }
+    } else if ((reinterpret_cast<uintptr_t>(src) & 7) == 0) {
+        acc = quad_stripes_aligned<16>(reinterpret_cast<const uint64_t*>(src) + j, nst, acc);
+    } else {
+        acc = quad_stripes_unaligned(src + 8 * j, nst, acc);
+    }
+    const uint64_t v1 = quad_bcast<0>(acc), v2 = quad_bcast<1>(acc), v3 = quad_bcast<2>(acc), v4 = quad_bcast<3>(acc);
+    if (j == 0 && live) {
+        const uint64_t h0 = (L >= 32) ? converge(v1, v2, v3, v4) : kP5;
+        emit(b, finish_fast(h0, L, s + 32 * static_cast<uint64_t>(nst), L & 31));
+    }
+}
+
+// PIPE: the pipelined body (multi_stage_hash_pipe), else whole blocks staged first.
+template <bool LENS, bool OFFS, bool VERIFY, int BPW, bool PIPE = true>
 __global__ __launch_bounds__(256) void k_xxh64_wide_multi(const uint8_t* __restrict__ base, uint64_t stride,
                                                             const uint32_t* __restrict__ lens, uint32_t len,
                                                             const uint64_t* __restrict__ offs, uint64_t n,
@@ -508,27 +656,31 @@ __global__ __launch_bounds__(256) void k_xxh64_wide_multi(const uint8_t* __restr
                                                             const uint64_t* __restrict__ expected,
                                                             unsigned long long* __restrict__ first_bad,
                                                             unsigned long long* __restrict__ n_bad) {
-    static_assert(BPW * kMultiPieces * 16 <= 160 * 1024, "LDS");
+    static_assert(BPW * kMultiPieces * 16 + kPipeChunks * 4 <= 160 * 1024, "LDS");
     __shared__ uint4 buf[BPW * kMultiPieces];
     const uint64_t first = static_cast<uint64_t>(blockIdx.x) * BPW;
     const uint32_t nlive = static_cast<uint32_t>(min<uint64_t>(BPW, n - first));
-    multi_stage_hash<BPW>(
-        buf, nlive,
-        [&](uint32_t b) {
-            const uint64_t blk = first + b;
-            return BlockRef{base + (OFFS ? offs[blk] : blk * stride), LENS ? lens[blk] : len};
-        },
-        [&](uint32_t b, uint64_t h) {
-            const uint64_t blk = first + b;
-            if (VERIFY) {
-                if (h != expected[blk]) {
-                    atomicMin(first_bad, static_cast<unsigned long long>(blk));
-                    atomicAdd(n_bad, 1ULL);
-                }
-            } else {
-                out[blk] = h;
+    auto src_of = [&](uint32_t b) {
+        const uint64_t blk = first + b;
+        return BlockRef{base + (OFFS ? offs[blk] : blk * stride), LENS ? lens[blk] : len};
+    };
+    auto emit = [&](uint32_t b, uint64_t h) {
+        const uint64_t blk = first + b;
+        if (VERIFY) {
+            if (h != expected[blk]) {
+                atomicMin(first_bad, static_cast<unsigned long long>(blk));
+                atomicAdd(n_bad, 1ULL);
             }
-        });
+        } else {
+            out[blk] = h;
+        }
+    };
+    if constexpr (PIPE) {
+        __shared__ uint32_t ready[kPipeChunks];
+        multi_stage_hash_pipe<BPW, kMultiPieces>(buf, ready, nlive, src_of, emit);
+    } else {
+        multi_stage_hash<BPW>(buf, nlive, src_of, emit);
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1279,13 +1431,13 @@ __global__ __launch_bounds__(256) void k_commit_level_wide(uint8_t* __restrict__
 // blocks per workgroup staged premultiplied in one round trip, one chain wave. The
 // workgroup's BPW records (56 B each, possibly in pinned host memory) cross the bus
 // once, into LDS, before any block address is known.
-template <int BPW>
+template <int BPW, bool PIPE = true>
 __global__ __launch_bounds__(256) void k_commit_level_multi(uint8_t* __restrict__ arena,
                                                              const stormck_dirty_block* __restrict__ blocks,
                                                              uint64_t lo, uint64_t cnt,
                                                              uint64_t* __restrict__ out_cs) {
     constexpr uint32_t RW = sizeof(stormck_dirty_block) / 8;  // 7 words per record
-    static_assert(BPW * kMultiPieces * 16 + BPW * RW * 8 <= 160 * 1024, "LDS");
+    static_assert(BPW * kMultiPieces * 16 + BPW * RW * 8 + kPipeChunks * 4 <= 160 * 1024, "LDS");
     static_assert(BPW * RW <= 256, "one record word per thread");
     __shared__ uint4 buf[BPW * kMultiPieces];
     __shared__ uint64_t rec_w[BPW * RW];
@@ -1295,19 +1447,24 @@ __global__ __launch_bounds__(256) void k_commit_level_multi(uint8_t* __restrict_
         rec_w[threadIdx.x] = reinterpret_cast<const uint64_t*>(blocks + lo + first)[threadIdx.x];
     __syncthreads();
     const stormck_dirty_block* rec = reinterpret_cast<const stormck_dirty_block*>(rec_w);
-    multi_stage_hash<BPW>(
-        buf, nlive, [&](uint32_t b) { return BlockRef{arena + rec[b].data_offset, rec[b].length}; },
-        [&](uint32_t b, uint64_t h) {
-            const stormck_dirty_block& r = rec[b];
-            out_cs[lo + first + b] = h;
-            if (r.origin_pointer != STORMCK_NO_ORIGIN) {
-                uint64_t* p = reinterpret_cast<uint64_t*>(arena + r.origin_pointer);
-                p[0] = h;
-                p[1] = r.address;
-                p[2] = r.birth_revision;
-                arena[r.origin_type] = r.type;
-            }
-        });
+    auto src_of = [&](uint32_t b) { return BlockRef{arena + rec[b].data_offset, rec[b].length}; };
+    auto emit = [&](uint32_t b, uint64_t h) {
+        const stormck_dirty_block& r = rec[b];
+        out_cs[lo + first + b] = h;
+        if (r.origin_pointer != STORMCK_NO_ORIGIN) {
+            uint64_t* p = reinterpret_cast<uint64_t*>(arena + r.origin_pointer);
+            p[0] = h;
+            p[1] = r.address;
+            p[2] = r.birth_revision;
+            arena[r.origin_type] = r.type;
+        }
+    };
+    if constexpr (PIPE) {
+        __shared__ uint32_t ready[kPipeChunks];
+        multi_stage_hash_pipe<BPW, kMultiPieces>(buf, ready, nlive, src_of, emit);
+    } else {
+        multi_stage_hash<BPW>(buf, nlive, src_of, emit);
+    }
 }
 
 template <int U>

@@ -206,6 +206,16 @@ uint64_t cu_count() {
     return static_cast<uint64_t>(v);
 }
 
+// Pipelined staging in the wide-multi kernels (kernels.h multi_stage_hash_pipe);
+// STORMCK_STAGE_PIPE=0 stages whole blocks first (A/B).
+bool pipe_staging() {
+    static const bool on = [] {
+        const char* e = std::getenv("STORMCK_STAGE_PIPE");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 bool grid_for(uint64_t threads, dim3* grid) {
     const uint64_t blocks = (threads + kThreads - 1) / kThreads;
     if (blocks == 0 || blocks > 0x7fffffffULL) return false;
@@ -251,15 +261,22 @@ int launch_checksum(const uint8_t* base, uint64_t stride, const uint32_t* lens, 
         const char* e = std::getenv("STORMCK_WIDE_MULTI");  // probe knob: "0" disables
         return !(e && e[0] == '0');
     }();
+    const bool stage_pipe = pipe_staging();
     const uint64_t ncu = cu_count();
     if (multi_on && ncu > 0 && n <= kMultiBpw * ncu &&
         (offs || lens ||
          ((reinterpret_cast<uintptr_t>(base) & 7) == 0 && (stride & 7) == 0 &&
           ((reinterpret_cast<uintptr_t>(base) & 15) + len + 15) / 16 <= kMultiPieces))) {
         const dim3 grid(static_cast<unsigned>((n + kMultiBpw - 1) / kMultiBpw));
-#define STORMCK_MULTI(LENS, OFFS, VER)                                                                       \
-    hipLaunchKernelGGL((k_xxh64_wide_multi<LENS, OFFS, VER, kMultiBpw>), grid, dim3(kThreads), 0, st, base, \
-                       stride, lens, len, offs, n, out, expected, first_bad, n_bad)
+#define STORMCK_MULTI(LENS, OFFS, VER)                                                                         \
+    do {                                                                                                      \
+        if (stage_pipe)                                                                                       \
+            hipLaunchKernelGGL((k_xxh64_wide_multi<LENS, OFFS, VER, kMultiBpw, true>), grid, dim3(kThreads), 0, \
+                               st, base, stride, lens, len, offs, n, out, expected, first_bad, n_bad);        \
+        else                                                                                                  \
+            hipLaunchKernelGGL((k_xxh64_wide_multi<LENS, OFFS, VER, kMultiBpw, false>), grid, dim3(kThreads), 0, \
+                               st, base, stride, lens, len, offs, n, out, expected, first_bad, n_bad);        \
+    } while (0)
         if (!verify) {
             if (lens && offs) STORMCK_MULTI(true, true, false);
             else if (lens) STORMCK_MULTI(true, false, false);
@@ -1395,8 +1412,13 @@ int stormck_commit_device(void* d_arena, stormck_dirty_block* blocks, uint64_t n
                                static_cast<uint8_t*>(d_arena), d_blocks, lo, d_cs);
         } else if (commit_multi && ncu > 0 && cnt <= kMultiBpw * ncu) {
             // up to kMultiBpw blocks per CU (a storm commit's leaves): wide-multi staging
-            hipLaunchKernelGGL((k_commit_level_multi<kMultiBpw>), dim3(static_cast<unsigned>((cnt + kMultiBpw - 1) / kMultiBpw)),
-                               dim3(kThreads), 0, st, static_cast<uint8_t*>(d_arena), d_blocks, lo, cnt, d_cs);
+            const dim3 grid(static_cast<unsigned>((cnt + kMultiBpw - 1) / kMultiBpw));
+            if (pipe_staging())
+                hipLaunchKernelGGL((k_commit_level_multi<kMultiBpw, true>), grid, dim3(kThreads), 0, st,
+                                   static_cast<uint8_t*>(d_arena), d_blocks, lo, cnt, d_cs);
+            else
+                hipLaunchKernelGGL((k_commit_level_multi<kMultiBpw, false>), grid, dim3(kThreads), 0, st,
+                                   static_cast<uint8_t*>(d_arena), d_blocks, lo, cnt, d_cs);
         } else {
             dim3 grid;
             if (!grid_for(cnt * 4, &grid)) return fail(STORMCK_EINVAL, "level too large");
