@@ -129,12 +129,9 @@ __device__ __forceinline__ uint64_t finish_fast(uint64_t h, uint64_t n, const ui
 // (at most roundup16(rem) bytes, so never past a 16-byte-padded key). The compiler
 // guards narrower LDS reads behind in-flight LDS-DMA with a full vmcnt(0) wait, which
 // would drain a key kernel's whole prefetch ring at every key's tail.
-__device__ __forceinline__ uint64_t finish_lds16(uint64_t h, uint64_t n, const uint8_t* p, uint32_t rem) {
+// Tail + avalanche of the rem < 32 tail bytes held little-endian in w[0..3].
+__device__ __forceinline__ uint64_t finish_regs(uint64_t h, uint64_t n, const uint64_t (&w)[4], uint32_t rem) {
     h += n;
-    u64x2 a = {0, 0}, b = {0, 0};
-    if (rem > 0) a = *reinterpret_cast<const u64x2*>(p);
-    if (rem > 16) b = *reinterpret_cast<const u64x2*>(p + 16);
-    const uint64_t w[4] = {a.x, a.y, b.x, b.y};
 #pragma unroll
     for (int q = 0; q < 3; ++q) {
         if (rem >= 8u * (q + 1)) {
@@ -157,6 +154,14 @@ __device__ __forceinline__ uint64_t finish_lds16(uint64_t h, uint64_t n, const u
         x >>= 8;
     }
     return avalanche(h);
+}
+
+__device__ __forceinline__ uint64_t finish_lds16(uint64_t h, uint64_t n, const uint8_t* p, uint32_t rem) {
+    u64x2 a = {0, 0}, b = {0, 0};
+    if (rem > 0) a = *reinterpret_cast<const u64x2*>(p);
+    if (rem > 16) b = *reinterpret_cast<const u64x2*>(p + 16);
+    const uint64_t w[4] = {a.x, a.y, b.x, b.y};
+    return finish_regs(h, n, w, rem);
 }
 
 // ---------------------------------------------------------------------------
@@ -319,11 +324,21 @@ struct BlockRef {
     uint32_t len;
 };
 
-// Pipelined staging (multi_stage_hash_pipe, below): chunks of 256 16-byte pieces per
-// block, an LDS counter per chunk, 3 stager waves.
-constexpr uint32_t kChunkPieces = 256;  // 4 KiB per block per chunk
-constexpr uint32_t kPipeChunks = 8;
-constexpr uint32_t kPipeStagers = 3;    // waves 1..3 of a 256-thread workgroup
+// Pipelined staging (multi_stage_hash_pipe, below): 4 KiB chunks (256 16-byte pieces)
+// of each block through a ring of kRingSlots LDS slots per block, an LDS counter per
+// chunk, 3 stager waves. A slot holds 2 pieces of pre-pad (the previous chunk's last
+// 32 bytes) and the chunk, so a stripe or tail that starts in one chunk and ends in
+// the next reads contiguous bytes from the later chunk's slot. Blocks are
+// kRingBlockPieces = 2 (mod 16) pieces apart, so the 5 chains of a wave read distinct
+// LDS banks (as kMultiPieces below).
+constexpr uint32_t kChunkPieces = 256;
+constexpr uint32_t kPipeMaxChunks = 16;  // covers up to 64 KiB
+constexpr uint32_t kPipeStagers = 3;     // waves 1..3 of a 256-thread workgroup
+constexpr uint32_t kRingSlots = 4;  // 7 slots measured slower (profiles/r02_pipe/)
+constexpr uint32_t kSlotPieces = 2 + kChunkPieces;
+constexpr uint32_t kRingBlockPieces = 1042;  // >= kRingSlots * kSlotPieces, = 2 (mod 16)
+constexpr uint32_t kRingSlackPieces = 2;     // a 32-byte tail read past the last slot stays inside
+static_assert(kRingBlockPieces >= kRingSlots * kSlotPieces && kRingBlockPieces % 16 == 2, "ring layout");
 
 // Quad 0's part of k_xxh64_wide. Inlined once per branch, so the words are read with
 // ds_read from the staged copy and with global loads otherwise: through one generic
@@ -508,33 +523,38 @@ __device__ __forceinline__ void multi_stage_hash(uint4* buf, uint32_t nlive, Src
 }
 
 // Pipelined form of multi_stage_hash. The whole-block staging above costs one full
-// round trip of BPW x 32 KiB per CU before the first chain round. Here the workgroup
-// stages only the first 4 KiB chunk of every block together, then wave 0 starts the
-// chains while waves 1-3 stage chunks 1.. in order; after each chunk a stager wave
-// adds 1 to that chunk's LDS counter, and the chain waits (s_sleep polls) for a
-// chunk's count to reach 3 before reading its stripes. A chain consumes a chunk in
-// ~3 us and the stagers fill one in about one memory round trip, so it rarely waits.
-// ready: kPipeChunks LDS words. Same contract as multi_stage_hash otherwise; the block
-// cover must fit PIECES (<= kPipeChunks chunks of 256 pieces).
+// round trip of BPW x 32 KiB per CU before the first chain round, and a 32 KiB block
+// (cover 2,048 or 2,049 pieces) does not fit its 2,034-piece slot at all. Here the
+// workgroup stages the first 4 KiB chunk of every block together; then wave 0 walks
+// the chains while waves 1-3 stage chunks 1.. in order through a 4-slot ring per
+// block (layout above). Per chunk, each stager wave adds 1 to the chunk's LDS counter
+// and the chain waits for 3 before reading it; the chain publishes how many chunks it
+// has finished, and a stager overwrites a slot only after the chain finished the chunk
+// that held it. A chain consumes a chunk in ~3 us, the stagers fill one in about one
+// memory round trip, so neither side waits long. Each lane keeps its block's tail
+// (< 32 bytes) in registers when it passes the tail's chunk, before the slot can be
+// reused. Blocks with 8-byte-aligned starts and covers up to 64 KiB are staged; others
+// hash from memory in the same lanes.
+// ring: BPW * kRingBlockPieces + kRingSlackPieces pieces; ready: kPipeMaxChunks words;
+// done: one word. Same contract as multi_stage_hash otherwise.
 
 // Bounded: a chunk that never completes (a staging/chain disagreement would be a bug)
 // gives a wrong checksum after ~0.1 s of polling, which the parity tests report,
 // instead of a wave that never exits.
-__device__ __forceinline__ void pipe_wait(const uint32_t* ready, uint32_t c) {
+__device__ __forceinline__ void pipe_wait(const uint32_t* word, uint32_t at_least) {
     for (uint32_t spin = 0;
-         __hip_atomic_load(ready + c, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < kPipeStagers &&
-         spin < (1u << 22);
+         __hip_atomic_load(word, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < at_least && spin < (1u << 22);
          ++spin)
         __builtin_amdgcn_s_sleep(1);
 }
 
-template <int BPW, uint32_t PIECES, class Src, class Emit>
-__device__ __forceinline__ void multi_stage_hash_pipe(uint4* buf, uint32_t* ready, uint32_t nlive, Src src_of,
-                                                      Emit emit) {
-    static_assert(PIECES <= kPipeChunks * kChunkPieces, "cover exceeds the chunk counters");
-    constexpr uint32_t NCH = (PIECES + kChunkPieces - 1) / kChunkPieces;
+template <int BPW, class Src, class Emit>
+__device__ __forceinline__ void multi_stage_hash_pipe(uint4* ring, uint32_t* ready, uint32_t* done, uint32_t nlive,
+                                                      Src src_of, Emit emit) {
+    constexpr uint32_t kMaxPieces = kPipeMaxChunks * kChunkPieces;
     const uint4* cover[BPW];
     uint32_t words[BPW], shift8[BPW], nw[BPW];
+    uint32_t nch = 0;  // chunks of the longest staged block (uniform over the workgroup)
 #pragma unroll
     for (int b = 0; b < BPW; ++b) {
         words[b] = 0;
@@ -545,11 +565,12 @@ __device__ __forceinline__ void multi_stage_hash_pipe(uint4* buf, uint32_t* read
             const BlockRef r = src_of(static_cast<uint32_t>(b));
             const uint32_t shift = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(r.p) & 15);
             const uint32_t w = (shift + r.len + 15) / 16;
-            if ((shift & 7) == 0 && w <= PIECES) {
+            if ((shift & 7) == 0 && w > 0 && w <= kMaxPieces) {
                 words[b] = w;
                 cover[b] = reinterpret_cast<const uint4*>(r.p - shift);
                 shift8[b] = shift / 8;
                 nw[b] = 4 * (r.len >> 5);
+                nch = max(nch, (w + kChunkPieces - 1) / kChunkPieces);
             }
         }
     }
@@ -564,44 +585,47 @@ __device__ __forceinline__ void multi_stage_hash_pipe(uint4* buf, uint32_t* read
         cv[b] = words[b] ? cover[b] : safe;
         lim[b] = words[b] ? words[b] - 1 : 0;
     }
-    // piece idx of block b, premultiplied, into its slot (idx < words[b])
-    auto put = [&](int b, uint32_t idx, const uint4& v) {
+    // cover piece idx of block b, premultiplied, into ring position pos of the block
+    auto put = [&](int b, uint32_t pos, uint32_t idx, const uint4& v) {
         uint64_t a = (static_cast<uint64_t>(v.y) << 32) | v.x;
         uint64_t c = (static_cast<uint64_t>(v.w) << 32) | v.z;
         const uint32_t wa = 2 * idx - shift8[b];
         if (wa < nw[b]) a *= kP2;
         if (wa + 1 < nw[b]) c *= kP2;
-        buf[b * PIECES + idx] = make_uint4(static_cast<uint32_t>(a), static_cast<uint32_t>(a >> 32),
-                                           static_cast<uint32_t>(c), static_cast<uint32_t>(c >> 32));
+        ring[b * kRingBlockPieces + pos] = make_uint4(static_cast<uint32_t>(a), static_cast<uint32_t>(a >> 32),
+                                                      static_cast<uint32_t>(c), static_cast<uint32_t>(c >> 32));
     };
-    if (threadIdx.x < kPipeChunks) ready[threadIdx.x] = 0;
-    if (safe) {  // chunk 0, every thread one piece of each block (uniform over the workgroup)
+    if (threadIdx.x < kPipeMaxChunks) ready[threadIdx.x] = 0;
+    if (threadIdx.x == 0) *done = 0;
+    if (safe) {  // chunk 0 into slot 0, every thread one piece of each block
         uint4 r[BPW];
 #pragma unroll
         for (int b = 0; b < BPW; ++b) r[b] = cv[b][min(threadIdx.x, lim[b])];
 #pragma unroll
         for (int b = 0; b < BPW; ++b)
-            if (threadIdx.x < words[b]) put(b, threadIdx.x, r[b]);
+            if (threadIdx.x < words[b]) put(b, 2 + threadIdx.x, threadIdx.x, r[b]);
     }
     __syncthreads();
     if (threadIdx.x >= 64) {
-        if (!safe) return;
-        // stagers: chunk c's 256 pieces per block over 192 threads, t and t + 192 (< 256);
-        // the second load of threads t >= 64 repeats a clamped address and is not stored
+        // stagers: slot position k < 258 of chunk c holds cover piece 256c - 2 + k; over
+        // 192 threads as k = t and t + 192 (the second load of t >= 66 repeats a clamped
+        // address and is not stored)
         const uint32_t t = threadIdx.x - 64;
-        for (uint32_t c = 1; c < NCH; ++c) {
+        for (uint32_t c = 1; c < nch; ++c) {
+            if (c >= kRingSlots) pipe_wait(done, c - kRingSlots + 1);  // the slot's old chunk is finished
+            const uint32_t slot = (c % kRingSlots) * kSlotPieces;
             uint4 r[BPW][2];
 #pragma unroll
             for (int b = 0; b < BPW; ++b)
 #pragma unroll
                 for (int q = 0; q < 2; ++q)
-                    r[b][q] = cv[b][min(c * kChunkPieces + min(t + 192u * q, kChunkPieces - 1), lim[b])];
+                    r[b][q] = cv[b][min(c * kChunkPieces - 2 + min(t + 192u * q, kSlotPieces - 1), lim[b])];
 #pragma unroll
             for (int b = 0; b < BPW; ++b)
 #pragma unroll
                 for (int q = 0; q < 2; ++q) {
-                    const uint32_t k = t + 192u * q, idx = c * kChunkPieces + k;
-                    if (k < kChunkPieces && idx < words[b]) put(b, idx, r[b][q]);
+                    const uint32_t k = t + 192u * q, idx = c * kChunkPieces - 2 + k;
+                    if (k < kSlotPieces && idx < words[b]) put(b, slot + k, idx, r[b][q]);
                 }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
             if ((threadIdx.x & 63) == 0)
@@ -617,33 +641,48 @@ __device__ __forceinline__ void multi_stage_hash_pipe(uint4* buf, uint32_t* read
     const uint32_t L = r.len;
     const uint32_t nst = L >> 5;
     const uint32_t shift = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(src) & 15);
-    // exactly the staging condition above (an empty block at a 16-byte boundary has no
-    // pieces, is not staged, and must not wait for chunks that nobody stages)
+    // exactly the staging condition above
     const uint32_t w = (shift + L + 15) / 16;
-    const bool staged = safe && (shift & 7) == 0 && w > 0 && w <= PIECES;
-    const uint8_t* s = staged ? reinterpret_cast<const uint8_t*>(buf + b * PIECES) + shift : src;
+    const bool staged = safe && (shift & 7) == 0 && w > 0 && w <= kMaxPieces;
+    const uint8_t* blk_ring = reinterpret_cast<const uint8_t*>(ring + b * kRingBlockPieces);
+    const uint32_t tail_chunk = (shift + L - (L > 0 ? 1 : 0)) / (16 * kChunkPieces);
     uint64_t acc = acc_seed(j);
-    if (staged) {
-        // stripes that end inside chunks 0..c, then wait for chunk c + 1
-        const uint64_t* w = reinterpret_cast<const uint64_t*>(s) + j;
-        uint32_t done = 0;
-        for (uint32_t c = 0; c < NCH; ++c) {
-            if (c > 0) pipe_wait(ready, c);
-            const uint32_t end = min(nst, (kChunkPieces * 16 * (c + 1) - shift) / 32);
-            if (end > done) {
-                acc = quad_stripes_aligned<16, false, true>(w + 4 * done, end - done, acc);
-                done = end;
+    uint64_t tail[4] = {0, 0, 0, 0};
+    uint32_t s_done = 0;
+    // every chain lane runs the chunk loop (lane 0 publishes progress for the wave)
+    for (uint32_t c = 0; c < nch; ++c) {
+        if (c > 0) pipe_wait(ready + c, kPipeStagers);
+        if (staged) {
+            // slot byte of cover byte x of this chunk: 32 + x - 4096c
+            const uint8_t* slot = blk_ring + (c % kRingSlots) * kSlotPieces * 16 + 32;
+            const int64_t base = static_cast<int64_t>(shift) - static_cast<int64_t>(16 * kChunkPieces) * c;
+            const uint32_t end = min(nst, (16 * kChunkPieces * (c + 1) - shift) / 32);
+            if (end > s_done) {
+                acc = quad_stripes_aligned<16, false, true>(
+                    reinterpret_cast<const uint64_t*>(slot + base + 32 * static_cast<int64_t>(s_done)) + j, end - s_done,
+                    acc);
+                s_done = end;
+            }
+            if (c == tail_chunk) {  // the tail's last byte is in this chunk, its first at most 31 before
+                const uint64_t* tp = reinterpret_cast<const uint64_t*>(slot + base + 32 * static_cast<int64_t>(nst));
+#pragma unroll
+                for (int q = 0; q < 4; ++q) tail[q] = tp[q];
             }
         }
-    } else if ((reinterpret_cast<uintptr_t>(src) & 7) == 0) {
-        acc = quad_stripes_aligned<16>(reinterpret_cast<const uint64_t*>(src) + j, nst, acc);
-    } else {
-        acc = quad_stripes_unaligned(src + 8 * j, nst, acc);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        if (threadIdx.x == 0) __hip_atomic_store(done, c + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    if (!staged) {
+        if ((reinterpret_cast<uintptr_t>(src) & 7) == 0)
+            acc = quad_stripes_aligned<16>(reinterpret_cast<const uint64_t*>(src) + j, nst, acc);
+        else
+            acc = quad_stripes_unaligned(src + 8 * j, nst, acc);
     }
     const uint64_t v1 = quad_bcast<0>(acc), v2 = quad_bcast<1>(acc), v3 = quad_bcast<2>(acc), v4 = quad_bcast<3>(acc);
     if (j == 0 && live) {
         const uint64_t h0 = (L >= 32) ? converge(v1, v2, v3, v4) : kP5;
-        emit(b, finish_fast(h0, L, s + 32 * static_cast<uint64_t>(nst), L & 31));
+        emit(b, staged ? finish_regs(h0, L, tail, L & 31)
+                       : finish_fast(h0, L, src + 32 * static_cast<uint64_t>(nst), L & 31));
     }
 }
 
@@ -656,8 +695,7 @@ __global__ __launch_bounds__(256) void k_xxh64_wide_multi(const uint8_t* __restr
                                                             const uint64_t* __restrict__ expected,
                                                             unsigned long long* __restrict__ first_bad,
                                                             unsigned long long* __restrict__ n_bad) {
-    static_assert(BPW * kMultiPieces * 16 + kPipeChunks * 4 <= 160 * 1024, "LDS");
-    __shared__ uint4 buf[BPW * kMultiPieces];
+    static_assert(BPW * kMultiPieces * 16 <= 160 * 1024, "LDS");
     const uint64_t first = static_cast<uint64_t>(blockIdx.x) * BPW;
     const uint32_t nlive = static_cast<uint32_t>(min<uint64_t>(BPW, n - first));
     auto src_of = [&](uint32_t b) {
@@ -676,9 +714,11 @@ __global__ __launch_bounds__(256) void k_xxh64_wide_multi(const uint8_t* __restr
         }
     };
     if constexpr (PIPE) {
-        __shared__ uint32_t ready[kPipeChunks];
-        multi_stage_hash_pipe<BPW, kMultiPieces>(buf, ready, nlive, src_of, emit);
+        __shared__ uint4 ring[BPW * kRingBlockPieces + kRingSlackPieces];
+        __shared__ uint32_t ready[kPipeMaxChunks], done[1];
+        multi_stage_hash_pipe<BPW>(ring, ready, done, nlive, src_of, emit);
     } else {
+        __shared__ uint4 buf[BPW * kMultiPieces];
         multi_stage_hash<BPW>(buf, nlive, src_of, emit);
     }
 }
@@ -1437,9 +1477,8 @@ __global__ __launch_bounds__(256) void k_commit_level_multi(uint8_t* __restrict_
                                                              uint64_t lo, uint64_t cnt,
                                                              uint64_t* __restrict__ out_cs) {
     constexpr uint32_t RW = sizeof(stormck_dirty_block) / 8;  // 7 words per record
-    static_assert(BPW * kMultiPieces * 16 + BPW * RW * 8 + kPipeChunks * 4 <= 160 * 1024, "LDS");
+    static_assert(BPW * kMultiPieces * 16 + BPW * RW * 8 <= 160 * 1024, "LDS");
     static_assert(BPW * RW <= 256, "one record word per thread");
-    __shared__ uint4 buf[BPW * kMultiPieces];
     __shared__ uint64_t rec_w[BPW * RW];
     const uint64_t first = static_cast<uint64_t>(blockIdx.x) * BPW;
     const uint32_t nlive = static_cast<uint32_t>(min<uint64_t>(BPW, cnt - first));
@@ -1460,9 +1499,11 @@ __global__ __launch_bounds__(256) void k_commit_level_multi(uint8_t* __restrict_
         }
     };
     if constexpr (PIPE) {
-        __shared__ uint32_t ready[kPipeChunks];
-        multi_stage_hash_pipe<BPW, kMultiPieces>(buf, ready, nlive, src_of, emit);
+        __shared__ uint4 ring[BPW * kRingBlockPieces + kRingSlackPieces];
+        __shared__ uint32_t ready[kPipeMaxChunks], done[1];
+        multi_stage_hash_pipe<BPW>(ring, ready, done, nlive, src_of, emit);
     } else {
+        __shared__ uint4 buf[BPW * kMultiPieces];
         multi_stage_hash<BPW>(buf, nlive, src_of, emit);
     }
 }

@@ -262,11 +262,13 @@ int launch_checksum(const uint8_t* base, uint64_t stride, const uint32_t* lens, 
         return !(e && e[0] == '0');
     }();
     const bool stage_pipe = pipe_staging();
+    // a uniform batch takes it when its blocks can be staged (pipelined: covers up to 64 KiB)
+    const uint64_t multi_pieces = stage_pipe ? uint64_t{kPipeMaxChunks} * kChunkPieces : kMultiPieces;
     const uint64_t ncu = cu_count();
     if (multi_on && ncu > 0 && n <= kMultiBpw * ncu &&
         (offs || lens ||
          ((reinterpret_cast<uintptr_t>(base) & 7) == 0 && (stride & 7) == 0 &&
-          ((reinterpret_cast<uintptr_t>(base) & 15) + len + 15) / 16 <= kMultiPieces))) {
+          ((reinterpret_cast<uintptr_t>(base) & 15) + len + 15) / 16 <= multi_pieces))) {
         const dim3 grid(static_cast<unsigned>((n + kMultiBpw - 1) / kMultiBpw));
 #define STORMCK_MULTI(LENS, OFFS, VER)                                                                         \
     do {                                                                                                      \

@@ -249,6 +249,47 @@ def test_uniform_fast_path_lengths(dev, length):
         del big
 
 
+@pytest.mark.parametrize("shift", [0, 8])
+def test_wide_multi_ring_long_blocks(dev, shift):
+    """Batches of up to 5 blocks per CU take k_xxh64_wide_multi, whose pipelined staging
+    streams each block through a 4-slot ring of 4 KiB chunks (kernels.h
+    multi_stage_hash_pipe). 700 blocks of random per-block lengths up to 64 KiB - 8
+    (covers of up to 16 chunks, stripes and tails straddling chunk and ring-wrap
+    boundaries, empty blocks), 16- and 8-byte-aligned starts; then uniform 32 KiB
+    blocks (storm's blob, a cover of 2,048 or 2,049 pieces); every block vs the C oracle,
+    and verify finds planted mismatches."""
+    from oracle import oracle as o
+    from storm_amd import engine
+    rng = np.random.default_rng(700 + shift)
+    n, stride = 700, 65552
+    lens = rng.integers(0, 65536 - 8, size=n).astype(np.uint32)
+    lens[:6] = [0, 1, 32, 4096 - shift, 4096 - shift + 31, 65536 - 16]
+    host = rng.integers(0, 256, size=shift + n * stride + 64, dtype=np.uint8)
+    d = torch.from_numpy(host).to(dev)
+    d_lens = torch.from_numpy(lens.view(np.int32)).to(dev)
+    out = torch.empty(n, dtype=torch.int64, device=dev)
+    engine.checksum_device(d.data_ptr() + shift, stride, n, out.data_ptr(), 0, d_lens.data_ptr())
+    torch.cuda.synchronize()
+    want = o.checksum_batch(host[shift:], n, stride, 0, lens=lens, threads=8)
+    bad = np.nonzero(_u64(out) != want)[0]
+    assert bad.size == 0, (shift, bad[:8], lens[bad[:8]])
+    m, L = 1200, 32768
+    blob = rng.integers(0, 256, size=shift + m * L + 64, dtype=np.uint8)
+    d2 = torch.from_numpy(blob).to(dev)
+    out2 = torch.empty(m, dtype=torch.int64, device=dev)
+    engine.checksum_device(d2.data_ptr() + shift, L, m, out2.data_ptr(), L)
+    torch.cuda.synchronize()
+    want2 = o.checksum_batch(blob[shift:], m, L, L, threads=8)
+    assert np.array_equal(_u64(out2), want2), shift
+    exp = want2.copy()
+    exp[[3, 777]] ^= np.uint64(1)
+    res = torch.zeros(2, dtype=torch.int64, device=dev)
+    engine.verify_device(d2.data_ptr() + shift, L, m, torch.from_numpy(exp.view(np.int64)).to(dev).data_ptr(),
+                         res.data_ptr(), L)
+    torch.cuda.synchronize()
+    assert _u64(res).tolist() == [3, 2]
+
+
 def test_mixed_c5(dev):
     from storm_amd import engine
     g = load_golden("mixed.json")
