@@ -329,16 +329,17 @@ struct BlockRef {
 // chunk, 3 stager waves. A slot holds 2 pieces of pre-pad (the previous chunk's last
 // 32 bytes) and the chunk, so a stripe or tail that starts in one chunk and ends in
 // the next reads contiguous bytes from the later chunk's slot. Blocks are
-// kRingBlockPieces = 2 (mod 16) pieces apart, so the 5 chains of a wave read distinct
+// ring_block_pieces(RS) = 2 (mod 16) pieces apart, so the 5 chains of a wave read distinct
 // LDS banks (as kMultiPieces below).
 constexpr uint32_t kChunkPieces = 256;
 constexpr uint32_t kPipeMaxChunks = 16;  // covers up to 64 KiB
 constexpr uint32_t kPipeStagers = 3;     // waves 1..3 of a 256-thread workgroup
-constexpr uint32_t kRingSlots = 4;  // 7 slots measured slower (profiles/r02_pipe/)
+constexpr uint32_t kRingSlots = 4;  // shipped ring depth (7 measured slower, profiles/r02_pipe/)
 constexpr uint32_t kSlotPieces = 2 + kChunkPieces;
-constexpr uint32_t kRingBlockPieces = 1042;  // >= kRingSlots * kSlotPieces, = 2 (mod 16)
-constexpr uint32_t kRingSlackPieces = 2;     // a 32-byte tail read past the last slot stays inside
-static_assert(kRingBlockPieces >= kRingSlots * kSlotPieces && kRingBlockPieces % 16 == 2, "ring layout");
+// pieces between two blocks' rings: >= RS slots, = 2 (mod 16)
+constexpr uint32_t ring_block_pieces(uint32_t rs) { return (rs * kSlotPieces + 13) / 16 * 16 + 2; }
+constexpr uint32_t kRingSlackPieces = 2;  // a 32-byte tail read past the last slot stays inside
+static_assert(ring_block_pieces(4) == 1042 && ring_block_pieces(7) == 1810, "ring layout");
 
 // Quad 0's part of k_xxh64_wide. Inlined once per branch, so the words are read with
 // ds_read from the staged copy and with global loads otherwise: through one generic
@@ -535,7 +536,7 @@ __device__ __forceinline__ void multi_stage_hash(uint4* buf, uint32_t nlive, Src
 // (< 32 bytes) in registers when it passes the tail's chunk, before the slot can be
 // reused. Blocks with 8-byte-aligned starts and covers up to 64 KiB are staged; others
 // hash from memory in the same lanes.
-// ring: BPW * kRingBlockPieces + kRingSlackPieces pieces; ready: kPipeMaxChunks words;
+// ring: BPW * ring_block_pieces(RS) + kRingSlackPieces pieces; ready: kPipeMaxChunks words;
 // done: one word. Same contract as multi_stage_hash otherwise.
 
 // Bounded: a chunk that never completes (a staging/chain disagreement would be a bug)
@@ -548,10 +549,11 @@ __device__ __forceinline__ void pipe_wait(const uint32_t* word, uint32_t at_leas
         __builtin_amdgcn_s_sleep(1);
 }
 
-template <int BPW, class Src, class Emit>
+template <int BPW, uint32_t RS, class Src, class Emit>
 __device__ __forceinline__ void multi_stage_hash_pipe(uint4* ring, uint32_t* ready, uint32_t* done, uint32_t nlive,
                                                       Src src_of, Emit emit) {
     constexpr uint32_t kMaxPieces = kPipeMaxChunks * kChunkPieces;
+    constexpr uint32_t kRingBlockPieces = ring_block_pieces(RS);
     const uint4* cover[BPW];
     uint32_t words[BPW], shift8[BPW], nw[BPW];
     uint32_t nch = 0;  // chunks of the longest staged block (uniform over the workgroup)
@@ -612,8 +614,8 @@ __device__ __forceinline__ void multi_stage_hash_pipe(uint4* ring, uint32_t* rea
         // address and is not stored)
         const uint32_t t = threadIdx.x - 64;
         for (uint32_t c = 1; c < nch; ++c) {
-            if (c >= kRingSlots) pipe_wait(done, c - kRingSlots + 1);  // the slot's old chunk is finished
-            const uint32_t slot = (c % kRingSlots) * kSlotPieces;
+            if (c >= RS) pipe_wait(done, c - RS + 1);  // the slot's old chunk is finished
+            const uint32_t slot = (c % RS) * kSlotPieces;
             uint4 r[BPW][2];
 #pragma unroll
             for (int b = 0; b < BPW; ++b)
@@ -654,7 +656,7 @@ __device__ __forceinline__ void multi_stage_hash_pipe(uint4* ring, uint32_t* rea
         if (c > 0) pipe_wait(ready + c, kPipeStagers);
         if (staged) {
             // slot byte of cover byte x of this chunk: 32 + x - 4096c
-            const uint8_t* slot = blk_ring + (c % kRingSlots) * kSlotPieces * 16 + 32;
+            const uint8_t* slot = blk_ring + (c % RS) * kSlotPieces * 16 + 32;
             const int64_t base = static_cast<int64_t>(shift) - static_cast<int64_t>(16 * kChunkPieces) * c;
             const uint32_t end = min(nst, (16 * kChunkPieces * (c + 1) - shift) / 32);
             if (end > s_done) {
@@ -686,8 +688,8 @@ __device__ __forceinline__ void multi_stage_hash_pipe(uint4* ring, uint32_t* rea
     }
 }
 
-// PIPE: the pipelined body (multi_stage_hash_pipe), else whole blocks staged first.
-template <bool LENS, bool OFFS, bool VERIFY, int BPW, bool PIPE = true>
+// RING: ring slots of the pipelined body (multi_stage_hash_pipe); 0 stages whole blocks first.
+template <bool LENS, bool OFFS, bool VERIFY, int BPW, uint32_t RING = kRingSlots>
 __global__ __launch_bounds__(256) void k_xxh64_wide_multi(const uint8_t* __restrict__ base, uint64_t stride,
                                                             const uint32_t* __restrict__ lens, uint32_t len,
                                                             const uint64_t* __restrict__ offs, uint64_t n,
@@ -713,10 +715,10 @@ __global__ __launch_bounds__(256) void k_xxh64_wide_multi(const uint8_t* __restr
             out[blk] = h;
         }
     };
-    if constexpr (PIPE) {
-        __shared__ uint4 ring[BPW * kRingBlockPieces + kRingSlackPieces];
+    if constexpr (RING > 0) {
+        __shared__ uint4 ring[BPW * ring_block_pieces(RING) + kRingSlackPieces];
         __shared__ uint32_t ready[kPipeMaxChunks], done[1];
-        multi_stage_hash_pipe<BPW>(ring, ready, done, nlive, src_of, emit);
+        multi_stage_hash_pipe<BPW, RING>(ring, ready, done, nlive, src_of, emit);
     } else {
         __shared__ uint4 buf[BPW * kMultiPieces];
         multi_stage_hash<BPW>(buf, nlive, src_of, emit);
@@ -1471,7 +1473,7 @@ __global__ __launch_bounds__(256) void k_commit_level_wide(uint8_t* __restrict__
 // blocks per workgroup staged premultiplied in one round trip, one chain wave. The
 // workgroup's BPW records (56 B each, possibly in pinned host memory) cross the bus
 // once, into LDS, before any block address is known.
-template <int BPW, bool PIPE = true>
+template <int BPW, uint32_t RING = kRingSlots>
 __global__ __launch_bounds__(256) void k_commit_level_multi(uint8_t* __restrict__ arena,
                                                              const stormck_dirty_block* __restrict__ blocks,
                                                              uint64_t lo, uint64_t cnt,
@@ -1498,10 +1500,10 @@ __global__ __launch_bounds__(256) void k_commit_level_multi(uint8_t* __restrict_
             arena[r.origin_type] = r.type;
         }
     };
-    if constexpr (PIPE) {
-        __shared__ uint4 ring[BPW * kRingBlockPieces + kRingSlackPieces];
+    if constexpr (RING > 0) {
+        __shared__ uint4 ring[BPW * ring_block_pieces(RING) + kRingSlackPieces];
         __shared__ uint32_t ready[kPipeMaxChunks], done[1];
-        multi_stage_hash_pipe<BPW>(ring, ready, done, nlive, src_of, emit);
+        multi_stage_hash_pipe<BPW, RING>(ring, ready, done, nlive, src_of, emit);
     } else {
         __shared__ uint4 buf[BPW * kMultiPieces];
         multi_stage_hash<BPW>(buf, nlive, src_of, emit);

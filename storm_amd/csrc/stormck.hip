@@ -206,14 +206,15 @@ uint64_t cu_count() {
     return static_cast<uint64_t>(v);
 }
 
-// Pipelined staging in the wide-multi kernels (kernels.h multi_stage_hash_pipe);
-// STORMCK_STAGE_PIPE=0 stages whole blocks first (A/B).
-bool pipe_staging() {
-    static const bool on = [] {
+// Ring depth of the pipelined staging in the wide-multi kernels (kernels.h
+// multi_stage_hash_pipe): kRingSlots; probe knob STORMCK_STAGE_PIPE=0 stages whole blocks
+// first (A/B). 6- and 7-slot rings were measured slower.
+uint32_t pipe_staging() {
+    static const uint32_t slots = [] {
         const char* e = std::getenv("STORMCK_STAGE_PIPE");
-        return !(e && e[0] == '0');
+        return (e && e[0] == '0') ? 0u : kRingSlots;
     }();
-    return on;
+    return slots;
 }
 
 bool grid_for(uint64_t threads, dim3* grid) {
@@ -261,9 +262,9 @@ int launch_checksum(const uint8_t* base, uint64_t stride, const uint32_t* lens, 
         const char* e = std::getenv("STORMCK_WIDE_MULTI");  // probe knob: "0" disables
         return !(e && e[0] == '0');
     }();
-    const bool stage_pipe = pipe_staging();
+    const uint32_t ring_slots = pipe_staging();
     // a uniform batch takes it when its blocks can be staged (pipelined: covers up to 64 KiB)
-    const uint64_t multi_pieces = stage_pipe ? uint64_t{kPipeMaxChunks} * kChunkPieces : kMultiPieces;
+    const uint64_t multi_pieces = ring_slots ? uint64_t{kPipeMaxChunks} * kChunkPieces : kMultiPieces;
     const uint64_t ncu = cu_count();
     if (multi_on && ncu > 0 && n <= kMultiBpw * ncu &&
         (offs || lens ||
@@ -272,11 +273,11 @@ int launch_checksum(const uint8_t* base, uint64_t stride, const uint32_t* lens, 
         const dim3 grid(static_cast<unsigned>((n + kMultiBpw - 1) / kMultiBpw));
 #define STORMCK_MULTI(LENS, OFFS, VER)                                                                         \
     do {                                                                                                      \
-        if (stage_pipe)                                                                                       \
-            hipLaunchKernelGGL((k_xxh64_wide_multi<LENS, OFFS, VER, kMultiBpw, true>), grid, dim3(kThreads), 0, \
-                               st, base, stride, lens, len, offs, n, out, expected, first_bad, n_bad);        \
+        if (ring_slots)                                                                                       \
+            hipLaunchKernelGGL((k_xxh64_wide_multi<LENS, OFFS, VER, kMultiBpw, kRingSlots>), grid, dim3(kThreads), \
+                               0, st, base, stride, lens, len, offs, n, out, expected, first_bad, n_bad);     \
         else                                                                                                  \
-            hipLaunchKernelGGL((k_xxh64_wide_multi<LENS, OFFS, VER, kMultiBpw, false>), grid, dim3(kThreads), 0, \
+            hipLaunchKernelGGL((k_xxh64_wide_multi<LENS, OFFS, VER, kMultiBpw, 0>), grid, dim3(kThreads), 0,    \
                                st, base, stride, lens, len, offs, n, out, expected, first_bad, n_bad);        \
     } while (0)
         if (!verify) {
@@ -1415,11 +1416,12 @@ int stormck_commit_device(void* d_arena, stormck_dirty_block* blocks, uint64_t n
         } else if (commit_multi && ncu > 0 && cnt <= kMultiBpw * ncu) {
             // up to kMultiBpw blocks per CU (a storm commit's leaves): wide-multi staging
             const dim3 grid(static_cast<unsigned>((cnt + kMultiBpw - 1) / kMultiBpw));
-            if (pipe_staging())
-                hipLaunchKernelGGL((k_commit_level_multi<kMultiBpw, true>), grid, dim3(kThreads), 0, st,
+            const uint32_t ring_slots = pipe_staging();
+            if (ring_slots)
+                hipLaunchKernelGGL((k_commit_level_multi<kMultiBpw, kRingSlots>), grid, dim3(kThreads), 0, st,
                                    static_cast<uint8_t*>(d_arena), d_blocks, lo, cnt, d_cs);
             else
-                hipLaunchKernelGGL((k_commit_level_multi<kMultiBpw, false>), grid, dim3(kThreads), 0, st,
+                hipLaunchKernelGGL((k_commit_level_multi<kMultiBpw, 0>), grid, dim3(kThreads), 0, st,
                                    static_cast<uint8_t*>(d_arena), d_blocks, lo, cnt, d_cs);
         } else {
             dim3 grid;
