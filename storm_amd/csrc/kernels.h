@@ -697,7 +697,9 @@ __global__ __launch_bounds__(256) void k_xxh64_wide_multi(const uint8_t* __restr
                                                             const uint64_t* __restrict__ expected,
                                                             unsigned long long* __restrict__ first_bad,
                                                             unsigned long long* __restrict__ n_bad) {
-    static_assert(BPW * kMultiPieces * 16 <= 160 * 1024, "LDS");
+    static_assert(RING > 0 ? (BPW * ring_block_pieces(RING) + kRingSlackPieces) * 16 <= 150 * 1024
+                           : BPW * kMultiPieces * 16 <= 160 * 1024,
+                  "LDS");
     const uint64_t first = static_cast<uint64_t>(blockIdx.x) * BPW;
     const uint32_t nlive = static_cast<uint32_t>(min<uint64_t>(BPW, n - first));
     auto src_of = [&](uint32_t b) {
@@ -1479,7 +1481,9 @@ __global__ __launch_bounds__(256) void k_commit_level_multi(uint8_t* __restrict_
                                                              uint64_t lo, uint64_t cnt,
                                                              uint64_t* __restrict__ out_cs) {
     constexpr uint32_t RW = sizeof(stormck_dirty_block) / 8;  // 7 words per record
-    static_assert(BPW * kMultiPieces * 16 + BPW * RW * 8 <= 160 * 1024, "LDS");
+    static_assert(RING > 0 ? (BPW * ring_block_pieces(RING) + kRingSlackPieces) * 16 + BPW * RW * 8 <= 150 * 1024
+                           : BPW * kMultiPieces * 16 + BPW * RW * 8 <= 160 * 1024,
+                  "LDS");
     static_assert(BPW * RW <= 256, "one record word per thread");
     __shared__ uint64_t rec_w[BPW * RW];
     const uint64_t first = static_cast<uint64_t>(blockIdx.x) * BPW;

@@ -135,6 +135,7 @@ constexpr unsigned kGldsThreads = 64 * kGldsWaves;
 constexpr unsigned kGldsBlocks = 16 * kGldsWaves;
 constexpr int kAuxNT = 2;
 constexpr uint64_t kMultiBpw = 5;          // blocks per workgroup of k_xxh64_wide_multi
+constexpr uint64_t kMultiBpwRing = 8;      // ring staging, batches above kMultiBpw per CU (133 KiB of LDS)
 constexpr uint64_t kWideBatch = 128;      // batches up to this many blocks: k_xxh64_wide
 constexpr uint64_t kCommitWide = 256;     // f1 levels up to this many blocks: k_commit_level_wide
 constexpr uint64_t kStreamBatch = 16384;  // f1 commit levels from this many blocks: k_commit_level_glds
@@ -217,6 +218,18 @@ uint32_t pipe_staging() {
     return slots;
 }
 
+// Blocks per workgroup of the wide-multi kernels for a batch of n on ncu CUs: kMultiBpw
+// up to kMultiBpw per CU; with ring staging, kMultiBpwRing up to that many per CU. One
+// wave walks all of a workgroup's chains, so 8 cost about what 5 do (1,600 / 2,048 blocks:
+// 24.2 / 25.4 us against 34.5 / 34.8 on the quad kernel); at or below 5 per CU the
+// 5-block workgroups are about 1 us faster (profiles/r02_pipe/bpw_ab/). 0: not this kernel.
+uint64_t multi_bpw(uint64_t n, uint64_t ncu) {
+    if (ncu == 0) return 0;
+    if (n <= kMultiBpw * ncu) return kMultiBpw;
+    if (pipe_staging() && n <= kMultiBpwRing * ncu) return kMultiBpwRing;
+    return 0;
+}
+
 bool grid_for(uint64_t threads, dim3* grid) {
     const uint64_t blocks = (threads + kThreads - 1) / kThreads;
     if (blocks == 0 || blocks > 0x7fffffffULL) return false;
@@ -256,8 +269,8 @@ int launch_checksum(const uint8_t* base, uint64_t stride, const uint32_t* lens, 
         HIP_TRY(hipGetLastError());
         return STORMCK_OK;
     }
-    // up to kMultiBpw blocks per CU: k_xxh64_wide_multi, one workgroup per CU staging
-    // kMultiBpw premultiplied blocks (the c5 commit batch is one such launch)
+    // up to 5 blocks per CU (8 with ring staging): k_xxh64_wide_multi, one workgroup per
+    // CU staging 5 (8) premultiplied blocks (the c5 commit batch is one such launch)
     static const bool multi_on = [] {
         const char* e = std::getenv("STORMCK_WIDE_MULTI");  // probe knob: "0" disables
         return !(e && e[0] == '0');
@@ -266,15 +279,19 @@ int launch_checksum(const uint8_t* base, uint64_t stride, const uint32_t* lens, 
     // a uniform batch takes it when its blocks can be staged (pipelined: covers up to 64 KiB)
     const uint64_t multi_pieces = ring_slots ? uint64_t{kPipeMaxChunks} * kChunkPieces : kMultiPieces;
     const uint64_t ncu = cu_count();
-    if (multi_on && ncu > 0 && n <= kMultiBpw * ncu &&
+    const uint64_t bpw = multi_bpw(n, ncu);
+    if (multi_on && bpw > 0 &&
         (offs || lens ||
          ((reinterpret_cast<uintptr_t>(base) & 7) == 0 && (stride & 7) == 0 &&
           ((reinterpret_cast<uintptr_t>(base) & 15) + len + 15) / 16 <= multi_pieces))) {
-        const dim3 grid(static_cast<unsigned>((n + kMultiBpw - 1) / kMultiBpw));
+        const dim3 grid(static_cast<unsigned>((n + bpw - 1) / bpw));
 #define STORMCK_MULTI(LENS, OFFS, VER)                                                                         \
     do {                                                                                                      \
-        if (ring_slots)                                                                                       \
+        if (ring_slots && bpw == kMultiBpw)                                                                   \
             hipLaunchKernelGGL((k_xxh64_wide_multi<LENS, OFFS, VER, kMultiBpw, kRingSlots>), grid, dim3(kThreads), \
+                               0, st, base, stride, lens, len, offs, n, out, expected, first_bad, n_bad);     \
+        else if (ring_slots)                                                                                  \
+            hipLaunchKernelGGL((k_xxh64_wide_multi<LENS, OFFS, VER, kMultiBpwRing, kRingSlots>), grid, dim3(kThreads), \
                                0, st, base, stride, lens, len, offs, n, out, expected, first_bad, n_bad);     \
         else                                                                                                  \
             hipLaunchKernelGGL((k_xxh64_wide_multi<LENS, OFFS, VER, kMultiBpw, 0>), grid, dim3(kThreads), 0,    \
@@ -1413,12 +1430,16 @@ int stormck_commit_device(void* d_arena, stormck_dirty_block* blocks, uint64_t n
             // one workgroup per block, premultiplied staging: the chain wave is alone on its SIMD
             hipLaunchKernelGGL(k_commit_level_wide, dim3(static_cast<unsigned>(cnt)), dim3(kThreads), 0, st,
                                static_cast<uint8_t*>(d_arena), d_blocks, lo, d_cs);
-        } else if (commit_multi && ncu > 0 && cnt <= kMultiBpw * ncu) {
-            // up to kMultiBpw blocks per CU (a storm commit's leaves): wide-multi staging
-            const dim3 grid(static_cast<unsigned>((cnt + kMultiBpw - 1) / kMultiBpw));
+        } else if (commit_multi && multi_bpw(cnt, ncu) > 0) {
+            // up to 5 (ring staging: 8) blocks per CU (a storm commit's leaves): wide-multi staging
+            const uint64_t bpw = multi_bpw(cnt, ncu);
+            const dim3 grid(static_cast<unsigned>((cnt + bpw - 1) / bpw));
             const uint32_t ring_slots = pipe_staging();
-            if (ring_slots)
+            if (ring_slots && bpw == kMultiBpw)
                 hipLaunchKernelGGL((k_commit_level_multi<kMultiBpw, kRingSlots>), grid, dim3(kThreads), 0, st,
+                                   static_cast<uint8_t*>(d_arena), d_blocks, lo, cnt, d_cs);
+            else if (ring_slots)
+                hipLaunchKernelGGL((k_commit_level_multi<kMultiBpwRing, kRingSlots>), grid, dim3(kThreads), 0, st,
                                    static_cast<uint8_t*>(d_arena), d_blocks, lo, cnt, d_cs);
             else
                 hipLaunchKernelGGL((k_commit_level_multi<kMultiBpw, 0>), grid, dim3(kThreads), 0, st,
