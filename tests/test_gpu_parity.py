@@ -249,19 +249,20 @@ def test_uniform_fast_path_lengths(dev, length):
         del big
 
 
-@pytest.mark.parametrize("shift", [0, 8])
-def test_wide_multi_ring_long_blocks(dev, shift):
+@pytest.mark.parametrize("shift,n", [(0, 700), (8, 700), (8, 1900), (0, 3500)])
+def test_wide_multi_ring_long_blocks(dev, shift, n):
     """Batches of up to 5 blocks per CU take k_xxh64_wide_multi, whose pipelined staging
     streams each block through a 4-slot ring of 4 KiB chunks (kernels.h
-    multi_stage_hash_pipe). 700 blocks of random per-block lengths up to 64 KiB - 8
+    multi_stage_hash_pipe). 700 (5 per CU) or 1,900 (8 per CU) blocks, and 3,500 (the
+    register-quad kernel, for comparison), of random per-block lengths up to 64 KiB - 8
     (covers of up to 16 chunks, stripes and tails straddling chunk and ring-wrap
     boundaries, empty blocks), 16- and 8-byte-aligned starts; then uniform 32 KiB
     blocks (storm's blob, a cover of 2,048 or 2,049 pieces); every block vs the C oracle,
     and verify finds planted mismatches."""
     from oracle import oracle as o
     from storm_amd import engine
-    rng = np.random.default_rng(700 + shift)
-    n, stride = 700, 65552
+    rng = np.random.default_rng(n + shift)
+    stride = 65552
     lens = rng.integers(0, 65536 - 8, size=n).astype(np.uint32)
     lens[:6] = [0, 1, 32, 4096 - shift, 4096 - shift + 31, 65536 - 16]
     host = rng.integers(0, 256, size=shift + n * stride + 64, dtype=np.uint8)
