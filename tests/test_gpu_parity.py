@@ -274,6 +274,13 @@ def test_wide_multi_ring_long_blocks(dev, shift, n):
     want = o.checksum_batch(host[shift:], n, stride, 0, lens=lens, threads=8)
     bad = np.nonzero(_u64(out) != want)[0]
     assert bad.size == 0, (shift, bad[:8], lens[bad[:8]])
+    exp = want.copy()
+    exp[[5, n - 1]] ^= np.uint64(1)
+    res = torch.zeros(2, dtype=torch.int64, device=dev)
+    engine.verify_device(d.data_ptr() + shift, stride, n, torch.from_numpy(exp.view(np.int64)).to(dev).data_ptr(),
+                         res.data_ptr(), 0, d_lens.data_ptr())
+    torch.cuda.synchronize()
+    assert _u64(res).tolist() == [5, 2], (shift, n)
     m, L = 1200, 32768
     blob = rng.integers(0, 256, size=shift + m * L + 64, dtype=np.uint8)
     d2 = torch.from_numpy(blob).to(dev)
