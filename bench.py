@@ -97,7 +97,12 @@ def settle(step, seconds: float, group_dev=None):
             torch.cuda.synchronize()
 
 
-def measured_read_peak(arena, arena_n: int, stream, achieved: float):
+def va_alignment(ptr: int) -> int:
+    """Largest power of two (up to 2^40) that divides a virtual address."""
+    return min(ptr & -ptr, 1 << 40) if ptr else 0
+
+
+def measured_read_peak(arena_ptr: int, arena_n: int, stream, achieved: float):
     """The shipped kernel's data movement with the hash replaced by xor
     (tools/libreadpeak.so), 3 launches on the bench's own arena, timed with HIP events
     on the launch stream. None if the measurement library is not built."""
@@ -111,12 +116,12 @@ def measured_read_peak(arena, arena_n: int, stream, achieved: float):
     fn = lib.readpeak_xor_skew
     fn.restype = ctypes.c_int
     fn.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]
-    sink = torch.empty(arena_n, dtype=torch.int64, device=arena.device)
+    sink = torch.empty(arena_n, dtype=torch.int64, device=stream.device)
     ms = []
     for r in range(4):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(stream)
-        if fn(arena.data_ptr(), BLOCK, BLOCK, arena_n, sink.data_ptr(), stream.cuda_stream) != 0:
+        if fn(arena_ptr, BLOCK, BLOCK, arena_n, sink.data_ptr(), stream.cuda_stream) != 0:
             return None
         e1.record(stream)
         torch.cuda.synchronize()
@@ -124,7 +129,7 @@ def measured_read_peak(arena, arena_n: int, stream, achieved: float):
             ms.append(e0.elapsed_time(e1))
     gbs = arena_n * (BLOCK + 8) / (sum(ms) / len(ms) * 1e-3) / 1e9
     return {"GB/s": round(gbs, 1), "frac": round(achieved / gbs, 4),
-            "kernel": "k_xxh64_glds_skew<16,nt,8w,4KiB> data movement with the hash replaced by xor "
+            "kernel": KERNEL + " data movement with the hash replaced by xor "
                       "(tools/readpeak.hip), 3 launches on the same arena after the timed region"}
 
 
@@ -548,6 +553,10 @@ def block_checksum_workload(a) -> int:
         else:
             dist.init_process_group("gloo")
     engine.init(gpu)
+    if distributed:
+        # what the process group actually formed (the driver's N > 1 line must show it)
+        group = {"world_size": dist.get_world_size(), "backend": str(dist.get_backend()),
+                 "device_count": torch.cuda.device_count(), "device": gpu}
 
     # c3 at N = 1 (16M blocks); c4 at N > 1 (64M blocks in contiguous shards, strong
     # scaling: 8M per GPU at N = 8). --blocks B: B per GPU instead (weak scaling).
@@ -563,7 +572,10 @@ def block_checksum_workload(a) -> int:
     stream = torch.cuda.current_stream(dev)
     st = stream.cuda_stream
 
-    arena = torch.empty((arena_n, BLOCK), dtype=torch.uint8, device=dev)
+    # The arena is the process's first device allocation (at N > 1, after RCCL's own
+    # buffers), taken by plain hipMalloc through the library rather than torch's caching
+    # allocator, so a profiled and a plain process place it the same way.
+    arena_ptr = engine.device_alloc(arena_n * BLOCK)
     cs = torch.empty(n_gpu, dtype=torch.int64, device=dev)
     ws = torch.empty(max(engine.merkle_workspace_bytes(n_gpu, FANOUT) // 8, 1), dtype=torch.int64, device=dev)
     torch.cuda.synchronize()
@@ -584,13 +596,13 @@ def block_checksum_workload(a) -> int:
             f = ev_pair() if record else None
             if f:
                 f[0].record(stream)
-            engine.fill_synthetic_device(arena.data_ptr(), BLOCK, cnt, lo + first, SYNTH_SEED, st)
+            engine.fill_synthetic_device(arena_ptr, BLOCK, cnt, lo + first, SYNTH_SEED, st)
             e = ev_pair() if record else None
             if f:
                 f[1].record(stream)
                 fill_ev.append(f)
                 e[0].record(stream)
-            engine.checksum_device(arena.data_ptr(), BLOCK, cnt, cs[first:].data_ptr(), BLOCK, 0, st)
+            engine.checksum_device(arena_ptr, BLOCK, cnt, cs[first:].data_ptr(), BLOCK, 0, st)
             if e:
                 e[1].record(stream)
                 hash_ev.append((e[0], e[1], cnt))
@@ -616,15 +628,24 @@ def block_checksum_workload(a) -> int:
     wall = t1 - t0
     fill_s = sum(f0.elapsed_time(f1) for f0, f1 in fill_ev) * 1e-3
     elapsed = wall - fill_s  # the K steps without the arena regeneration
-    if distributed:
-        t = torch.tensor([elapsed, wall], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, wall = float(t[0].item()), float(t[1].item())
-
     # dominant kernel: per-launch durations from HIP events on its stream
     kms = sorted(e0.elapsed_time(e1) for (e0, e1, _) in hash_ev)
     kblocks = [c for (_, _, c) in hash_ev]
     avg_ms = sum(kms) / len(kms)
+    ranks = None
+    if distributed:
+        # every rank's step time and kernel launches; the MAX step time sets `value`
+        tdev = dev if a.dist_backend == "nccl" else "cpu"  # gloo all-gathers host tensors
+        mine = torch.tensor([elapsed, wall, avg_ms, kms[0], kms[-1], float(rank)], dtype=torch.float64, device=tdev)
+        allr = [torch.empty_like(mine) for _ in range(world)]
+        dist.all_gather(allr, mine)
+        rows = [[float(x) for x in r.cpu().tolist()] for r in allr]
+        slow = max(range(world), key=lambda r: rows[r][0])
+        elapsed, wall = rows[slow][0], max(r[1] for r in rows)
+        ranks = {"slowest_rank": slow,
+                 "per_rank": [{"rank": int(r[5]), "ms_per_step": round(r[0] / a.steps * 1e3, 3),
+                               "kernel_avg_ms": round(r[2], 4), "kernel_min_ms": round(r[3], 4),
+                               "kernel_max_ms": round(r[4], 4)} for r in rows]}
     avg_blocks = sum(kblocks) / len(kblocks)
     alg_bytes = avg_blocks * (BLOCK + 8)          # L bytes read + 8 bytes written per block
     achieved = alg_bytes / (avg_ms * 1e-3) / 1e9  # GB/s (decimal, like the spec peak)
@@ -641,12 +662,12 @@ def block_checksum_workload(a) -> int:
             # the committed rocprofv3 session this line's frac can be recomputed from
             # (tools/collect_profile.py): its kernel-trace average and the frac it implies
             prof = {k: tj.get(k) for k in ("source", "profile_calls", "profile_avg_launch_ms", "profile_frac",
-                                           "traffic_over_algorithmic")}
+                                           "traffic_over_algorithmic", "placement_spread")}
 
     # also report against a measured stream-read peak. Measured here, after
     # the timed region, on the same arena: the rate depends on where the arena lands in
     # HBM, so a peak from another process or box would not compare.
-    read_peak = measured_read_peak(arena, arena_n, stream, achieved)
+    read_peak = measured_read_peak(arena_ptr, arena_n, stream, achieved)
 
     gather = ""
     if distributed:
@@ -673,6 +694,10 @@ def block_checksum_workload(a) -> int:
                        "total_blocks": n_total, "blocks_per_gpu": n_gpu, "block_bytes": BLOCK,
                        "arena_blocks": arena_n, "passes_per_step": passes,
                        "parallelism": f"dp{world} (contiguous block ranges)",
+                       "arena": {"va": "0x%x" % arena_ptr, "va_alignment": va_alignment(arena_ptr),
+                                 "bytes": arena_n * BLOCK,
+                                 "alloc": "hipMalloc (stormck_device_alloc), the process's first device allocation"
+                                          + (" after the process group's" if distributed else "")},
                        "timed": "K steps between barrier + synchronize, minus the on-device regeneration of "
                                 "each arena pass (its own HIP events)",
                        "ms_per_step_with_regeneration": round(wall / a.steps * 1e3, 3)},
@@ -680,18 +705,24 @@ def block_checksum_workload(a) -> int:
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "kernel": KERNEL, "avg_launch_ms": round(avg_ms, 4),
                          "launch_ms": {"n": len(kms), "min": round(kms[0], 4),
-                                       "median": round(kms[len(kms) // 2], 4), "max": round(kms[-1], 4)},
+                                       "median": round(kms[len(kms) // 2], 4), "max": round(kms[-1], 4),
+                                       "in_order": [round(e0.elapsed_time(e1), 3) for (e0, e1, _) in hash_ev]},
                          "algorithmic_bytes_per_launch": int(alg_bytes), "profile_source": prof,
                          "measured_read_peak": read_peak},
             "root": "0x%016x" % root_t[0],
             "root_pointer": ["0x%016x" % v for v in root_t[:3]] + [root_t[3]],
             "root_check": check,
         }
+        if distributed:
+            res["config"]["process_group"] = group
+            res["ranks"] = ranks
         if world == 1 and not a.no_cpu:
             res["cpu_baseline"] = cpu_baseline(a.cpu_seconds)
         print(json.dumps(res), flush=True)
     if distributed:
         dist.destroy_process_group()
+    torch.cuda.synchronize()
+    engine.device_free(arena_ptr)
     return rc
 
 

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define STORMCK_ABI_VERSION 1
+#define STORMCK_ABI_VERSION 2
 
 #define STORMCK_OK 0
 #define STORMCK_EINVAL (-1)  /* bad argument (null pointer, n/len/stride out of range, ...) */
@@ -71,6 +71,22 @@ int stormck_device_count(int* count);
 int stormck_init(int device);
 /* Free pinned staging / device buffers of every context. */
 void stormck_shutdown(void);
+/* Ring-kernel faults. The small-batch kernels stage blocks through an LDS ring whose
+ * waits are bounded; a wait that expires (a liveness bug, never expected) is an error,
+ * not a value: the kernel writes no checksum (and reports no mismatch) for the blocks
+ * of the stalled workgroup and records a fault for the device. Host-synchronous entry
+ * points (_host, _host_multi, stormck_commit_device, stormck_read_verify_fd) check it
+ * after their sync and return STORMCK_EHIP naming the kernel; their outputs are then
+ * unspecified. For the asynchronous _device entry points, stormck_device_status
+ * synchronises `stream` and returns STORMCK_EHIP if any ring kernel on the calling
+ * thread's current device faulted since the last check (the fault is then cleared),
+ * otherwise the stream's own status. */
+int stormck_device_status(void* stream);
+/* Device memory for a block arena (storm's cache.data mirrored in HBM) on the calling
+ * thread's current device: plain hipMalloc, outside any caching allocator, so an arena
+ * taken first in a process is placed the same way whatever else the process allocates. */
+int stormck_device_alloc(uint64_t bytes, void** d_ptr);
+int stormck_device_free(void* d_ptr);
 
 /* ---- hot path: batch checksums of device-resident blocks -------------------
  * Block i starts at d_base + i*stride and is (d_lens ? d_lens[i] : len) bytes

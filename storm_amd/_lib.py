@@ -46,6 +46,9 @@ SIGNATURES = {
     "stormck_device_count": (c_int, [POINTER(c_int)]),
     "stormck_init": (c_int, [c_int]),
     "stormck_shutdown": (None, []),
+    "stormck_device_status": (c_int, [c_void_p]),
+    "stormck_device_alloc": (c_int, [c_uint64, POINTER(c_void_p)]),
+    "stormck_device_free": (c_int, [c_void_p]),
     "stormck_checksum_device": (c_int, [c_void_p, c_uint64, c_void_p, c_uint32, c_uint64, c_void_p, c_void_p]),
     "stormck_checksum_gather_device": (c_int, [c_void_p, c_void_p, c_void_p, c_uint32, c_uint64, c_void_p, c_void_p]),
     "stormck_verify_device": (c_int, [c_void_p, c_uint64, c_void_p, c_uint32, c_uint64, c_void_p, c_void_p, c_void_p]),

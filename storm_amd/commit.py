@@ -113,3 +113,151 @@ def pointer_forest(n_leaves: int, leaf_lens, fanout: int, slot: int = 32768, rev
         ex = np.asarray(existing, dtype=bool)
         b["birth_revision"][ex] = revision  # born in an earlier revision -> relocated on commit
     return b, (total + 1) * slot, last
+
+
+# ---------------------------------------------------------------------------
+# storm's Cache.commitData on the GPU: the Python mirror of the Go binding
+# integration/go/cache/commit_stormck.go (same steps, same order, same errors).
+# ---------------------------------------------------------------------------
+#
+# The caller is storm's cache (cache/cache.go:16-53) with the stormck patch
+# (integration/go/cache/trace_types.patch): every blockMetadata whose PostCommitFunc is
+# set also records what that closure captured, as
+#   meta.commit_origin  BlockOrigin (where the parent keeps this block's Pointer/type)
+#   meta.commit_parent  parentBlockMeta (the block holding the origin, or None)
+#   meta.commit_size    unsafe.Sizeof(T) of the block (the bytes BlockChecksum hashes)
+#   meta.commit_type    the BlockType the closure stores (Leaf / Pointer)
+# and the cache exposes what commitData touches: .dirty (the dirty set), .data
+# (cache.data), .blocks' .data / .address / .birth_revision / .n_commits /
+# .n_references / .state / .post_commit, .origin_offsets(origin) -> (pointer, type)
+# offsets into cache.data or None (the singularity), .write_origin(...),
+# .revision() / .last_allocated() / .set_last_allocated(v), .store.write_block(addr,
+# bytes) and .find_cached_block(addr, birth).
+
+USED_STATE, INVALID_STATE = 1, 2  # cache/types.go:10-15
+
+
+class StillReferenced(RuntimeError):
+    """A dirty block keeps NReferences > 0 after all its dirty children commit: storm's
+    commitData (cache/cache.go:88-90) would sweep forever; the binding refuses."""
+
+
+def cache_records(cache):
+    """The dirty forest as stormck_dirty_block records (commit_stormck.go collectDirty).
+
+    Records: the dirty set in its iteration order, then every ancestor reached through a
+    recorded parent that is not in it yet (storm adds those to the dirty set only when a
+    child's PostCommitFunc runs, trace.go:278-281,302-305). Returns (records, metas in
+    record order, indices of records whose origin lies outside cache.data)."""
+    metas = list(cache.dirty)
+    index = {id(m): i for i, m in enumerate(metas)}
+    k = 0
+    while k < len(metas):
+        m = metas[k]
+        p = m.commit_parent if m.post_commit is not None else None
+        if p is not None and id(p) not in index:
+            index[id(p)] = len(metas)
+            metas.append(p)
+        k += 1
+    recs = np.zeros(len(metas), dtype=DIRTY_DTYPE)
+    external = []
+    for i, m in enumerate(metas):
+        r = recs[i]
+        r["data_offset"] = m.data
+        r["address"] = m.address
+        r["birth_revision"] = m.birth_revision
+        r["origin_pointer"] = NO_ORIGIN
+        r["origin_type"] = NO_ORIGIN
+        r["parent"] = NO_PARENT
+        if m.post_commit is None:  # committed and written, nothing stored anywhere
+            continue
+        r["length"] = m.commit_size
+        r["type"] = m.commit_type
+        off = cache.origin_offsets(m.commit_origin)
+        if off is None:
+            external.append(i)  # the singularity's SpacePointer: stored by the host afterwards
+        else:
+            r["origin_pointer"], r["origin_type"] = off
+        if m.commit_parent is not None:
+            r["parent"] = index[id(m.commit_parent)]
+    return recs, metas, external
+
+
+def commit_heights(recs: np.ndarray) -> np.ndarray:
+    """Height of every record above the blocks with no dirty child (the library's level:
+    stormck_commit_device commits height 0, then 1, ... in record order)."""
+    n = len(recs)
+    h = np.zeros(n, dtype=np.int64)
+    par = recs["parent"]
+    for i in range(n):
+        cur, d, steps = i, 0, 0
+        while par[cur] >= 0:
+            cur = int(par[cur])
+            d += 1
+            steps += 1
+            if steps > n:
+                raise ValueError("parent links form a cycle")
+            if h[cur] >= d:
+                break
+            h[cur] = d
+    return h
+
+
+def check_references(metas, recs: np.ndarray, heights: np.ndarray) -> None:
+    """storm's reference accounting over the whole forest, before anything changes: a
+    child's PostCommitFunc lowers its parent's NReferences by the child's NCommits and
+    adds them to the parent's (trace.go:278-281), so in children-first order every block
+    must reach NReferences == 0 (cache.go:88-90)."""
+    refs = [m.n_references for m in metas]
+    commits = [m.n_commits for m in metas]
+    for i in np.argsort(heights, kind="stable"):
+        if refs[i] != 0:
+            raise StillReferenced(f"dirty block at address {metas[i].address} keeps {refs[i]} references")
+        p = int(recs["parent"][i])
+        if p >= 0:
+            refs[p] -= commits[i]
+            commits[p] += commits[i]
+
+
+def commit_cache(cache, run_commit) -> np.ndarray:
+    """Cache.commitData through the level-synchronous commit (cache/cache.go:87-137).
+
+    run_commit(records, revision, last_allocated) -> (checksums, last_allocated) runs
+    stormck_commit_device on cache.data (in Go: blocks.CommitBatch over the registered
+    arena), updating records' address / birth_revision in place. Then, as storm's loop
+    leaves them: the relocations into the metadata and LastAllocatedBlock, the root's
+    Pointer into the singularity, every block written at its address, NCommits /
+    NReferences zero, PostCommitFuncs consumed, and each relocated block's Data swapped
+    into the slot of its new address (cache.go:96-107), in commit order. Returns the
+    checksums in record order."""
+    recs, metas, external = cache_records(cache)
+    if len(metas) == 0:
+        return np.zeros(0, dtype=np.uint64)
+    heights = commit_heights(recs)
+    check_references(metas, recs, heights)
+    before = recs["address"].copy()
+    cs, last = run_commit(recs, cache.revision(), cache.last_allocated())
+    cache.set_last_allocated(last)
+    order = np.lexsort((np.arange(len(metas)), heights))  # the library's commit order
+    for i in order:
+        m = metas[i]
+        m.address = int(recs["address"][i])
+        m.birth_revision = int(recs["birth_revision"][i])
+    for i in external:
+        m = metas[i]
+        cache.write_origin(m.commit_origin, int(cs[i]), m.address, m.birth_revision, int(recs["type"][i]))
+    for i in order:
+        m = metas[i]
+        cache.store.write_block(m.address, cache.data[m.data:m.data + cache.bs])
+        cache.dirty.pop(m, None)
+        m.post_commit = None
+        m.n_commits = 0
+        m.n_references = 0
+    for i in order:
+        m = metas[i]
+        if m.address != int(before[i]):
+            m.state = INVALID_STATE
+            m2 = cache.find_cached_block(m.address, m.birth_revision)
+            m2.state = USED_STATE
+            m2.data, m.data = m.data, m2.data
+    return cs

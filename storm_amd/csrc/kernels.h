@@ -539,19 +539,53 @@ __device__ __forceinline__ void multi_stage_hash(uint4* buf, uint32_t nlive, Src
 // ring: BPW * ring_block_pieces(RS) + kRingSlackPieces pieces; ready: kPipeMaxChunks words;
 // done: one word. Same contract as multi_stage_hash otherwise.
 
-// Bounded: a chunk that never completes (a staging/chain disagreement would be a bug)
-// gives a wrong checksum after ~0.1 s of polling, which the parity tests report,
-// instead of a wave that never exits.
-__device__ __forceinline__ void pipe_wait(const uint32_t* word, uint32_t at_least) {
-    for (uint32_t spin = 0;
-         __hip_atomic_load(word, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < at_least && spin < (1u << 22);
-         ++spin)
+// Liveness and integrity of the ring. Every wait is bounded (~0.1 s of polling): a
+// chunk that never completes (a staging/chain disagreement would be a bug) must not
+// leave a wave that never exits. An expired wait is an ERROR, never a value: the
+// waiting wave sets the workgroup's abort word (every other wait of the workgroup then
+// returns at once), the chain emits no checksum for any of its blocks, stagers stop
+// writing slots, and the kernel stores its fault code into the library's fault word
+// (pinned host memory, one per device), which every host-synchronous entry point
+// checks after its sync and stormck_device_status() reports for the async ones.
+// fault codes: kernel id | side
+constexpr uint32_t kFaultWideMulti = 1u, kFaultCommitMulti = 2u;
+constexpr uint32_t kFaultChain = 0x100u, kFaultStager = 0x200u;
+constexpr uint32_t kPipeSpin = 1u << 22;
+
+// Pipe control shared by one workgroup's chain and stager waves (LDS), plus the
+// kernel's fault word and its debug stall (STORMCK_DEBUG_STALL_CHUNK: stager wave 1 of
+// workgroup 0 never reports chunk `stall`, so the chain's wait for it expires).
+struct PipeCtl {
+    uint32_t* ready;   // kPipeMaxChunks LDS counters
+    uint32_t* done;    // LDS: chunks the chain has finished
+    uint32_t* abort;   // LDS: set by the first expired wait
+    uint32_t* fault;   // pinned host word of the device, or null
+    uint32_t kernel;   // kFault* id
+    uint32_t stall;    // 0 = off
+};
+
+// Wait until *word >= at_least. false: the wait expired (this call set the abort word)
+// or another wave of the workgroup aborted.
+__device__ __forceinline__ bool pipe_wait(const PipeCtl& pc, const uint32_t* word, uint32_t at_least,
+                                          uint32_t side) {
+    for (uint32_t spin = 0; __hip_atomic_load(word, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < at_least;
+         ++spin) {
+        if (__hip_atomic_load(pc.abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) return false;
+        if (spin >= kPipeSpin) {
+            __hip_atomic_store(pc.abort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (pc.fault) __hip_atomic_store(pc.fault, pc.kernel | side, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            return false;
+        }
         __builtin_amdgcn_s_sleep(1);
+    }
+    return true;
 }
 
 template <int BPW, uint32_t RS, class Src, class Emit>
-__device__ __forceinline__ void multi_stage_hash_pipe(uint4* ring, uint32_t* ready, uint32_t* done, uint32_t nlive,
-                                                      Src src_of, Emit emit) {
+__device__ __forceinline__ void multi_stage_hash_pipe(uint4* ring, const PipeCtl& pc, uint32_t nlive, Src src_of,
+                                                      Emit emit) {
+    uint32_t* ready = pc.ready;
+    uint32_t* done = pc.done;
     constexpr uint32_t kMaxPieces = kPipeMaxChunks * kChunkPieces;
     constexpr uint32_t kRingBlockPieces = ring_block_pieces(RS);
     const uint4* cover[BPW];
@@ -598,7 +632,10 @@ __device__ __forceinline__ void multi_stage_hash_pipe(uint4* ring, uint32_t* rea
                                                       static_cast<uint32_t>(c), static_cast<uint32_t>(c >> 32));
     };
     if (threadIdx.x < kPipeMaxChunks) ready[threadIdx.x] = 0;
-    if (threadIdx.x == 0) *done = 0;
+    if (threadIdx.x == 0) {
+        *done = 0;
+        *pc.abort = 0;
+    }
     if (safe) {  // chunk 0 into slot 0, every thread one piece of each block
         uint4 r[BPW];
 #pragma unroll
@@ -614,7 +651,9 @@ __device__ __forceinline__ void multi_stage_hash_pipe(uint4* ring, uint32_t* rea
         // address and is not stored)
         const uint32_t t = threadIdx.x - 64;
         for (uint32_t c = 1; c < nch; ++c) {
-            if (c >= RS) pipe_wait(done, c - RS + 1);  // the slot's old chunk is finished
+            // the slot's old chunk is finished; on an expired wait (or an abort) stop
+            // writing: the chain may still be reading the slot
+            if (c >= RS && !pipe_wait(pc, done, c - RS + 1, kFaultStager)) return;
             const uint32_t slot = (c % RS) * kSlotPieces;
             uint4 r[BPW][2];
 #pragma unroll
@@ -630,7 +669,8 @@ __device__ __forceinline__ void multi_stage_hash_pipe(uint4* ring, uint32_t* rea
                     if (k < kSlotPieces && idx < words[b]) put(b, slot + k, idx, r[b][q]);
                 }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-            if ((threadIdx.x & 63) == 0)
+            const bool stalled = pc.stall == c && blockIdx.x == 0 && threadIdx.x < 128;  // debug knob only
+            if ((threadIdx.x & 63) == 0 && !stalled)
                 __hip_atomic_fetch_add(ready + c, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
         return;
@@ -651,9 +691,13 @@ __device__ __forceinline__ void multi_stage_hash_pipe(uint4* ring, uint32_t* rea
     uint64_t acc = acc_seed(j);
     uint64_t tail[4] = {0, 0, 0, 0};
     uint32_t s_done = 0;
+    bool ok = true;
     // every chain lane runs the chunk loop (lane 0 publishes progress for the wave)
     for (uint32_t c = 0; c < nch; ++c) {
-        if (c > 0) pipe_wait(ready + c, kPipeStagers);
+        if (c > 0 && !pipe_wait(pc, ready + c, kPipeStagers, kFaultChain)) {
+            ok = false;  // the chunk never arrived: no checksum from this workgroup
+            break;
+        }
         if (staged) {
             // slot byte of cover byte x of this chunk: 32 + x - 4096c
             const uint8_t* slot = blk_ring + (c % RS) * kSlotPieces * 16 + 32;
@@ -680,6 +724,10 @@ __device__ __forceinline__ void multi_stage_hash_pipe(uint4* ring, uint32_t* rea
         else
             acc = quad_stripes_unaligned(src + 8 * j, nst, acc);
     }
+    // a stager that gave up (its wait for `done` expired) also voids the workgroup:
+    // it may have left a slot unwritten that the chain already passed
+    if (__hip_atomic_load(pc.abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) ok = false;
+    if (!ok) return;
     const uint64_t v1 = quad_bcast<0>(acc), v2 = quad_bcast<1>(acc), v3 = quad_bcast<2>(acc), v4 = quad_bcast<3>(acc);
     if (j == 0 && live) {
         const uint64_t h0 = (L >= 32) ? converge(v1, v2, v3, v4) : kP5;
@@ -696,7 +744,8 @@ __global__ __launch_bounds__(256) void k_xxh64_wide_multi(const uint8_t* __restr
                                                             uint64_t* __restrict__ out,
                                                             const uint64_t* __restrict__ expected,
                                                             unsigned long long* __restrict__ first_bad,
-                                                            unsigned long long* __restrict__ n_bad) {
+                                                            unsigned long long* __restrict__ n_bad,
+                                                            uint32_t* __restrict__ fault, uint32_t stall) {
     static_assert(RING > 0 ? (BPW * ring_block_pieces(RING) + kRingSlackPieces) * 16 <= 150 * 1024
                            : BPW * kMultiPieces * 16 <= 160 * 1024,
                   "LDS");
@@ -719,8 +768,9 @@ __global__ __launch_bounds__(256) void k_xxh64_wide_multi(const uint8_t* __restr
     };
     if constexpr (RING > 0) {
         __shared__ uint4 ring[BPW * ring_block_pieces(RING) + kRingSlackPieces];
-        __shared__ uint32_t ready[kPipeMaxChunks], done[1];
-        multi_stage_hash_pipe<BPW, RING>(ring, ready, done, nlive, src_of, emit);
+        __shared__ uint32_t ready[kPipeMaxChunks], done[1], abort_w[1];
+        const PipeCtl pc{ready, done, abort_w, fault, kFaultWideMulti, stall};
+        multi_stage_hash_pipe<BPW, RING>(ring, pc, nlive, src_of, emit);
     } else {
         __shared__ uint4 buf[BPW * kMultiPieces];
         multi_stage_hash<BPW>(buf, nlive, src_of, emit);
@@ -1479,7 +1529,8 @@ template <int BPW, uint32_t RING = kRingSlots>
 __global__ __launch_bounds__(256) void k_commit_level_multi(uint8_t* __restrict__ arena,
                                                              const stormck_dirty_block* __restrict__ blocks,
                                                              uint64_t lo, uint64_t cnt,
-                                                             uint64_t* __restrict__ out_cs) {
+                                                             uint64_t* __restrict__ out_cs,
+                                                             uint32_t* __restrict__ fault, uint32_t stall) {
     constexpr uint32_t RW = sizeof(stormck_dirty_block) / 8;  // 7 words per record
     static_assert(RING > 0 ? (BPW * ring_block_pieces(RING) + kRingSlackPieces) * 16 + BPW * RW * 8 <= 150 * 1024
                            : BPW * kMultiPieces * 16 + BPW * RW * 8 <= 160 * 1024,
@@ -1506,8 +1557,9 @@ __global__ __launch_bounds__(256) void k_commit_level_multi(uint8_t* __restrict_
     };
     if constexpr (RING > 0) {
         __shared__ uint4 ring[BPW * ring_block_pieces(RING) + kRingSlackPieces];
-        __shared__ uint32_t ready[kPipeMaxChunks], done[1];
-        multi_stage_hash_pipe<BPW, RING>(ring, ready, done, nlive, src_of, emit);
+        __shared__ uint32_t ready[kPipeMaxChunks], done[1], abort_w[1];
+        const PipeCtl pc{ready, done, abort_w, fault, kFaultCommitMulti, stall};
+        multi_stage_hash_pipe<BPW, RING>(ring, pc, nlive, src_of, emit);
     } else {
         __shared__ uint4 buf[BPW * kMultiPieces];
         multi_stage_hash<BPW>(buf, nlive, src_of, emit);

@@ -207,6 +207,62 @@ uint64_t cu_count() {
     return static_cast<uint64_t>(v);
 }
 
+// Fault word of each device (kernels.h PipeCtl): one pinned, device-mapped, coherent u32,
+// allocated on first use (stormck_init allocates it up front). A ring kernel whose
+// bounded wait expired stores its fault code there and writes no checksum for the
+// affected blocks; host-synchronous entry points check it after their sync
+// (take_fault), stormck_device_status() for the asynchronous ones.
+std::mutex g_fault_mu;
+uint32_t* g_fault[64] = {};
+
+int fault_word(uint32_t** out) {
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev));
+    if (dev < 0 || dev >= 64) return fail(STORMCK_EINVAL, "device index beyond 64");
+    std::lock_guard<std::mutex> g(g_fault_mu);
+    if (!g_fault[dev]) {
+        void* p = nullptr;
+        HIP_TRY(hipHostMalloc(&p, 64, hipHostMallocMapped | hipHostMallocPortable | hipHostMallocCoherent));
+        std::memset(p, 0, 64);
+        g_fault[dev] = static_cast<uint32_t*>(p);
+    }
+    *out = g_fault[dev];
+    return STORMCK_OK;
+}
+
+std::string fault_text(uint32_t code) {
+    const uint32_t k = code & 0xff;
+    const char* kernel = k == kFaultWideMulti ? "k_xxh64_wide_multi" : (k == kFaultCommitMulti ? "k_commit_level_multi" : "ring kernel");
+    const char* side = (code & kFaultStager) ? "a stager wave's wait for the chain" : "the chain wave's wait for a staged chunk";
+    return std::string(kernel) + ": ring staging stalled (" + side +
+           " expired); no checksum was written for the blocks of the stalled workgroup";
+}
+
+// After a sync on device `dev`: STORMCK_EHIP with the fault's text if a ring kernel
+// reported one since the last check (the word is then cleared), else STORMCK_OK.
+int take_fault(int dev) {
+    if (dev < 0 || dev >= 64) return STORMCK_OK;
+    uint32_t* w = nullptr;
+    {
+        std::lock_guard<std::mutex> g(g_fault_mu);
+        w = g_fault[dev];
+    }
+    if (!w) return STORMCK_OK;
+    const uint32_t code = __atomic_exchange_n(w, 0u, __ATOMIC_ACQ_REL);
+    if (code == 0) return STORMCK_OK;
+    return fail(STORMCK_EHIP, "device " + std::to_string(dev) + ": " + fault_text(code));
+}
+
+// STORMCK_DEBUG_STALL_CHUNK=c: stager wave 1 of workgroup 0 of every ring kernel never
+// reports chunk c (c >= 1), so the chain's wait expires (tests of the fault path only).
+uint32_t debug_stall() {
+    static const uint32_t c = [] {
+        const char* e = std::getenv("STORMCK_DEBUG_STALL_CHUNK");
+        return e ? static_cast<uint32_t>(std::strtoul(e, nullptr, 10)) : 0u;
+    }();
+    return c;
+}
+
 // Ring depth of the pipelined staging in the wide-multi kernels (kernels.h
 // multi_stage_hash_pipe): kRingSlots; probe knob STORMCK_STAGE_PIPE=0 stages whole blocks
 // first (A/B). 6- and 7-slot rings were measured slower.
@@ -285,17 +341,23 @@ int launch_checksum(const uint8_t* base, uint64_t stride, const uint32_t* lens, 
          ((reinterpret_cast<uintptr_t>(base) & 7) == 0 && (stride & 7) == 0 &&
           ((reinterpret_cast<uintptr_t>(base) & 15) + len + 15) / 16 <= multi_pieces))) {
         const dim3 grid(static_cast<unsigned>((n + bpw - 1) / bpw));
+        uint32_t* fault = nullptr;
+        if (ring_slots) {
+            const int frc = fault_word(&fault);
+            if (frc) return frc;
+        }
+        const uint32_t stall = debug_stall();
 #define STORMCK_MULTI(LENS, OFFS, VER)                                                                         \
     do {                                                                                                      \
         if (ring_slots && bpw == kMultiBpw)                                                                   \
             hipLaunchKernelGGL((k_xxh64_wide_multi<LENS, OFFS, VER, kMultiBpw, kRingSlots>), grid, dim3(kThreads), \
-                               0, st, base, stride, lens, len, offs, n, out, expected, first_bad, n_bad);     \
+                               0, st, base, stride, lens, len, offs, n, out, expected, first_bad, n_bad, fault, stall); \
         else if (ring_slots)                                                                                  \
             hipLaunchKernelGGL((k_xxh64_wide_multi<LENS, OFFS, VER, kMultiBpwRing, kRingSlots>), grid, dim3(kThreads), \
-                               0, st, base, stride, lens, len, offs, n, out, expected, first_bad, n_bad);     \
+                               0, st, base, stride, lens, len, offs, n, out, expected, first_bad, n_bad, fault, stall); \
         else                                                                                                  \
             hipLaunchKernelGGL((k_xxh64_wide_multi<LENS, OFFS, VER, kMultiBpw, 0>), grid, dim3(kThreads), 0,    \
-                               st, base, stride, lens, len, offs, n, out, expected, first_bad, n_bad);        \
+                               st, base, stride, lens, len, offs, n, out, expected, first_bad, n_bad, fault, stall); \
     } while (0)
         if (!verify) {
             if (lens && offs) STORMCK_MULTI(true, true, false);
@@ -566,6 +628,11 @@ int host_pipeline(const void* base, uint64_t stride, const uint32_t* lens, uint3
     auto drain = [&](Stage& s) -> int {
         if (!s.busy) return STORMCK_OK;
         HIP_TRY(hipEventSynchronize(s.done));
+        s.busy = false;
+        // a stalled ring kernel wrote no checksum (or no mismatch) for some blocks:
+        // nothing of this stage reaches the caller
+        const int frc = take_fault(c->device);
+        if (frc) return frc;
         if (expected) {
             if (s.h_result[1] > 0) {
                 nb += s.h_result[1];
@@ -574,7 +641,6 @@ int host_pipeline(const void* base, uint64_t stride, const uint32_t* lens, uint3
         } else {
             std::memcpy(out + s.first, s.h_out, s.count * 8);
         }
-        s.busy = false;
         return STORMCK_OK;
     };
 
@@ -769,7 +835,37 @@ int stormck_init(int device) {
     if (device < 0 || device >= count) return fail(STORMCK_EINVAL, "device index out of range");
     HIP_TRY(hipSetDevice(device));
     DeviceCtx* c = nullptr;
-    return get_ctx(&c);  // host-path staging is allocated on first host call
+    rc = get_ctx(&c);  // host-path staging is allocated on first host call
+    if (rc) return rc;
+    uint32_t* fw = nullptr;  // the ring kernels' fault word, before any capture can start
+    return fault_word(&fw);
+}
+
+int stormck_device_status(void* stream) {
+    int rc = device_check();
+    if (rc) return rc;
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev));
+    HIP_TRY(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
+    return take_fault(dev);
+}
+
+int stormck_device_alloc(uint64_t bytes, void** d_ptr) {
+    if (!d_ptr) return fail(STORMCK_EINVAL, "d_ptr is null");
+    *d_ptr = nullptr;
+    if (bytes == 0) return fail(STORMCK_EINVAL, "bytes is 0");
+    int rc = device_check();
+    if (rc) return rc;
+    HIP_TRY(hipMalloc(d_ptr, bytes));
+    return STORMCK_OK;
+}
+
+int stormck_device_free(void* d_ptr) {
+    if (!d_ptr) return STORMCK_OK;
+    int rc = device_check();
+    if (rc) return rc;
+    HIP_TRY(hipFree(d_ptr));
+    return STORMCK_OK;
 }
 
 void stormck_shutdown(void) {
@@ -1435,15 +1531,21 @@ int stormck_commit_device(void* d_arena, stormck_dirty_block* blocks, uint64_t n
             const uint64_t bpw = multi_bpw(cnt, ncu);
             const dim3 grid(static_cast<unsigned>((cnt + bpw - 1) / bpw));
             const uint32_t ring_slots = pipe_staging();
+            uint32_t* fault = nullptr;
+            if (ring_slots) {
+                const int frc = fault_word(&fault);
+                if (frc) return frc;
+            }
+            const uint32_t stall = debug_stall();
             if (ring_slots && bpw == kMultiBpw)
                 hipLaunchKernelGGL((k_commit_level_multi<kMultiBpw, kRingSlots>), grid, dim3(kThreads), 0, st,
-                                   static_cast<uint8_t*>(d_arena), d_blocks, lo, cnt, d_cs);
+                                   static_cast<uint8_t*>(d_arena), d_blocks, lo, cnt, d_cs, fault, stall);
             else if (ring_slots)
                 hipLaunchKernelGGL((k_commit_level_multi<kMultiBpwRing, kRingSlots>), grid, dim3(kThreads), 0, st,
-                                   static_cast<uint8_t*>(d_arena), d_blocks, lo, cnt, d_cs);
+                                   static_cast<uint8_t*>(d_arena), d_blocks, lo, cnt, d_cs, fault, stall);
             else
                 hipLaunchKernelGGL((k_commit_level_multi<kMultiBpw, 0>), grid, dim3(kThreads), 0, st,
-                                   static_cast<uint8_t*>(d_arena), d_blocks, lo, cnt, d_cs);
+                                   static_cast<uint8_t*>(d_arena), d_blocks, lo, cnt, d_cs, fault, stall);
         } else {
             dim3 grid;
             if (!grid_for(cnt * 4, &grid)) return fail(STORMCK_EINVAL, "level too large");
@@ -1616,6 +1718,8 @@ int stormck_commit_device(void* d_arena, stormck_dirty_block* blocks, uint64_t n
                 rc = fail(STORMCK_EHIP, "commit: checksum copy-back failed");
                 break;
             }
+            rc = take_fault(c->device);  // a stalled ring level wrote no checksum for some blocks
+            if (rc) break;
             const unsigned tn = static_cast<unsigned>(std::min<uint64_t>({8, fj.size(), x.cnt / 65536 + 1}));
             fj.run(tn, [&](unsigned t) {
                 const uint64_t lo = x.lo + x.cnt * t / tn, hi = x.lo + x.cnt * (t + 1) / tn;
@@ -1631,6 +1735,7 @@ int stormck_commit_device(void* d_arena, stormck_dirty_block* blocks, uint64_t n
     const hipError_t s1 = hipStreamSynchronize(st);
     for (Back& x : back) (void)hipEventDestroy(x.hashed);
     if (rc == STORMCK_OK && s1 != hipSuccess) rc = fail(STORMCK_EHIP, std::string("commit: ") + hipGetErrorString(s1));
+    if (rc == STORMCK_OK) rc = take_fault(c->device);
     pt.mark("device");
     return rc;
 }

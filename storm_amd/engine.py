@@ -70,6 +70,24 @@ def init(device: int) -> None:
     check(lib.stormck_init(device))
 
 
+def device_status(stream: int = 0) -> None:
+    """Synchronise `stream`; raise if a ring kernel on the current device faulted
+    (stormck_device_status: a stalled workgroup wrote no checksums)."""
+    check(lib.stormck_device_status(stream or None))
+
+
+def device_alloc(nbytes: int) -> int:
+    """hipMalloc through the library (a block arena outside torch's caching allocator)."""
+    import ctypes
+    p = ctypes.c_void_p()
+    check(lib.stormck_device_alloc(nbytes, ctypes.byref(p)))
+    return int(p.value)
+
+
+def device_free(d_ptr: int) -> None:
+    check(lib.stormck_device_free(d_ptr or None))
+
+
 def shutdown() -> None:
     lib.stormck_shutdown()
 

@@ -40,7 +40,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version():
     from storm_amd import _lib, ABI_VERSION
-    assert _lib.lib.stormck_abi_version() == ABI_VERSION == 1
+    assert _lib.lib.stormck_abi_version() == ABI_VERSION == 2
 
 
 def test_pointer_struct_is_24_bytes():
@@ -106,6 +106,8 @@ def test_argument_errors_precede_the_device_check():
                                                            1 << 22, (1 << 22) + 24, None)),
         ("fill stride", lambda: L.stormck_fill_synthetic_device(1 << 20, 24, 4, 0, 1, None)),
         ("register empty", lambda: L.stormck_host_register(None, 0)),
+        ("alloc null", lambda: L.stormck_device_alloc(16, None)),
+        ("alloc 0 bytes", lambda: L.stormck_device_alloc(0, ctypes.byref(ctypes.c_void_p()))),
         ("device pointer null", lambda: L.stormck_host_device_pointer(None, None)),
         ("key tags null", lambda: L.stormck_key_tags_device(None, 48, None, None, 48, 10, 1 << 20, None)),
         ("host null base", lambda: L.stormck_checksum_host(None, 32, None, 32, 4, ctypes.addressof(out))),

@@ -75,7 +75,23 @@ def test_bench_rccl_world1_root_matches_oracle():
                       "MASTER_PORT": str(_free_port())})
     assert "RCCL all-gather" in res["config"]["workload"]
     assert res["config"]["passes_per_step"] == 3 and res["n_gpus"] == 1
+    _check_group(res, 1, "nccl")
     assert _root(res) == _want(1)
+
+
+def _check_group(res, world, backend):
+    """The N > 1 line shows the process group that formed and every rank's timing."""
+    g = res["config"]["process_group"]
+    assert g["world_size"] == world and g["backend"] == backend and g["device_count"] >= 1
+    per = res["ranks"]["per_rank"]
+    assert [r["rank"] for r in per] == list(range(world))
+    assert 0 <= res["ranks"]["slowest_rank"] < world
+    for r in per:
+        assert 0 < r["kernel_min_ms"] <= r["kernel_avg_ms"] <= r["kernel_max_ms"]
+    slow = per[res["ranks"]["slowest_rank"]]
+    assert slow["ms_per_step"] == max(r["ms_per_step"] for r in per) == res["ms_per_step"]
+    arena = res["config"]["arena"]
+    assert int(arena["va"], 16) % arena["va_alignment"] == 0 and arena["va_alignment"] >= 4096
 
 
 @pytest.mark.timeout(300)
@@ -85,4 +101,5 @@ def test_bench_self_spawned_two_ranks_root_matches_oracle():
     res = _run_bench(["--gpus", "2", "--dist-backend", "gloo"], {})
     assert res["n_gpus"] == 2 and res["config"]["total_blocks"] == N_TOTAL
     assert res["config"]["blocks_per_gpu"] == sdist.shard_range(N_TOTAL, 2, 0)[1]
+    _check_group(res, 2, "gloo")
     assert _root(res) == _want(2)
