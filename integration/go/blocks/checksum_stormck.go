@@ -23,6 +23,8 @@ package blocks
 #cgo CFLAGS: -I${SRCDIR}/../third_party/stormck/include
 #cgo LDFLAGS: -L${SRCDIR}/../third_party/stormck/lib -lstormck -Wl,-rpath,${SRCDIR}/../third_party/stormck/lib
 #include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
 #include "stormck.h"
 */
 import "C"
@@ -158,6 +160,28 @@ func RegisterHostMemory(b []byte) error {
 		return stormckError(rc)
 	}
 	return nil
+}
+
+// NewHostArena returns n zeroed bytes outside the Go heap (a 4 KiB-aligned C
+// allocation), registered with RegisterHostMemory: storm's cache.data in the stormck
+// build (cache/cache.go:36-40, newArena in integration/go/cache/commit_stormck.go), the
+// arena CommitBatch hashes and updates in place. It lives as long as the process, as
+// cache.data does.
+func NewHostArena(n int) ([]byte, error) {
+	if n <= 0 {
+		return nil, errors.New("NewHostArena: size must be positive")
+	}
+	p := C.aligned_alloc(4096, C.size_t((n+4095)&^4095))
+	if p == nil {
+		return nil, errors.New("NewHostArena: out of host memory")
+	}
+	C.memset(p, 0, C.size_t(n))
+	b := unsafe.Slice((*byte)(p), n)
+	if err := RegisterHostMemory(b); err != nil {
+		C.free(p)
+		return nil, err
+	}
+	return b, nil
 }
 
 // DirtyBlock mirrors stormck_dirty_block (include/stormck.h): one dirty block of

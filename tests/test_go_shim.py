@@ -144,3 +144,80 @@ def test_go_dirty_block_has_the_c_layout():
         assert DIRTY_DTYPE.fields[cname][1] == off, (gname, cname)
         off += gsize
     assert off == DIRTY_DTYPE.itemsize == 56
+
+
+# --- the storm-side f1 binding (integration/go/cache) ---------------------------------
+
+CACHE_DIR = os.path.join(ROOT, "integration", "go", "cache")
+
+
+def _go(name):
+    return open(os.path.join(CACHE_DIR, name)).read()
+
+
+def _go_funcs(text):
+    """name -> number of parameters of every top-level func / method in a Go file."""
+    out = {}
+    for m in re.finditer(r"^func\s+(?:\([^)]*\)\s*)?([A-Za-z_]\w*)\s*(?:\[[^\]]*\])?\s*\(", text, flags=re.M):
+        args = _split_args(_balanced(text, m.end() - 1))
+        n = 0
+        for a in args:  # "a, b int" declares two parameters
+            n += 1
+        out[m.group(1)] = n
+    return out
+
+
+def test_cache_binding_build_tags_and_entry_points():
+    stormck, default, record = _go("commit_stormck.go"), _go("commit_default.go"), _go("commit_record.go")
+    assert stormck.startswith("//go:build stormck\n")
+    assert default.startswith("//go:build !stormck\n")
+    assert "//go:build" not in record.split("package")[0]
+    for text in (stormck, default):  # both builds provide what the patched cache.go calls
+        f = _go_funcs(text)
+        assert "commitDirty" in f and "newArena" in f
+    assert "recordCommit" in _go_funcs(record)
+    assert re.search(r"type commitRecord struct \{\s*origin BlockOrigin\s*parent \*blockMetadata\s*size\s+uint32\s*"
+                     r"typ\s+blocks\.BlockType\s*\}", record)
+    for field in re.findall(r"\.commit\.(\w+)", stormck):
+        assert field in ("origin", "parent", "size", "typ"), field
+
+
+def test_cache_binding_calls_match_the_blocks_shim():
+    stormck = re.sub(r"//[^\n]*", "", _go("commit_stormck.go"))
+    shim_funcs = _go_funcs(open(SHIM).read())
+    calls = [(m.group(1), len(_split_args(_balanced(stormck, m.end() - 1))))
+             for m in re.finditer(r"\bblocks\.([A-Z]\w*)\s*\(", stormck)]
+    assert ("CommitBatch", 5) in calls and ("NewHostArena", 1) in calls
+    for name, n in calls:
+        assert name in shim_funcs, f"blocks.{name} is not defined in the shim"
+        assert shim_funcs[name] == n, f"blocks.{name}: {n} args, shim declares {shim_funcs[name]}"
+    # DirtyBlock fields the binding sets exist in the shim's mirror of stormck_dirty_block
+    fields = {n for n, _ in go_dirty_block_fields()}
+    for f in set(re.findall(r"\bd\.(\w+)\s*=", stormck)) | set(re.findall(r"dirty\[i\]\.(\w+)", stormck)):
+        assert f in fields, f
+
+
+def test_storm_patch_applies_to_the_reference(tmp_path):
+    """trace_types.patch applies cleanly to storm's cache/ (types.go, trace.go, cache.go)
+    and wires exactly what the binding needs. Skipped where /root/reference is absent."""
+    import shutil
+    import subprocess
+    ref = "/root/reference/cache"
+    if not os.path.isdir(ref):
+        import pytest
+        pytest.skip("reference not present")
+    dst = tmp_path / "cache"
+    dst.mkdir()
+    for f in ("types.go", "trace.go", "cache.go"):
+        shutil.copy(os.path.join(ref, f), dst / f)
+    p = subprocess.run(["patch", "-p1", "-d", str(tmp_path), "-i", os.path.join(CACHE_DIR, "trace_types.patch")],
+                       capture_output=True, text=True)
+    assert p.returncode == 0, p.stdout + p.stderr
+    assert "offset" not in p.stdout and "fuzz" not in p.stdout, p.stdout
+    trace = (dst / "trace.go").read_text()
+    assert trace.count(".recordCommit(") == 2
+    assert "pointerBlockMeta.recordCommit(origin, parentBlockMeta, unsafe.Sizeof(*pointerBlock), blocks.PointerBlockType)" in trace
+    assert "leafBlockMeta.recordCommit(origin, parentBlockMeta, unsafe.Sizeof(*leafBlock), blocks.LeafBlockType)" in trace
+    cache = (dst / "cache.go").read_text()
+    assert "c.commitDirty()" in cache and "newArena(" in cache and "c.commitData()" not in cache
+    assert "commit commitRecord" in (dst / "types.go").read_text()
