@@ -61,7 +61,8 @@ def parse():
     p.add_argument("--c5-mix", default="keystore", choices=["keystore", "storm"],
                    help="c5 batch: BenchmarkKeyStore's commit (objectlist leaves) or BenchmarkStorm's (blob leaves "
                         "and a spacelist block)")
-    p.add_argument("--workload", default="c3", choices=["c3", "commit", "keytags", "c5"],
+    p.add_argument("--gather-blocks", type=int, default=4 << 20, help="gather workload: blocks per step")
+    p.add_argument("--workload", default="c3", choices=["c3", "commit", "keytags", "c5", "gather"],
                    help="c3 = BASELINE metric (default); commit = f1 level-synchronous Cache.Commit of a dirty "
                         "forest; keytags = f4 xxhash.Sum64 of 48-byte keys")
     p.add_argument("--commit-leaves", type=int, default=1 << 20)
@@ -352,6 +353,75 @@ def c5_workload(a):
     return rc
 
 
+def gather_workload(a):
+    """storm's batch shape on the LDS-DMA ring: 4M dirty blocks gathered from a 4M-slot
+    arena of 32 KiB slots (cache.data, cache/cache.go:36-40) in a shuffled slot order,
+    lengths drawn from storm's leaf and node sizes 31,808 / 30,000 / 32,768 / 28,808 B
+    (blocks/objectlist, pointer, blob, spacelist), per-block lengths (k_xxh64_glds_var,
+    persistent and 4 KiB-skewed). One step = one stormck_checksum_gather_device call."""
+    import numpy as np
+    import torch
+    from storm_amd import engine
+
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    engine.init(0)
+    n, slot = a.gather_blocks, BLOCK
+    rng = np.random.default_rng(3)
+    perm = rng.permutation(n).astype(np.uint64)
+    lens = np.array([31808, 30000, 32768, 28808], dtype=np.uint32)[rng.integers(0, 4, size=n)]
+    arena_ptr = engine.device_alloc(n * slot)
+    engine.fill_synthetic_device(arena_ptr, slot, n, 0, SYNTH_SEED)
+    d_offs = torch.from_numpy((perm * np.uint64(slot)).view(np.int64)).to(dev)
+    d_lens = torch.from_numpy(lens.view(np.int32)).to(dev)
+    out = torch.empty(n, dtype=torch.int64, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    st = stream.cuda_stream
+
+    def step():
+        engine.checksum_gather_device(arena_ptr, d_offs.data_ptr(), n, out.data_ptr(), 0, d_lens.data_ptr(), st)
+
+    settle(step, a.settle)
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    evs = []
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        e = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        e[0].record(stream)
+        step()
+        e[1].record(stream)
+        evs.append(e)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    kms = sorted(e0.elapsed_time(e1) for e0, e1 in evs)
+    avg_ms = sum(kms) / len(kms)
+    hashed = int(lens.sum())
+    alg = hashed + n * (8 + 8 + 4)  # block bytes + checksum written + offset and length read
+    res = {"metric": "GiB/s gathered per-block-length checksum (storm's dirty-slot batch shape), device-resident",
+           "value": round(hashed * a.steps / el / 2**30, 2), "unit": "GiB/s", "n_gpus": 1, "steps": a.steps,
+           "warmup": a.warmup, "ms_per_step": round(el / a.steps * 1e3, 3), "higher_is_better": True,
+           "scaling": "weak", "vs_baseline": None, "dtype": "u64", "data": "synthetic",
+           "config": {"workload": f"gather: {n} blocks from {n} shuffled 32 KiB slots, lengths of 31808/30000/32768/"
+                                  "28808 B, per-block lengths (stormck_checksum_gather_device)",
+                      "blocks": n, "hashed_bytes": hashed,
+                      "arena": {"va": "0x%x" % arena_ptr, "va_alignment": va_alignment(arena_ptr)}},
+           "roofline": {"bound": "hbm", "achieved": round(alg / (avg_ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
+                        "unit": "GB/s", "frac": round(alg / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
+                        "kernel": "k_xxh64_glds_var<16,nt,8w,4KiB,lens,offs>", "avg_launch_ms": round(avg_ms, 4),
+                        "launch_ms": {"n": len(kms), "min": round(kms[0], 4), "max": round(kms[-1], 4)},
+                        "algorithmic_bytes_per_launch": alg}}
+    from storm_amd import blocks
+    digest = blocks.Checksum(out.cpu().numpy().view(np.uint64).astype("<u8"))
+    res["digest"] = "0x%016x" % digest
+    print(json.dumps(res), flush=True)
+    del out
+    torch.cuda.synchronize()
+    engine.device_free(arena_ptr)
+    return 0
+
+
 def keytags_workload(a):
     """f4: one step = xxhash.Sum64 of 64M 48-byte keys resident in HBM (the key shape of
     keystore/benchmark_test.go:27-32), one lane per key (stormck_key_tags_device)."""
@@ -523,6 +593,8 @@ def main():
         rc = keytags_workload(a)
     elif a.workload == "c5":
         rc = c5_workload(a)
+    elif a.workload == "gather":
+        rc = gather_workload(a)
     else:
         rc = block_checksum_workload(a)
     if rc:

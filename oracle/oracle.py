@@ -46,6 +46,8 @@ def _load():
     lib.oracle_checksum_batch.argtypes = [c_void_p, c_size_t, c_void_p, c_uint32, c_size_t, c_void_p]
     lib.oracle_checksum_batch_mt.restype = None
     lib.oracle_checksum_batch_mt.argtypes = [c_void_p, c_size_t, c_void_p, c_uint32, c_size_t, c_void_p, c_int]
+    lib.oracle_checksum_gather_mt.restype = None
+    lib.oracle_checksum_gather_mt.argtypes = [c_void_p, c_void_p, c_void_p, c_uint32, c_size_t, c_void_p, c_int]
     lib.oracle_synth_word.restype = c_uint64
     lib.oracle_synth_word.argtypes = [c_uint64, c_uint64, c_uint64]
     lib.oracle_fill_synthetic.restype = None
@@ -84,6 +86,19 @@ def checksum_batch(buf, n: int, stride: int, length: int = 0, lens: Optional[Seq
         lib.oracle_checksum_batch_mt(a.ctypes.data, stride, lp, length, n, out.ctypes.data, threads)
     else:
         lib.oracle_checksum_batch(a.ctypes.data, stride, lp, length, n, out.ctypes.data)
+    return out
+
+
+def checksum_gather(buf, offs, length: int = 0, lens: Optional[Sequence[int]] = None,
+                    threads: int = 8) -> np.ndarray:
+    """Block i = buf[offs[i] : offs[i] + (lens[i] if lens else length)]."""
+    a = _u8(buf)
+    oa = np.ascontiguousarray(np.asarray(offs, dtype=np.uint64))
+    n = oa.size
+    out = np.zeros(n, dtype=np.uint64)
+    la = None if lens is None else np.ascontiguousarray(np.asarray(lens, dtype=np.uint32))
+    lib.oracle_checksum_gather_mt(a.ctypes.data, oa.ctypes.data, None if la is None else la.ctypes.data, length, n,
+                                  out.ctypes.data, threads)
     return out
 
 

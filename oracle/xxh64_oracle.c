@@ -114,29 +114,38 @@ void oracle_checksum_batch(const void* base, size_t stride, const uint32_t* lens
 
 /* ---- multi-threaded batch (CPU baseline "all cores" leg) ---- */
 typedef struct {
-    const uint8_t* base; size_t stride; const uint32_t* lens; uint32_t len;
+    const uint8_t* base; size_t stride; const uint64_t* offs; const uint32_t* lens; uint32_t len;
     size_t lo, hi; uint64_t* out;
 } mt_arg;
 static void* mt_body(void* a_) {
     mt_arg* a = (mt_arg*)a_;
     for (size_t i = a->lo; i < a->hi; ++i)
-        a->out[i] = oracle_xxh64(a->base + i * a->stride, a->lens ? a->lens[i] : a->len);
+        a->out[i] = oracle_xxh64(a->base + (a->offs ? a->offs[i] : i * a->stride), a->lens ? a->lens[i] : a->len);
     return NULL;
 }
-void oracle_checksum_batch_mt(const void* base, size_t stride, const uint32_t* lens, uint32_t len,
-                              size_t n, uint64_t* out, int threads) {
+static void mt_run(const void* base, size_t stride, const uint64_t* offs, const uint32_t* lens, uint32_t len,
+                   size_t n, uint64_t* out, int threads) {
     if (threads < 1) threads = 1;
     if (threads > 256) threads = 256;
     pthread_t th[256];
     mt_arg args[256];
     for (int t = 0; t < threads; ++t) {
-        args[t].base = (const uint8_t*)base; args[t].stride = stride; args[t].lens = lens;
+        args[t].base = (const uint8_t*)base; args[t].stride = stride; args[t].offs = offs; args[t].lens = lens;
         args[t].len = len; args[t].out = out;
         args[t].lo = n * (size_t)t / (size_t)threads;
         args[t].hi = n * (size_t)(t + 1) / (size_t)threads;
         pthread_create(&th[t], NULL, mt_body, &args[t]);
     }
     for (int t = 0; t < threads; ++t) pthread_join(th[t], NULL);
+}
+void oracle_checksum_batch_mt(const void* base, size_t stride, const uint32_t* lens, uint32_t len,
+                              size_t n, uint64_t* out, int threads) {
+    mt_run(base, stride, NULL, lens, len, n, out, threads);
+}
+/* Gathered blocks: block i at base + offs[i] (stormck_checksum_gather_device's shape). */
+void oracle_checksum_gather_mt(const void* base, const uint64_t* offs, const uint32_t* lens, uint32_t len,
+                               size_t n, uint64_t* out, int threads) {
+    mt_run(base, 0, offs, lens, len, n, out, threads);
 }
 
 /* ---- synthetic blocks ----

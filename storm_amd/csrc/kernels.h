@@ -331,15 +331,22 @@ struct BlockRef {
 // the next reads contiguous bytes from the later chunk's slot. Blocks are
 // ring_block_pieces(RS) = 2 (mod 16) pieces apart, so the 5 chains of a wave read distinct
 // LDS banks (as kMultiPieces below).
+// The chunk is a template parameter (CP pieces): 4 KiB up to 8 blocks per workgroup;
+// 2 KiB at 16 blocks per workgroup, whose 4-slot rings must fit the same LDS.
 constexpr uint32_t kChunkPieces = 256;
-constexpr uint32_t kPipeMaxChunks = 16;  // covers up to 64 KiB
+constexpr uint32_t kPipeMaxPieces = 4096;  // staged covers up to 64 KiB
+constexpr uint32_t pipe_max_chunks(uint32_t cp) { return kPipeMaxPieces / cp; }
+constexpr uint32_t kPipeMaxChunks = pipe_max_chunks(kChunkPieces);
 constexpr uint32_t kPipeStagers = 3;     // waves 1..3 of a 256-thread workgroup
 constexpr uint32_t kRingSlots = 4;  // shipped ring depth (7 measured slower, profiles/r02_pipe/)
 constexpr uint32_t kSlotPieces = 2 + kChunkPieces;
-// pieces between two blocks' rings: >= RS slots, = 2 (mod 16)
-constexpr uint32_t ring_block_pieces(uint32_t rs) { return (rs * kSlotPieces + 13) / 16 * 16 + 2; }
+// pieces between two blocks' rings: >= RS slots of 2 + CP pieces, = 2 (mod 16)
+constexpr uint32_t ring_block_pieces(uint32_t rs, uint32_t cp = kChunkPieces) {
+    return (rs * (2 + cp) + 13) / 16 * 16 + 2;
+}
 constexpr uint32_t kRingSlackPieces = 2;  // a 32-byte tail read past the last slot stays inside
-static_assert(ring_block_pieces(4) == 1042 && ring_block_pieces(7) == 1810, "ring layout");
+static_assert(ring_block_pieces(4) == 1042 && ring_block_pieces(7) == 1810 && ring_block_pieces(4, 128) == 530,
+              "ring layout");
 
 // Quad 0's part of k_xxh64_wide. Inlined once per branch, so the words are read with
 // ds_read from the staged copy and with global loads otherwise: through one generic
@@ -556,7 +563,7 @@ constexpr uint32_t kPipeSpin = 1u << 22;
 // kernel's fault word and its debug stall (STORMCK_DEBUG_STALL_CHUNK: stager wave 1 of
 // workgroup 0 never reports chunk `stall`, so the chain's wait for it expires).
 struct PipeCtl {
-    uint32_t* ready;   // kPipeMaxChunks LDS counters
+    uint32_t* ready;   // pipe_max_chunks(CP) LDS counters
     uint32_t* done;    // LDS: chunks the chain has finished
     uint32_t* abort;   // LDS: set by the first expired wait
     uint32_t* fault;   // pinned host word of the device, or null
@@ -581,13 +588,16 @@ __device__ __forceinline__ bool pipe_wait(const PipeCtl& pc, const uint32_t* wor
     return true;
 }
 
-template <int BPW, uint32_t RS, class Src, class Emit>
+template <int BPW, uint32_t RS, uint32_t CP, class Src, class Emit>
 __device__ __forceinline__ void multi_stage_hash_pipe(uint4* ring, const PipeCtl& pc, uint32_t nlive, Src src_of,
                                                       Emit emit) {
+    static_assert(BPW <= 16 && CP <= 256 && kPipeMaxPieces % CP == 0, "one chain wave, chunks of <= 256 pieces");
     uint32_t* ready = pc.ready;
     uint32_t* done = pc.done;
-    constexpr uint32_t kMaxPieces = kPipeMaxChunks * kChunkPieces;
-    constexpr uint32_t kRingBlockPieces = ring_block_pieces(RS);
+    constexpr uint32_t kMaxPieces = kPipeMaxPieces;
+    constexpr uint32_t kSlot = 2 + CP;                   // pieces per ring slot
+    constexpr uint32_t kPasses = (kSlot + 191) / 192;    // stager loads per block per chunk
+    constexpr uint32_t kRingBlockPieces = ring_block_pieces(RS, CP);
     const uint4* cover[BPW];
     uint32_t words[BPW], shift8[BPW], nw[BPW];
     uint32_t nch = 0;  // chunks of the longest staged block (uniform over the workgroup)
@@ -606,7 +616,7 @@ __device__ __forceinline__ void multi_stage_hash_pipe(uint4* ring, const PipeCtl
                 cover[b] = reinterpret_cast<const uint4*>(r.p - shift);
                 shift8[b] = shift / 8;
                 nw[b] = 4 * (r.len >> 5);
-                nch = max(nch, (w + kChunkPieces - 1) / kChunkPieces);
+                nch = max(nch, (w + CP - 1) / CP);
             }
         }
     }
@@ -631,42 +641,42 @@ __device__ __forceinline__ void multi_stage_hash_pipe(uint4* ring, const PipeCtl
         ring[b * kRingBlockPieces + pos] = make_uint4(static_cast<uint32_t>(a), static_cast<uint32_t>(a >> 32),
                                                       static_cast<uint32_t>(c), static_cast<uint32_t>(c >> 32));
     };
-    if (threadIdx.x < kPipeMaxChunks) ready[threadIdx.x] = 0;
+    if (threadIdx.x < pipe_max_chunks(CP)) ready[threadIdx.x] = 0;
     if (threadIdx.x == 0) {
         *done = 0;
         *pc.abort = 0;
     }
-    if (safe) {  // chunk 0 into slot 0, every thread one piece of each block
+    if (safe) {  // chunk 0 into slot 0, threads < CP one piece of each block
         uint4 r[BPW];
 #pragma unroll
         for (int b = 0; b < BPW; ++b) r[b] = cv[b][min(threadIdx.x, lim[b])];
 #pragma unroll
         for (int b = 0; b < BPW; ++b)
-            if (threadIdx.x < words[b]) put(b, 2 + threadIdx.x, threadIdx.x, r[b]);
+            if (threadIdx.x < CP && threadIdx.x < words[b]) put(b, 2 + threadIdx.x, threadIdx.x, r[b]);
     }
     __syncthreads();
     if (threadIdx.x >= 64) {
-        // stagers: slot position k < 258 of chunk c holds cover piece 256c - 2 + k; over
-        // 192 threads as k = t and t + 192 (the second load of t >= 66 repeats a clamped
+        // stagers: slot position k < CP + 2 of chunk c holds cover piece CP*c - 2 + k; over
+        // 192 threads as k = t, t + 192, ... (a load past the slot repeats a clamped
         // address and is not stored)
         const uint32_t t = threadIdx.x - 64;
         for (uint32_t c = 1; c < nch; ++c) {
             // the slot's old chunk is finished; on an expired wait (or an abort) stop
             // writing: the chain may still be reading the slot
             if (c >= RS && !pipe_wait(pc, done, c - RS + 1, kFaultStager)) return;
-            const uint32_t slot = (c % RS) * kSlotPieces;
-            uint4 r[BPW][2];
+            const uint32_t slot = (c % RS) * kSlot;
+            uint4 r[BPW][kPasses];
 #pragma unroll
             for (int b = 0; b < BPW; ++b)
 #pragma unroll
-                for (int q = 0; q < 2; ++q)
-                    r[b][q] = cv[b][min(c * kChunkPieces - 2 + min(t + 192u * q, kSlotPieces - 1), lim[b])];
+                for (int q = 0; q < static_cast<int>(kPasses); ++q)
+                    r[b][q] = cv[b][min(c * CP - 2 + min(t + 192u * q, kSlot - 1), lim[b])];
 #pragma unroll
             for (int b = 0; b < BPW; ++b)
 #pragma unroll
-                for (int q = 0; q < 2; ++q) {
-                    const uint32_t k = t + 192u * q, idx = c * kChunkPieces - 2 + k;
-                    if (k < kSlotPieces && idx < words[b]) put(b, slot + k, idx, r[b][q]);
+                for (int q = 0; q < static_cast<int>(kPasses); ++q) {
+                    const uint32_t k = t + 192u * q, idx = c * CP - 2 + k;
+                    if (k < kSlot && idx < words[b]) put(b, slot + k, idx, r[b][q]);
                 }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
             const bool stalled = pc.stall == c && blockIdx.x == 0 && threadIdx.x < 128;  // debug knob only
@@ -687,7 +697,7 @@ __device__ __forceinline__ void multi_stage_hash_pipe(uint4* ring, const PipeCtl
     const uint32_t w = (shift + L + 15) / 16;
     const bool staged = safe && (shift & 7) == 0 && w > 0 && w <= kMaxPieces;
     const uint8_t* blk_ring = reinterpret_cast<const uint8_t*>(ring + b * kRingBlockPieces);
-    const uint32_t tail_chunk = (shift + L - (L > 0 ? 1 : 0)) / (16 * kChunkPieces);
+    const uint32_t tail_chunk = (shift + L - (L > 0 ? 1 : 0)) / (16 * CP);
     uint64_t acc = acc_seed(j);
     uint64_t tail[4] = {0, 0, 0, 0};
     uint32_t s_done = 0;
@@ -699,10 +709,10 @@ __device__ __forceinline__ void multi_stage_hash_pipe(uint4* ring, const PipeCtl
             break;
         }
         if (staged) {
-            // slot byte of cover byte x of this chunk: 32 + x - 4096c
-            const uint8_t* slot = blk_ring + (c % RS) * kSlotPieces * 16 + 32;
-            const int64_t base = static_cast<int64_t>(shift) - static_cast<int64_t>(16 * kChunkPieces) * c;
-            const uint32_t end = min(nst, (16 * kChunkPieces * (c + 1) - shift) / 32);
+            // slot byte of cover byte x of this chunk: 32 + x - 16*CP*c
+            const uint8_t* slot = blk_ring + (c % RS) * kSlot * 16 + 32;
+            const int64_t base = static_cast<int64_t>(shift) - static_cast<int64_t>(16 * CP) * c;
+            const uint32_t end = min(nst, (16 * CP * (c + 1) - shift) / 32);
             if (end > s_done) {
                 acc = quad_stripes_aligned<16, false, true>(
                     reinterpret_cast<const uint64_t*>(slot + base + 32 * static_cast<int64_t>(s_done)) + j, end - s_done,
@@ -737,7 +747,7 @@ __device__ __forceinline__ void multi_stage_hash_pipe(uint4* ring, const PipeCtl
 }
 
 // RING: ring slots of the pipelined body (multi_stage_hash_pipe); 0 stages whole blocks first.
-template <bool LENS, bool OFFS, bool VERIFY, int BPW, uint32_t RING = kRingSlots>
+template <bool LENS, bool OFFS, bool VERIFY, int BPW, uint32_t RING = kRingSlots, uint32_t CP = kChunkPieces>
 __global__ __launch_bounds__(256) void k_xxh64_wide_multi(const uint8_t* __restrict__ base, uint64_t stride,
                                                             const uint32_t* __restrict__ lens, uint32_t len,
                                                             const uint64_t* __restrict__ offs, uint64_t n,
@@ -746,7 +756,7 @@ __global__ __launch_bounds__(256) void k_xxh64_wide_multi(const uint8_t* __restr
                                                             unsigned long long* __restrict__ first_bad,
                                                             unsigned long long* __restrict__ n_bad,
                                                             uint32_t* __restrict__ fault, uint32_t stall) {
-    static_assert(RING > 0 ? (BPW * ring_block_pieces(RING) + kRingSlackPieces) * 16 <= 150 * 1024
+    static_assert(RING > 0 ? (BPW * ring_block_pieces(RING, CP) + kRingSlackPieces) * 16 <= 150 * 1024
                            : BPW * kMultiPieces * 16 <= 160 * 1024,
                   "LDS");
     const uint64_t first = static_cast<uint64_t>(blockIdx.x) * BPW;
@@ -767,10 +777,10 @@ __global__ __launch_bounds__(256) void k_xxh64_wide_multi(const uint8_t* __restr
         }
     };
     if constexpr (RING > 0) {
-        __shared__ uint4 ring[BPW * ring_block_pieces(RING) + kRingSlackPieces];
-        __shared__ uint32_t ready[kPipeMaxChunks], done[1], abort_w[1];
+        __shared__ uint4 ring[BPW * ring_block_pieces(RING, CP) + kRingSlackPieces];
+        __shared__ uint32_t ready[pipe_max_chunks(CP)], done[1], abort_w[1];
         const PipeCtl pc{ready, done, abort_w, fault, kFaultWideMulti, stall};
-        multi_stage_hash_pipe<BPW, RING>(ring, pc, nlive, src_of, emit);
+        multi_stage_hash_pipe<BPW, RING, CP>(ring, pc, nlive, src_of, emit);
     } else {
         __shared__ uint4 buf[BPW * kMultiPieces];
         multi_stage_hash<BPW>(buf, nlive, src_of, emit);
@@ -1032,6 +1042,271 @@ __global__ __launch_bounds__(64 * WAVES) void k_xxh64_glds_skew(const uint8_t* _
             ++hc;
         }
     }
+}
+
+// ---------------------------------------------------------------------------
+// Per-block lengths and/or gathered offsets through the LDS-DMA ring: the batch shape
+// storm produces (dirty slots of cache.data, cache/cache.go:36-40, with mixed
+// Sizeof(T), blocks/objectlist/block.go:29-40, blocks/blob/block.go:25-29). The
+// k_xxh64_glds_skew scheme (workgroups of 16*WAVES blocks, 512-byte rows, 2-slot ring,
+// persistent with the waves SKEW tiles apart) with three changes:
+//  * each wave streams its own number of tiles per group: the longest of its 16
+//    blocks, the last tile partial. LDS-DMA lanes of pieces past a block's last stripe
+//    are switched off (exec mask) and the quads predicate the rounds of a partial tile,
+//    so every stripe of a staged block comes through LDS; the tail (< 32 B) is read
+//    from global memory when the group ends;
+//  * a block whose start is not 16-byte aligned is not staged: its quad hashes it from
+//    global memory when its group ends (any alignment is correct; storm's slots are
+//    32 KiB aligned, so this is the exception, and the host sends base+stride batches
+//    with unaligned rows to k_xxh64_quad);
+//  * the waves' streams differ in length, so a step runs while any wave of the
+//    workgroup still has work: each wave posts a flag before the step's barrier.
+// The starts and lengths of group g+G are loaded while group g streams, so a group
+// change waits for no memory.
+// ---------------------------------------------------------------------------
+template <int T, int AUX, bool VERIFY, int WAVES, int SKEW, bool LENS, bool OFFS>
+__global__ __launch_bounds__(64 * WAVES) void k_xxh64_glds_var(const uint8_t* __restrict__ base, uint64_t stride,
+                                                               const uint32_t* __restrict__ lens, uint32_t len,
+                                                               const uint64_t* __restrict__ offs, uint64_t n,
+                                                               uint64_t* __restrict__ out,
+                                                               const uint64_t* __restrict__ expected,
+                                                               unsigned long long* __restrict__ first_bad,
+                                                               unsigned long long* __restrict__ n_bad) {
+    constexpr int BPW = 16 * WAVES;
+    constexpr int ROW = 32 * T;
+    constexpr int TILE = BPW * ROW;
+    constexpr int INSTR = TILE / 1024;
+    constexpr int PER_WAVE = INSTR / WAVES;
+    static_assert(INSTR % WAVES == 0 && T % 2 == 0 && WAVES <= 8, "a wave's pieces must be its own block rows");
+    // the ring, then the waves' step flags [2][8] (in the same array: a second __shared__
+    // array makes hipcc guard ds_reads after an LDS-DMA with vmcnt(0), k_commit_level_glds)
+    __shared__ __attribute__((aligned(16))) uint8_t lds[2 * TILE + 16];
+    uint8_t* flags = lds + 2 * TILE;
+
+    const uint32_t tid = threadIdx.x;
+    const uint32_t wave = tid >> 6, lane = tid & 63;
+    const uint64_t ngroups = (n + BPW - 1) / BPW;
+    const uint64_t G = gridDim.x;
+    if (blockIdx.x >= ngroups) return;
+    const uint64_t ph = static_cast<uint64_t>(wave) * SKEW;  // this wave's start delay
+    if (tid < 16) flags[tid] = 0;
+    __syncthreads();  // before any wave posts its first flag
+
+    auto block_ptr = [&](uint64_t gb) -> const uint8_t* { return base + (OFFS ? offs[gb] : gb * stride); };
+    auto staged_bytes = [](const uint8_t* p, uint32_t L) -> uint32_t {  // stripe bytes through LDS, 0 = none
+        return (reinterpret_cast<uintptr_t>(p) & 15) == 0 ? (L >> 5) * 32 : 0;
+    };
+    auto wave_max = [](uint32_t v) {
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1) v = max(v, static_cast<uint32_t>(__shfl_xor(static_cast<int>(v), m)));
+        return v;
+    };
+
+    // ---- issue side: piece k of this lane is row prow[k] of the group, source byte pofs[k]
+    uint32_t prow[PER_WAVE], pofs[PER_WAVE];
+#pragma unroll
+    for (int k = 0; k < PER_WAVE; ++k) {
+        const uint32_t off = (wave * PER_WAVE + k) * 1024 + lane * 16;
+        const uint32_t b = off / ROW, q = (off % ROW) / 16;
+        prow[k] = b;
+        pofs[k] = ((q + glds_rot<T>(b)) % (2 * T)) * 16;
+    }
+    const uint8_t* i_src[PER_WAVE];
+    uint32_t i_lim[PER_WAVE];
+    const uint8_t* i_np[PER_WAVE];  // next group, prefetched
+    uint32_t i_nl[PER_WAVE];
+    auto i_fetch = [&](uint64_t g) __attribute__((always_inline)) {
+#pragma unroll
+        for (int k = 0; k < PER_WAVE; ++k) {
+            const uint64_t gb = g * BPW + prow[k];
+            const bool live = g < ngroups && gb < n;
+            const uint64_t gc = live ? gb : 0;
+            // unconditional loads (clamped index): a load under a branch gets its own
+            // vmcnt(0) wait, which would serialise the 2 * PER_WAVE loads
+            const uint32_t l = LENS ? lens[gc] : len;
+            i_np[k] = block_ptr(gc);
+            i_nl[k] = live ? l : 0;
+        }
+    };
+    uint64_t ig = blockIdx.x;
+    [[maybe_unused]] uint32_t it = 0;  // tile of group ig to issue next (used by the device pass)
+    uint32_t i_ntl = 0;
+    bool i_done = false;
+    auto i_switch = [&]() __attribute__((always_inline)) {  // make the prefetched group current, prefetch the one after
+        uint32_t tiles = 0;
+#pragma unroll
+        for (int k = 0; k < PER_WAVE; ++k) {
+            i_src[k] = i_np[k] + pofs[k];
+            i_lim[k] = staged_bytes(i_np[k], i_nl[k]);
+            tiles = max(tiles, (i_lim[k] + ROW - 1) / ROW);
+        }
+        i_ntl = wave_max(tiles);
+        i_fetch(ig + G);
+    };
+    auto i_next_group = [&]() __attribute__((always_inline)) {  // the next group with tiles for this wave
+        for (;;) {
+            ig += G;
+            if (ig >= ngroups) {
+                i_done = true;
+                return;
+            }
+            i_switch();
+            if (i_ntl > 0) return;
+        }
+    };
+    i_fetch(ig);
+    i_switch();
+    if (i_ntl == 0) i_next_group();
+#if defined(__HIP_DEVICE_COMPILE__)
+#define STORMCK_GLDS_VAR_ISSUE(SLOT)                                                                   \
+    do {                                                                                               \
+        uint8_t* dst_ = lds + (SLOT) * TILE + wave * PER_WAVE * 1024;                                  \
+        const uint32_t t0_ = it * ROW;                                                                 \
+        _Pragma("unroll") for (int k_ = 0; k_ < PER_WAVE; ++k_) if (t0_ + pofs[k_] < i_lim[k_])        \
+            __builtin_amdgcn_global_load_lds(i_src[k_] + t0_, dst_ + k_ * 1024, 16, 0, AUX);          \
+        ++it;                                                                                          \
+    } while (0)
+#else
+#define STORMCK_GLDS_VAR_ISSUE(SLOT) do { } while (0)
+#endif
+
+    // ---- hash side: quad (b, j) hashes row b of each group
+    const uint32_t b = tid >> 2, j = tid & 3;
+    const uint32_t rot = glds_rot<T>(b);
+    const uint8_t* h_np = nullptr;  // next group, prefetched
+    uint32_t h_nl = 0;
+    bool h_nlive = false;
+    auto h_fetch = [&](uint64_t g) __attribute__((always_inline)) {
+        const uint64_t gb = g * BPW + b;
+        h_nlive = g < ngroups && gb < n;
+        const uint64_t gc = h_nlive ? gb : 0;
+        const uint32_t l = LENS ? lens[gc] : len;  // unconditional, as i_fetch
+        h_np = block_ptr(gc);
+        h_nl = h_nlive ? l : 0;
+    };
+    uint64_t hg = blockIdx.x;
+    uint32_t ht = 0, h_ntl = 0, h_L = 0, h_nst = 0, h_sst = 0;
+    const uint8_t* h_p = nullptr;
+    bool h_live = false, h_done = false;
+    uint64_t acc = acc_seed(j);
+    // the tail (< 32 bytes after the last stripe) of a staged block, loaded when its group
+    // starts: 8-byte-aligned words that hold a tail byte (never past the page of the
+    // block's last byte); the other addresses read a word of out / expected, unused
+    uint64_t tail[4] = {0, 0, 0, 0};
+    const uint8_t* safe = VERIFY ? reinterpret_cast<const uint8_t*>(expected) : reinterpret_cast<const uint8_t*>(out);
+    auto h_switch = [&]() __attribute__((always_inline)) {
+        h_p = h_np;
+        h_L = h_nl;
+        h_live = h_nlive;
+        h_nst = h_L >> 5;
+        const uint32_t sb = staged_bytes(h_p, h_L);
+        h_sst = sb >> 5;  // stripes through LDS (h_nst, or 0 if not staged)
+        h_ntl = wave_max((sb + ROW - 1) / ROW);
+        acc = acc_seed(j);
+        const uint32_t rem = h_L & 31;
+        const uint8_t* t = h_p + 32 * static_cast<uint64_t>(h_nst);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const bool use = j == 0 && sb > 0 && 8u * q < rem;  // (sb > 0: 16-byte aligned start)
+            tail[q] = *reinterpret_cast<const uint64_t*>(use ? t + 8 * q : safe);
+        }
+        h_fetch(hg + G);
+    };
+    auto h_finish = [&]() __attribute__((always_inline)) {  // the group's blocks are complete: unstaged stripes, tail, checksum
+        if (h_sst < h_nst) {
+            if ((reinterpret_cast<uintptr_t>(h_p) & 7) == 0)
+                acc = quad_stripes_aligned<16>(reinterpret_cast<const uint64_t*>(h_p) + j, h_nst, acc);
+            else
+                acc = quad_stripes_unaligned(h_p + 8 * j, h_nst, acc);
+        }
+        const uint64_t v1 = quad_bcast<0>(acc), v2 = quad_bcast<1>(acc), v3 = quad_bcast<2>(acc), v4 = quad_bcast<3>(acc);
+        if (j == 0 && h_live) {
+            const uint64_t gbk = hg * BPW + b;
+            const uint64_t h0 = (h_L >= 32) ? converge(v1, v2, v3, v4) : kP5;
+            const uint64_t h = h_sst == h_nst && h_L >= 32 ? finish_regs(h0, h_L, tail, h_L & 31)
+                                                           : finish_fast(h0, h_L, h_p + 32 * static_cast<uint64_t>(h_nst), h_L & 31);
+            if constexpr (VERIFY) {
+                if (h != expected[gbk]) {
+                    atomicMin(first_bad, static_cast<unsigned long long>(gbk));
+                    atomicAdd(n_bad, 1ULL);
+                }
+            } else {
+                out[gbk] = h;
+            }
+        }
+    };
+    auto h_next_group = [&]() __attribute__((always_inline)) {  // finish groups without tiles on the way
+        for (;;) {
+            hg += G;
+            if (hg >= ngroups) {
+                h_done = true;
+                return;
+            }
+            h_switch();
+            if (h_ntl > 0) return;
+            h_finish();
+        }
+    };
+    h_fetch(hg);
+    h_switch();
+    if (h_ntl == 0) {
+        h_finish();
+        h_next_group();
+    }
+
+    // Each step: post the flag, wait for this wave's tile, barrier; then group changes
+    // (their loads were prefetched and have landed: the step's vmcnt(0) covered them,
+    // where after this step's LDS-DMA issue a use of them would wait for the new tile
+    // too), the issue of the next tile into the other slot, and the rounds of this one.
+    if (ph == 0 && !i_done) STORMCK_GLDS_VAR_ISSUE(0u);
+    bool h_fin = false;  // the current group's last tile is hashed: finish it next step
+    for (uint64_t u = 0;; ++u) {
+        flags[(u & 1) * 8 + wave] = h_done ? 0 : 1;
+        wait_vmcnt<0>();
+        wait_lgkm0();
+        __builtin_amdgcn_s_barrier();
+        if (*reinterpret_cast<const volatile uint64_t*>(flags + (u & 1) * 8) == 0) break;  // every wave done
+        if (h_fin) {
+            h_fin = false;
+            h_finish();
+            h_next_group();
+        }
+        if (u + 1 >= ph && !i_done) {
+            if (it == i_ntl) {
+                it = 0;
+                i_next_group();
+            }
+            if (!i_done) STORMCK_GLDS_VAR_ISSUE((u + 1) & 1);
+        }
+        if (u >= ph && !h_done) {
+            const uint8_t* row = lds + (u & 1) * TILE + b * ROW + (j & 1) * 8;
+            const uint32_t s0 = ht * T;
+            // all T words read first (the reads stay batched); a full tile takes the plain
+            // rounds, the block's last partial tile selects: a predicate on each round
+            // would put each LDS read in its own branch and wait for it there
+            uint64_t w[T];
+#pragma unroll
+            for (int s = 0; s < T; ++s) {
+                const uint32_t q = (2 * s + (j >> 1) + 2 * T - rot) % (2 * T);
+                w[s] = *reinterpret_cast<const uint64_t*>(row + q * 16);
+            }
+            if (s0 + T <= h_sst) {
+#pragma unroll
+                for (int s = 0; s < T; ++s) acc = round(acc, w[s]);
+            } else {
+#pragma unroll
+                for (int s = 0; s < T; ++s) {
+                    const uint64_t r = round(acc, w[s]);
+                    acc = s0 + s < h_sst ? r : acc;
+                }
+            }
+            if (++ht == h_ntl) {
+                ht = 0;
+                h_fin = true;
+            }
+        }
+    }
+#undef STORMCK_GLDS_VAR_ISSUE
 }
 
 // ---------------------------------------------------------------------------
@@ -1525,14 +1800,14 @@ __global__ __launch_bounds__(256) void k_commit_level_wide(uint8_t* __restrict__
 // blocks per workgroup staged premultiplied in one round trip, one chain wave. The
 // workgroup's BPW records (56 B each, possibly in pinned host memory) cross the bus
 // once, into LDS, before any block address is known.
-template <int BPW, uint32_t RING = kRingSlots>
+template <int BPW, uint32_t RING = kRingSlots, uint32_t CP = kChunkPieces>
 __global__ __launch_bounds__(256) void k_commit_level_multi(uint8_t* __restrict__ arena,
                                                              const stormck_dirty_block* __restrict__ blocks,
                                                              uint64_t lo, uint64_t cnt,
                                                              uint64_t* __restrict__ out_cs,
                                                              uint32_t* __restrict__ fault, uint32_t stall) {
     constexpr uint32_t RW = sizeof(stormck_dirty_block) / 8;  // 7 words per record
-    static_assert(RING > 0 ? (BPW * ring_block_pieces(RING) + kRingSlackPieces) * 16 + BPW * RW * 8 <= 150 * 1024
+    static_assert(RING > 0 ? (BPW * ring_block_pieces(RING, CP) + kRingSlackPieces) * 16 + BPW * RW * 8 <= 150 * 1024
                            : BPW * kMultiPieces * 16 + BPW * RW * 8 <= 160 * 1024,
                   "LDS");
     static_assert(BPW * RW <= 256, "one record word per thread");
@@ -1556,10 +1831,10 @@ __global__ __launch_bounds__(256) void k_commit_level_multi(uint8_t* __restrict_
         }
     };
     if constexpr (RING > 0) {
-        __shared__ uint4 ring[BPW * ring_block_pieces(RING) + kRingSlackPieces];
-        __shared__ uint32_t ready[kPipeMaxChunks], done[1], abort_w[1];
+        __shared__ uint4 ring[BPW * ring_block_pieces(RING, CP) + kRingSlackPieces];
+        __shared__ uint32_t ready[pipe_max_chunks(CP)], done[1], abort_w[1];
         const PipeCtl pc{ready, done, abort_w, fault, kFaultCommitMulti, stall};
-        multi_stage_hash_pipe<BPW, RING>(ring, pc, nlive, src_of, emit);
+        multi_stage_hash_pipe<BPW, RING, CP>(ring, pc, nlive, src_of, emit);
     } else {
         __shared__ uint4 buf[BPW * kMultiPieces];
         multi_stage_hash<BPW>(buf, nlive, src_of, emit);

@@ -136,6 +136,8 @@ constexpr unsigned kGldsBlocks = 16 * kGldsWaves;
 constexpr int kAuxNT = 2;
 constexpr uint64_t kMultiBpw = 5;          // blocks per workgroup of k_xxh64_wide_multi
 constexpr uint64_t kMultiBpwRing = 8;      // ring staging, batches above kMultiBpw per CU (133 KiB of LDS)
+constexpr uint64_t kMultiBpwWide = 16;     // ring staging in 2 KiB chunks, batches above 8 per CU (133 KiB)
+constexpr uint32_t kChunkPiecesWide = 128; // the 2 KiB chunk of kMultiBpwWide
 constexpr uint64_t kWideBatch = 128;      // batches up to this many blocks: k_xxh64_wide
 constexpr uint64_t kCommitWide = 256;     // f1 levels up to this many blocks: k_commit_level_wide
 constexpr uint64_t kStreamBatch = 16384;  // f1 commit levels from this many blocks: k_commit_level_glds
@@ -274,6 +276,17 @@ uint32_t pipe_staging() {
     return slots;
 }
 
+// 16 blocks per workgroup (one full chain wave) through 4-slot rings of 2 KiB chunks, for
+// batches of 9..16 blocks per CU. Probe knob STORMCK_WIDE16=0 sends them to the quad
+// kernel (A/B).
+bool wide16_on() {
+    static const bool on = [] {
+        const char* e = std::getenv("STORMCK_WIDE16");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 // Blocks per workgroup of the wide-multi kernels for a batch of n on ncu CUs: kMultiBpw
 // up to kMultiBpw per CU; with ring staging, kMultiBpwRing up to that many per CU. One
 // wave walks all of a workgroup's chains, so 8 cost about what 5 do (1,600 / 2,048 blocks:
@@ -283,6 +296,7 @@ uint64_t multi_bpw(uint64_t n, uint64_t ncu) {
     if (ncu == 0) return 0;
     if (n <= kMultiBpw * ncu) return kMultiBpw;
     if (pipe_staging() && n <= kMultiBpwRing * ncu) return kMultiBpwRing;
+    if (pipe_staging() && n <= kMultiBpwWide * ncu && wide16_on()) return kMultiBpwWide;
     return 0;
 }
 
@@ -349,7 +363,11 @@ int launch_checksum(const uint8_t* base, uint64_t stride, const uint32_t* lens, 
         const uint32_t stall = debug_stall();
 #define STORMCK_MULTI(LENS, OFFS, VER)                                                                         \
     do {                                                                                                      \
-        if (ring_slots && bpw == kMultiBpw)                                                                   \
+        if (ring_slots && bpw == kMultiBpwWide)                                                               \
+            hipLaunchKernelGGL((k_xxh64_wide_multi<LENS, OFFS, VER, kMultiBpwWide, kRingSlots, kChunkPiecesWide>), \
+                               grid, dim3(kThreads), 0, st, base, stride, lens, len, offs, n, out, expected,   \
+                               first_bad, n_bad, fault, stall);                                               \
+        else if (ring_slots && bpw == kMultiBpw)                                                              \
             hipLaunchKernelGGL((k_xxh64_wide_multi<LENS, OFFS, VER, kMultiBpw, kRingSlots>), grid, dim3(kThreads), \
                                0, st, base, stride, lens, len, offs, n, out, expected, first_bad, n_bad, fault, stall); \
         else if (ring_slots)                                                                                  \
@@ -371,6 +389,51 @@ int launch_checksum(const uint8_t* base, uint64_t stride, const uint32_t* lens, 
             else STORMCK_MULTI(false, false, true);
         }
 #undef STORMCK_MULTI
+        HIP_TRY(hipGetLastError());
+        return STORMCK_OK;
+    }
+    // Per-block lengths and/or gathered offsets (storm's dirty slots with mixed Sizeof(T)):
+    // the LDS-DMA ring with per-wave tile counts, k_xxh64_glds_var, in the same
+    // workgroup shapes as the uniform path below. base + stride batches need 16-byte
+    // aligned rows (else the quad kernel); gathered blocks are checked per block in the
+    // kernel, which hashes an unaligned one from global memory. Probe knob
+    // STORMCK_GLDS_VAR=0 restores the quad kernel (A/B).
+    static const bool var_on = [] {
+        const char* e = std::getenv("STORMCK_GLDS_VAR");
+        return !(e && e[0] == '0');
+    }();
+    if (var_on && n >= kMidBatch && (lens || offs) &&
+        (offs || ((reinterpret_cast<uintptr_t>(base) & 15) == 0 && (stride & 15) == 0))) {
+        const bool big = n >= kBigBatch;
+        const uint64_t per_wg = big ? kGldsBlocks : 16 * kMidWaves;
+        const uint64_t wgs = (n + per_wg - 1) / per_wg;
+        if (wgs > 0x7fffffffULL) return fail(STORMCK_EINVAL, "batch too large for one launch");
+        const uint64_t cus = cu_count();
+        // tile steps per workgroup: per-block lengths are on the device, assume 32 KiB
+        const uint64_t tiles = lens ? uint64_t{32768 / 32 / kTileStripes} : (uint64_t{len} / 32 + kTileStripes - 1) / kTileStripes;
+        const bool persistent = big && cus > 0 && wgs >= cus && (wgs + cus - 1) / cus * tiles >= kSkewMinSteps;
+        const dim3 grid(static_cast<unsigned>(persistent ? cus : wgs));
+#define STORMCK_VAR(VER, W, SK, LN, OF)                                                                          \
+    hipLaunchKernelGGL((k_xxh64_glds_var<kTileStripes, kAuxNT, VER, W, SK, LN, OF>), grid, dim3(64 * W), 0, st, base, \
+                       stride, lens, len, offs, n, out, expected, first_bad, n_bad)
+#define STORMCK_VAR_SHAPE(LN, OF)                                                                                \
+    do {                                                                                                         \
+        if (!big) {                                                                                              \
+            if (verify) STORMCK_VAR(true, kMidWaves, 0, LN, OF);                                                 \
+            else STORMCK_VAR(false, kMidWaves, 0, LN, OF);                                                       \
+        } else if (persistent) {                                                                                 \
+            if (verify) STORMCK_VAR(true, kGldsWaves, kSkewTiles, LN, OF);                                       \
+            else STORMCK_VAR(false, kGldsWaves, kSkewTiles, LN, OF);                                             \
+        } else {                                                                                                 \
+            if (verify) STORMCK_VAR(true, kGldsWaves, 0, LN, OF);                                                \
+            else STORMCK_VAR(false, kGldsWaves, 0, LN, OF);                                                      \
+        }                                                                                                        \
+    } while (0)
+        if (lens && offs) STORMCK_VAR_SHAPE(true, true);
+        else if (lens) STORMCK_VAR_SHAPE(true, false);
+        else STORMCK_VAR_SHAPE(false, true);
+#undef STORMCK_VAR_SHAPE
+#undef STORMCK_VAR
         HIP_TRY(hipGetLastError());
         return STORMCK_OK;
     }
@@ -1537,7 +1600,11 @@ int stormck_commit_device(void* d_arena, stormck_dirty_block* blocks, uint64_t n
                 if (frc) return frc;
             }
             const uint32_t stall = debug_stall();
-            if (ring_slots && bpw == kMultiBpw)
+            if (ring_slots && bpw == kMultiBpwWide)
+                hipLaunchKernelGGL((k_commit_level_multi<kMultiBpwWide, kRingSlots, kChunkPiecesWide>), grid,
+                                   dim3(kThreads), 0, st, static_cast<uint8_t*>(d_arena), d_blocks, lo, cnt, d_cs,
+                                   fault, stall);
+            else if (ring_slots && bpw == kMultiBpw)
                 hipLaunchKernelGGL((k_commit_level_multi<kMultiBpw, kRingSlots>), grid, dim3(kThreads), 0, st,
                                    static_cast<uint8_t*>(d_arena), d_blocks, lo, cnt, d_cs, fault, stall);
             else if (ring_slots)

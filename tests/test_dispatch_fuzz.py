@@ -1,7 +1,8 @@
 """Seeded random batches across the batch-size dispatch of launch_checksum
 (storm_amd/csrc/stormck.hip): one workgroup per block (<= 128), five staged blocks per
-workgroup (<= 5 per CU), register quad, LDS-staged streaming in 2- and 8-wave
-workgroups; uniform lengths, per-block lengths and gathered offsets; 16-byte, 8-byte and
+workgroup (<= 5 per CU), 8 and 16 ring-staged blocks per workgroup (<= 16 per CU),
+register quad, LDS-staged streaming in 2- and 8-wave workgroups (uniform lengths:
+k_xxh64_glds; per-block lengths and gathered offsets: k_xxh64_glds_var); uniform lengths, per-block lengths and gathered offsets; 16-byte, 8-byte and
 odd base alignments and strides; checksum and verify (first bad index, count). Every
 block is compared with the C oracle (XXH64 seed 0 = blocks.Checksum,
 /root/reference/blocks/checksum.go:15-17). The named tests in test_gpu_parity.py pin
@@ -14,7 +15,7 @@ from oracle import oracle as o
 pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
 
-CLASSES = [(1, 128), (129, 1280), (1281, 10239), (10240, 24575), (24576, 40000)]
+CLASSES = [(1, 128), (129, 1280), (1281, 2048), (2049, 4096), (4097, 10239), (10240, 24575), (24576, 40000)]
 BUDGET = 48 << 20  # bytes of block data per case
 
 
@@ -47,7 +48,7 @@ def _case(seed):
     return rng, n, mode, length, lens, stride, shift
 
 
-@pytest.mark.parametrize("seed", range(40))
+@pytest.mark.parametrize("seed", range(49))
 def test_dispatch_fuzz(dev, seed):
     from storm_amd import engine
     rng, n, mode, length, lens, stride, shift = _case(seed)

@@ -249,16 +249,17 @@ def test_uniform_fast_path_lengths(dev, length):
         del big
 
 
-@pytest.mark.parametrize("shift,n", [(0, 700), (8, 700), (8, 1900), (0, 3500)])
+@pytest.mark.parametrize("shift,n", [(0, 700), (8, 700), (8, 1900), (0, 2049), (8, 3500), (0, 4096), (8, 4097)])
 def test_wide_multi_ring_long_blocks(dev, shift, n):
-    """Batches of up to 5 blocks per CU take k_xxh64_wide_multi, whose pipelined staging
-    streams each block through a 4-slot ring of 4 KiB chunks (kernels.h
-    multi_stage_hash_pipe). 700 (5 per CU) or 1,900 (8 per CU) blocks, and 3,500 (the
-    register-quad kernel, for comparison), of random per-block lengths up to 64 KiB - 8
-    (covers of up to 16 chunks, stripes and tails straddling chunk and ring-wrap
-    boundaries, empty blocks), 16- and 8-byte-aligned starts; then uniform 32 KiB
-    blocks (storm's blob, a cover of 2,048 or 2,049 pieces); every block vs the C oracle,
-    and verify finds planted mismatches."""
+    """Batches of up to 16 blocks per CU take k_xxh64_wide_multi, whose pipelined staging
+    streams each block through a 4-slot ring (kernels.h multi_stage_hash_pipe): 4 KiB
+    chunks at 5 and 8 blocks per workgroup (700, 1,900 blocks), 2 KiB chunks at 16
+    (2,049 .. 4,096 blocks); 4,097 takes the register-quad kernel, for comparison. Random
+    per-block lengths up to 64 KiB - 8 (covers of up to 16 / 32 chunks, stripes and tails
+    straddling chunk and ring-wrap boundaries, empty blocks), 16- and 8-byte-aligned
+    starts; then uniform 32 KiB blocks (storm's blob, a cover of 2,048 or 2,049 pieces) in
+    the same batch-size class; every block vs the C oracle, and verify finds planted
+    mismatches."""
     from oracle import oracle as o
     from storm_amd import engine
     rng = np.random.default_rng(n + shift)
@@ -281,7 +282,7 @@ def test_wide_multi_ring_long_blocks(dev, shift, n):
                          res.data_ptr(), 0, d_lens.data_ptr())
     torch.cuda.synchronize()
     assert _u64(res).tolist() == [5, 2], (shift, n)
-    m, L = 1200, 32768
+    m, L = min(n, 4100), 32768
     blob = rng.integers(0, 256, size=shift + m * L + 64, dtype=np.uint8)
     d2 = torch.from_numpy(blob).to(dev)
     out2 = torch.empty(m, dtype=torch.int64, device=dev)
