@@ -62,6 +62,9 @@ def parse():
                    help="c5 batch: BenchmarkKeyStore's commit (objectlist leaves) or BenchmarkStorm's (blob leaves "
                         "and a spacelist block)")
     p.add_argument("--gather-blocks", type=int, default=4 << 20, help="gather workload: blocks per step")
+    p.add_argument("--gather-order", default="shuffled", choices=["shuffled", "sequential"],
+                   help="gather workload: slot order (storm's cache slots are spread by addressingOffsets)")
+    p.add_argument("--gather-lens", type=int, default=0, help="gather workload: one length for every block (A/B)")
     p.add_argument("--workload", default="c3", choices=["c3", "commit", "keytags", "c5", "gather"],
                    help="c3 = BASELINE metric (default); commit = f1 level-synchronous Cache.Commit of a dirty "
                         "forest; keytags = f4 xxhash.Sum64 of 48-byte keys")
@@ -368,8 +371,10 @@ def gather_workload(a):
     engine.init(0)
     n, slot = a.gather_blocks, BLOCK
     rng = np.random.default_rng(3)
-    perm = rng.permutation(n).astype(np.uint64)
+    perm = rng.permutation(n).astype(np.uint64) if a.gather_order == "shuffled" else np.arange(n, dtype=np.uint64)
     lens = np.array([31808, 30000, 32768, 28808], dtype=np.uint32)[rng.integers(0, 4, size=n)]
+    if a.gather_lens:
+        lens[:] = a.gather_lens
     arena_ptr = engine.device_alloc(n * slot)
     engine.fill_synthetic_device(arena_ptr, slot, n, 0, SYNTH_SEED)
     d_offs = torch.from_numpy((perm * np.uint64(slot)).view(np.int64)).to(dev)
@@ -403,8 +408,9 @@ def gather_workload(a):
            "value": round(hashed * a.steps / el / 2**30, 2), "unit": "GiB/s", "n_gpus": 1, "steps": a.steps,
            "warmup": a.warmup, "ms_per_step": round(el / a.steps * 1e3, 3), "higher_is_better": True,
            "scaling": "weak", "vs_baseline": None, "dtype": "u64", "data": "synthetic",
-           "config": {"workload": f"gather: {n} blocks from {n} shuffled 32 KiB slots, lengths of 31808/30000/32768/"
-                                  "28808 B, per-block lengths (stormck_checksum_gather_device)",
+           "config": {"workload": f"gather: {n} blocks from {n} {a.gather_order} 32 KiB slots, lengths of "
+                                  + (f"{a.gather_lens} B" if a.gather_lens else "31808/30000/32768/28808 B")
+                                  + ", per-block lengths (stormck_checksum_gather_device)",
                       "blocks": n, "hashed_bytes": hashed,
                       "arena": {"va": "0x%x" % arena_ptr, "va_alignment": va_alignment(arena_ptr)}},
            "roofline": {"bound": "hbm", "achieved": round(alg / (avg_ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
@@ -412,6 +418,23 @@ def gather_workload(a):
                         "kernel": "k_xxh64_glds_var<16,nt,8w,4KiB,lens,offs>", "avg_launch_ms": round(avg_ms, 4),
                         "launch_ms": {"n": len(kms), "min": round(kms[0], 4), "max": round(kms[-1], 4)},
                         "algorithmic_bytes_per_launch": alg}}
+    # the same arena through the uniform-length path (k_xxh64_glds_skew: every block 32 KiB,
+    # in slot order), 3 launches after the timed region: the rate this placement gives the
+    # uniform kernel, beside which the gather's frac reads
+    ref = torch.empty(n, dtype=torch.int64, device=dev)
+    rms = []
+    for r in range(4):
+        e = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        e[0].record(stream)
+        engine.checksum_device(arena_ptr, slot, n, ref.data_ptr(), slot, 0, st)
+        e[1].record(stream)
+        torch.cuda.synchronize()
+        if r:
+            rms.append(e[0].elapsed_time(e[1]))
+    ref_gbs = n * (slot + 8) / (sum(rms) / len(rms) * 1e-3) / 1e9
+    res["roofline"]["uniform_same_arena"] = {"kernel": KERNEL, "GB/s": round(ref_gbs, 1),
+                                             "frac": round(ref_gbs / HBM_PEAK_GBS, 4)}
+    del ref
     from storm_amd import blocks
     digest = blocks.Checksum(out.cpu().numpy().view(np.uint64).astype("<u8"))
     res["digest"] = "0x%016x" % digest
@@ -573,10 +596,14 @@ def root_fixture(n_total: int, world: int, distributed: bool):
     with open(path) as f:
         fx = json.load(f)
     row = None
+    worlds = fx["c4"]["worlds"]
     if world == 1 and not distributed and n_total == fx["c3"]["n"]:
         row, name = fx["c3"]["root"], "c3"
-    elif world > 1 and n_total == fx["c4"]["n_total"] and str(world) in fx["c4"]["worlds"]:
-        row, name = fx["c4"]["worlds"][str(world)]["global_root"], f"c4 world {world}"
+    elif world == 1 and not distributed and n_total == fx["c4"]["n_total"] and "1" in worlds:
+        # the strong-scaling series' N = 1 point: all 64M blocks in one shard tree
+        row, name = worlds["1"]["shard_roots"][0], "c4 world 1 (shard root)"
+    elif n_total == fx["c4"]["n_total"] and str(world) in worlds and (world > 1 or distributed):
+        row, name = worlds[str(world)]["global_root"], f"c4 world {world}"
     if row is None:
         return None, None
     return (int(row[0], 16), int(row[1], 16), int(row[2], 16), int(row[3])), name

@@ -423,8 +423,10 @@ def gen_c4() -> None:
     c4: 64M blocks split into `world` contiguous shards (storm_amd.dist.shard_range
     rule restated here); shard s's tree has leaf addresses lo_s.., interior nodes from
     64M + lo_s; the global root hashes one pointer block of the world shard roots and
-    has address 2 * 64M (storm_amd.dist.global_root_addr). Roots for world 2, 4 and 8
-    (the bench's N > 1 lines, strong scaling over the c4 set)."""
+    has address 2 * 64M (storm_amd.dist.global_root_addr). Roots for world 1, 2, 4 and 8
+    (the bench's strong-scaling series over the c4 set; at world 1 the shard root is
+    what `bench.py --total-blocks 67108864` prints, the global root what it prints with
+    --force-dist)."""
     import multiprocessing as mp
     n_total, rev, f = 1 << 26, 1, 1200
     # the numpy packer agrees with the per-entry packer on ragged trees
@@ -450,7 +452,7 @@ def gen_c4() -> None:
     assert h(xx(np.ascontiguousarray(cs[:1 << 24]).astype("<u8").tobytes())) == dig, "16M prefix digest"
     c3 = tree_root_np(cs[:1 << 24], 0, 1 << 24, rev, f)
     worlds = {}
-    for world in (2, 4, 8):
+    for world in (1, 2, 4, 8):
         table = []
         for r in range(world):
             q, rem = divmod(n_total, world)

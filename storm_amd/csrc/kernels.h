@@ -49,6 +49,23 @@ __device__ __forceinline__ T ldg(const T* p) {
     else return *p;
 }
 
+// s_waitcnt vmcnt(N) only (expcnt / lgkmcnt left at their "don't wait" maxima).
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+    static_assert(N >= 0 && N < 64, "vmcnt range");
+#if defined(__HIP_DEVICE_COMPILE__)
+    constexpr int imm = (N & 0xF) | ((N >> 4) << 14) | (0x7 << 4) | (0xF << 8);
+    __builtin_amdgcn_s_waitcnt(imm);
+#endif
+}
+
+// Wait for this wave's outstanding LDS reads (lgkmcnt(0)), vmcnt/expcnt untouched.
+__device__ __forceinline__ void wait_lgkm0() {
+#if defined(__HIP_DEVICE_COMPILE__)
+    __builtin_amdgcn_s_waitcnt(0xF | (0x3 << 14) | (0x7 << 4));
+#endif
+}
+
 // Stripe loop of one accumulator over nst stripes, 8-byte-aligned source.
 // p points at word j of stripe 0; word j of stripe s is p[4*s].
 // Software-pipelined in groups of U loads: group g+1 is in flight while group g hashes.
@@ -571,11 +588,20 @@ struct PipeCtl {
     uint32_t stall;    // 0 = off
 };
 
+// The ring's signals are LDS words between the waves of one workgroup. LDS executes a
+// wave's operations in order, so a counter bump issued after a wave's slot writes is seen
+// only after them, and reads issued after a counter was seen come after the writes it
+// counts: relaxed atomics plus compiler-only fences suffice. (An acquire / release fence
+// would also wait for the wave's outstanding global loads, vmcnt(0), which serialises
+// a stager's double-buffered loads.)
+__device__ __forceinline__ void lds_signal_fence() { __atomic_signal_fence(__ATOMIC_SEQ_CST); }
+
 // Wait until *word >= at_least. false: the wait expired (this call set the abort word)
 // or another wave of the workgroup aborted.
 __device__ __forceinline__ bool pipe_wait(const PipeCtl& pc, const uint32_t* word, uint32_t at_least,
                                           uint32_t side) {
-    for (uint32_t spin = 0; __hip_atomic_load(word, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < at_least;
+    lds_signal_fence();
+    for (uint32_t spin = 0; __hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < at_least;
          ++spin) {
         if (__hip_atomic_load(pc.abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) return false;
         if (spin >= kPipeSpin) {
@@ -585,10 +611,14 @@ __device__ __forceinline__ bool pipe_wait(const PipeCtl& pc, const uint32_t* wor
         }
         __builtin_amdgcn_s_sleep(1);
     }
+    lds_signal_fence();  // the caller's LDS reads / writes stay after the wait
     return true;
 }
 
-template <int BPW, uint32_t RS, uint32_t CP, class Src, class Emit>
+// DBL: each stager keeps two chunks in flight (loads of chunk c+1 issued before chunk c
+// is stored): with 2 KiB chunks one chunk per memory round trip is less than the chains
+// consume.
+template <int BPW, uint32_t RS, uint32_t CP, bool DBL, class Src, class Emit>
 __device__ __forceinline__ void multi_stage_hash_pipe(uint4* ring, const PipeCtl& pc, uint32_t nlive, Src src_of,
                                                       Emit emit) {
     static_assert(BPW <= 16 && CP <= 256 && kPipeMaxPieces % CP == 0, "one chain wave, chunks of <= 256 pieces");
@@ -660,17 +690,19 @@ __device__ __forceinline__ void multi_stage_hash_pipe(uint4* ring, const PipeCtl
         // 192 threads as k = t, t + 192, ... (a load past the slot repeats a clamped
         // address and is not stored)
         const uint32_t t = threadIdx.x - 64;
-        for (uint32_t c = 1; c < nch; ++c) {
-            // the slot's old chunk is finished; on an expired wait (or an abort) stop
-            // writing: the chain may still be reading the slot
-            if (c >= RS && !pipe_wait(pc, done, c - RS + 1, kFaultStager)) return;
-            const uint32_t slot = (c % RS) * kSlot;
-            uint4 r[BPW][kPasses];
+        auto load = [&](uint32_t c, uint4 (&r)[BPW][kPasses]) __attribute__((always_inline)) {
 #pragma unroll
             for (int b = 0; b < BPW; ++b)
 #pragma unroll
                 for (int q = 0; q < static_cast<int>(kPasses); ++q)
                     r[b][q] = cv[b][min(c * CP - 2 + min(t + 192u * q, kSlot - 1), lim[b])];
+        };
+        // chunk c into its slot, then count this wave in; false: stop (expired wait / abort)
+        auto store = [&](uint32_t c, const uint4 (&r)[BPW][kPasses]) __attribute__((always_inline)) -> bool {
+            // the slot's old chunk is finished; on an expired wait (or an abort) stop
+            // writing: the chain may still be reading the slot
+            if (c >= RS && !pipe_wait(pc, done, c - RS + 1, kFaultStager)) return false;
+            const uint32_t slot = (c % RS) * kSlot;
 #pragma unroll
             for (int b = 0; b < BPW; ++b)
 #pragma unroll
@@ -678,10 +710,35 @@ __device__ __forceinline__ void multi_stage_hash_pipe(uint4* ring, const PipeCtl
                     const uint32_t k = t + 192u * q, idx = c * CP - 2 + k;
                     if (k < kSlot && idx < words[b]) put(b, slot + k, idx, r[b][q]);
                 }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            // the slot writes are performed before the count (LDS order; see pipe_wait)
+            wait_lgkm0();
+            lds_signal_fence();
             const bool stalled = pc.stall == c && blockIdx.x == 0 && threadIdx.x < 128;  // debug knob only
             if ((threadIdx.x & 63) == 0 && !stalled)
-                __hip_atomic_fetch_add(ready + c, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                __hip_atomic_fetch_add(ready + c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            return true;
+        };
+        if constexpr (DBL) {
+            // two buffers, fully unrolled (no loop back-edge, across which the compiler
+            // would wait for every load): each store waits for exactly the older buffer
+            uint4 ra[BPW][kPasses], rb[BPW][kPasses];
+            if (nch > 1) load(1, ra);
+#pragma unroll
+            for (uint32_t p = 0; p < pipe_max_chunks(CP) / 2; ++p) {
+                const uint32_t c = 1 + 2 * p;
+                if (c >= nch) break;
+                if (c + 1 < nch) load(c + 1, rb);
+                if (!store(c, ra)) return;
+                if (c + 1 >= nch) break;
+                if (c + 2 < nch) load(c + 2, ra);
+                if (!store(c + 1, rb)) return;
+            }
+        } else {
+            for (uint32_t c = 1; c < nch; ++c) {
+                uint4 r[BPW][kPasses];
+                load(c, r);
+                if (!store(c, r)) return;
+            }
         }
         return;
     }
@@ -747,7 +804,8 @@ __device__ __forceinline__ void multi_stage_hash_pipe(uint4* ring, const PipeCtl
 }
 
 // RING: ring slots of the pipelined body (multi_stage_hash_pipe); 0 stages whole blocks first.
-template <bool LENS, bool OFFS, bool VERIFY, int BPW, uint32_t RING = kRingSlots, uint32_t CP = kChunkPieces>
+template <bool LENS, bool OFFS, bool VERIFY, int BPW, uint32_t RING = kRingSlots, uint32_t CP = kChunkPieces,
+          bool DBL = false>
 __global__ __launch_bounds__(256) void k_xxh64_wide_multi(const uint8_t* __restrict__ base, uint64_t stride,
                                                             const uint32_t* __restrict__ lens, uint32_t len,
                                                             const uint64_t* __restrict__ offs, uint64_t n,
@@ -780,7 +838,7 @@ __global__ __launch_bounds__(256) void k_xxh64_wide_multi(const uint8_t* __restr
         __shared__ uint4 ring[BPW * ring_block_pieces(RING, CP) + kRingSlackPieces];
         __shared__ uint32_t ready[pipe_max_chunks(CP)], done[1], abort_w[1];
         const PipeCtl pc{ready, done, abort_w, fault, kFaultWideMulti, stall};
-        multi_stage_hash_pipe<BPW, RING, CP>(ring, pc, nlive, src_of, emit);
+        multi_stage_hash_pipe<BPW, RING, CP, DBL>(ring, pc, nlive, src_of, emit);
     } else {
         __shared__ uint4 buf[BPW * kMultiPieces];
         multi_stage_hash<BPW>(buf, nlive, src_of, emit);
@@ -804,23 +862,6 @@ __device__ __forceinline__ uint32_t glds_rot(uint32_t b) {
     constexpr uint32_t pieces = 2 * T;
     if constexpr (T >= 8) return (2 * b) % pieces;
     else return (2 * (b / (8 / T))) % pieces;
-}
-
-// s_waitcnt vmcnt(N) only (expcnt / lgkmcnt left at their "don't wait" maxima).
-template <int N>
-__device__ __forceinline__ void wait_vmcnt() {
-    static_assert(N >= 0 && N < 64, "vmcnt range");
-#if defined(__HIP_DEVICE_COMPILE__)
-    constexpr int imm = (N & 0xF) | ((N >> 4) << 14) | (0x7 << 4) | (0xF << 8);
-    __builtin_amdgcn_s_waitcnt(imm);
-#endif
-}
-
-// Wait for this wave's outstanding LDS reads (lgkmcnt(0)), vmcnt/expcnt untouched.
-__device__ __forceinline__ void wait_lgkm0() {
-#if defined(__HIP_DEVICE_COMPILE__)
-    __builtin_amdgcn_s_waitcnt(0xF | (0x3 << 14) | (0x7 << 4));
-#endif
 }
 
 // One tile's worth of this wave's LDS-DMA pieces: instruction k moves 64 x 16 B from
@@ -1078,10 +1119,11 @@ __global__ __launch_bounds__(64 * WAVES) void k_xxh64_glds_var(const uint8_t* __
     constexpr int INSTR = TILE / 1024;
     constexpr int PER_WAVE = INSTR / WAVES;
     static_assert(INSTR % WAVES == 0 && T % 2 == 0 && WAVES <= 8, "a wave's pieces must be its own block rows");
-    // the ring, then the waves' step flags [2][8] (in the same array: a second __shared__
-    // array makes hipcc guard ds_reads after an LDS-DMA with vmcnt(0), k_commit_level_glds)
+    // the ring, then the count of waves whose stream has ended (in the same array: a
+    // second __shared__ array makes hipcc guard ds_reads after an LDS-DMA with vmcnt(0),
+    // k_commit_level_glds)
     __shared__ __attribute__((aligned(16))) uint8_t lds[2 * TILE + 16];
-    uint8_t* flags = lds + 2 * TILE;
+    uint32_t* n_finished = reinterpret_cast<uint32_t*>(lds + 2 * TILE);
 
     const uint32_t tid = threadIdx.x;
     const uint32_t wave = tid >> 6, lane = tid & 63;
@@ -1089,8 +1131,8 @@ __global__ __launch_bounds__(64 * WAVES) void k_xxh64_glds_var(const uint8_t* __
     const uint64_t G = gridDim.x;
     if (blockIdx.x >= ngroups) return;
     const uint64_t ph = static_cast<uint64_t>(wave) * SKEW;  // this wave's start delay
-    if (tid < 16) flags[tid] = 0;
-    __syncthreads();  // before any wave posts its first flag
+    if (tid == 0) *n_finished = 0;
+    __syncthreads();  // before any wave can finish
 
     auto block_ptr = [&](uint64_t gb) -> const uint8_t* { return base + (OFFS ? offs[gb] : gb * stride); };
     auto staged_bytes = [](const uint8_t* p, uint32_t L) -> uint32_t {  // stripe bytes through LDS, 0 = none
@@ -1240,6 +1282,10 @@ __global__ __launch_bounds__(64 * WAVES) void k_xxh64_glds_var(const uint8_t* __
             hg += G;
             if (hg >= ngroups) {
                 h_done = true;
+                // count this wave out; the add lands before the next barrier, after which
+                // every wave reads the count
+                if (lane == 0) __hip_atomic_fetch_add(n_finished, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                wait_lgkm0();
                 return;
             }
             h_switch();
@@ -1254,18 +1300,18 @@ __global__ __launch_bounds__(64 * WAVES) void k_xxh64_glds_var(const uint8_t* __
         h_next_group();
     }
 
-    // Each step: post the flag, wait for this wave's tile, barrier; then group changes
-    // (their loads were prefetched and have landed: the step's vmcnt(0) covered them,
-    // where after this step's LDS-DMA issue a use of them would wait for the new tile
-    // too), the issue of the next tile into the other slot, and the rounds of this one.
+    // Each step: wait for this wave's tile, barrier, read the finished-wave count (used at
+    // the step's end: every wave read it after the same barrier, so all leave together);
+    // then group changes (their loads were prefetched and have landed: the step's
+    // vmcnt(0) covered them, where after this step's LDS-DMA issue a use of them would
+    // wait for the new tile too), the issue of the next tile into the other slot, and
+    // the rounds of this one.
     if (ph == 0 && !i_done) STORMCK_GLDS_VAR_ISSUE(0u);
     bool h_fin = false;  // the current group's last tile is hashed: finish it next step
     for (uint64_t u = 0;; ++u) {
-        flags[(u & 1) * 8 + wave] = h_done ? 0 : 1;
         wait_vmcnt<0>();
-        wait_lgkm0();
         __builtin_amdgcn_s_barrier();
-        if (*reinterpret_cast<const volatile uint64_t*>(flags + (u & 1) * 8) == 0) break;  // every wave done
+        const uint32_t finished = __hip_atomic_load(n_finished, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         if (h_fin) {
             h_fin = false;
             h_finish();
@@ -1305,6 +1351,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_xxh64_glds_var(const uint8_t* __
                 h_fin = true;
             }
         }
+        if (finished == WAVES) break;  // every wave's stream had ended before this step's barrier
     }
 #undef STORMCK_GLDS_VAR_ISSUE
 }
@@ -1543,60 +1590,6 @@ __device__ __forceinline__ void ring_finish(uint64_t acc, uint32_t j, uint64_t n
     if (j == 0 && node < pm) parent_cs[node] = h;
 }
 
-// One wave produces and consumes (k_pointer_level_ring).
-template <uint32_t F, uint32_t TS_, int D, bool FULL>
-__device__ __forceinline__ void pointer_level_ring_body(const uint64_t* __restrict__ cs, uint64_t m, uint64_t pm,
-                                                        uint64_t node0, uint64_t addr_base, uint64_t rev, uint8_t type,
-                                                        uint64_t* __restrict__ parent_cs,
-                                                        uint64_t (*ring)[16][RingShape<TS_>::RS]) {
-    using P = RingProducer<F, TS_, FULL>;
-    constexpr uint32_t TS = P::TS, NT = P::NT, IT = P::IT;
-    static_assert(NT % D == 0, "tile shape");
-    const uint32_t lane = threadIdx.x, q = lane >> 2, j = lane & 3;
-    const P prod(cs, m, pm, node0, addr_base, rev, lane);
-    uint64_t raw[D][IT];
-    uint64_t acc = acc_seed(j);
-#pragma unroll
-    for (int d = 0; d < D; ++d) prod.load(d, raw[d]);
-    prod.produce(0, raw[0], ring[0]);
-    prod.load(D, raw[0]);
-    // Tile t: produce tile t+1 into ring slot (t+1)&1 and refill its registers with
-    // tile t+1+D, then walk the 15 chain rounds of tile t (slot t&1). D is even and t0
-    // a multiple of D, so the slots are compile-time constants. (Merging the three
-    // into one basic block so the scheduler interleaves them measured 6 % slower.)
-    static_assert(D % 2 == 0, "static ring slots");
-    for (uint32_t t0 = 0; t0 < NT; t0 += D) {
-#pragma unroll
-        for (int d = 0; d < D; ++d) {
-            const uint32_t t = t0 + d;
-            const int nb = (d + 1) % D;
-            if (t + 1 < NT) {
-                prod.produce(t + 1, raw[nb], ring[(d + 1) & 1]);
-                if (t + 1 + D < NT) prod.load(t + 1 + D, raw[nb]);
-            }
-            __builtin_amdgcn_wave_barrier();
-            const uint64_t* row = &ring[d & 1][q][j];
-#pragma unroll
-            for (uint32_t s = 0; s < TS; ++s) acc = round_pm(acc, row[4 * s]);
-            __builtin_amdgcn_wave_barrier();
-        }
-    }
-    ring_finish<F, FULL>(acc, j, node0 + q, pm, m, type, parent_cs);
-}
-
-template <uint32_t F, uint32_t TS, int D>
-__global__ __launch_bounds__(64) void k_pointer_level_ring(const uint64_t* __restrict__ cs, uint64_t m,
-                                                           uint64_t addr_base, uint64_t rev, uint8_t type,
-                                                           uint64_t* __restrict__ parent_cs) {
-    __shared__ uint64_t ring[2][16][RingShape<TS>::RS];  // two tiles of 16 nodes (15 KiB at TS = 15)
-    const uint64_t pm = (m + F - 1) / F;
-    const uint64_t node0 = static_cast<uint64_t>(blockIdx.x) * 16;
-    if (node0 + 16 <= m / F)  // every node of this wave has F children (wave-uniform branch)
-        pointer_level_ring_body<F, TS, D, true>(cs, m, pm, node0, addr_base, rev, type, parent_cs, ring);
-    else
-        pointer_level_ring_body<F, TS, D, false>(cs, m, pm, node0, addr_base, rev, type, parent_cs, ring);
-}
-
 // Producer / consumer waves (k_pointer_level_pc): C chain waves and C producer waves
 // per workgroup; producer wave C+i writes the premultiplied tiles of chain wave i's
 // 16 nodes, and the quads of the chain waves walk them, so a chain wave's instruction
@@ -1800,7 +1793,7 @@ __global__ __launch_bounds__(256) void k_commit_level_wide(uint8_t* __restrict__
 // blocks per workgroup staged premultiplied in one round trip, one chain wave. The
 // workgroup's BPW records (56 B each, possibly in pinned host memory) cross the bus
 // once, into LDS, before any block address is known.
-template <int BPW, uint32_t RING = kRingSlots, uint32_t CP = kChunkPieces>
+template <int BPW, uint32_t RING = kRingSlots, uint32_t CP = kChunkPieces, bool DBL = false>
 __global__ __launch_bounds__(256) void k_commit_level_multi(uint8_t* __restrict__ arena,
                                                              const stormck_dirty_block* __restrict__ blocks,
                                                              uint64_t lo, uint64_t cnt,
@@ -1834,7 +1827,7 @@ __global__ __launch_bounds__(256) void k_commit_level_multi(uint8_t* __restrict_
         __shared__ uint4 ring[BPW * ring_block_pieces(RING, CP) + kRingSlackPieces];
         __shared__ uint32_t ready[pipe_max_chunks(CP)], done[1], abort_w[1];
         const PipeCtl pc{ready, done, abort_w, fault, kFaultCommitMulti, stall};
-        multi_stage_hash_pipe<BPW, RING, CP>(ring, pc, nlive, src_of, emit);
+        multi_stage_hash_pipe<BPW, RING, CP, DBL>(ring, pc, nlive, src_of, emit);
     } else {
         __shared__ uint4 buf[BPW * kMultiPieces];
         multi_stage_hash<BPW>(buf, nlive, src_of, emit);

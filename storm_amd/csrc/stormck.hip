@@ -364,7 +364,7 @@ int launch_checksum(const uint8_t* base, uint64_t stride, const uint32_t* lens, 
 #define STORMCK_MULTI(LENS, OFFS, VER)                                                                         \
     do {                                                                                                      \
         if (ring_slots && bpw == kMultiBpwWide)                                                               \
-            hipLaunchKernelGGL((k_xxh64_wide_multi<LENS, OFFS, VER, kMultiBpwWide, kRingSlots, kChunkPiecesWide>), \
+            hipLaunchKernelGGL((k_xxh64_wide_multi<LENS, OFFS, VER, kMultiBpwWide, kRingSlots, kChunkPiecesWide, true>), \
                                grid, dim3(kThreads), 0, st, base, stride, lens, len, offs, n, out, expected,   \
                                first_bad, n_bad, fault, stall);                                               \
         else if (ring_slots && bpw == kMultiBpw)                                                              \
@@ -573,9 +573,11 @@ int get_ctx(DeviceCtx** out) {
     HIP_TRY(hipGetDevice(&dev));
     std::lock_guard<std::mutex> g(g_ctx_mu);
     if (g_ctx.size() <= static_cast<size_t>(dev)) g_ctx.resize(dev + 1);
-    if (!g_ctx[dev]) g_ctx[dev].reset(new DeviceCtx());
+    if (!g_ctx[dev]) {
+        g_ctx[dev].reset(new DeviceCtx());
+        g_ctx[dev]->device = dev;  // fixed for the context's life (read under its own mutex only)
+    }
     *out = g_ctx[dev].get();
-    (*out)->device = dev;
     return STORMCK_OK;
 }
 
@@ -1107,11 +1109,10 @@ int stormck_pointer_level_device(const uint64_t* d_child_cs, uint64_t m, uint64_
         HIP_TRY(hipGetLastError());
         return STORMCK_OK;
     }
-    // probe knob STORMCK_POINTER_RING: "0" = the register-quad kernel, "1" = one wave
-    // producing and hashing (k_pointer_level_ring); default: the producer / chain wave
-    // pair (k_pointer_level_pc). Measured alternatives (30- and 45-stripe tiles, prefetch
-    // 4 and 12 tiles, two pairs per workgroup, one producer for two chain waves):
-    // DESIGN.md §5, profiles/r02_merkle/.
+    // probe knob STORMCK_POINTER_RING: "0" = the register-quad kernel; default: the
+    // producer / chain wave pair (k_pointer_level_pc). Measured alternatives (one wave
+    // producing and hashing, 30- and 45-stripe tiles, prefetch 4 and 12 tiles, two pairs
+    // per workgroup, one producer for two chain waves): DESIGN.md §5, profiles/r02_merkle/.
     static const int ring_mode = [] {
         const char* e = std::getenv("STORMCK_POINTER_RING");
         return e ? std::atoi(e) : 2;
@@ -1123,12 +1124,8 @@ int stormck_pointer_level_device(const uint64_t* d_child_cs, uint64_t m, uint64_
         if (groups > 0x7fffffffULL) return fail(STORMCK_EINVAL, "level too large");
         const dim3 grid(static_cast<unsigned>(groups));
         hipStream_t st = static_cast<hipStream_t>(stream);
-        if (ring_mode == 1)
-            hipLaunchKernelGGL((k_pointer_level_ring<F, kRingTile, 4>), grid, dim3(64), 0, st, d_child_cs, m,
-                               child_addr_base, rev, child_type, d_parent_cs);
-        else
-            hipLaunchKernelGGL((k_pointer_level_pc<F, kRingTile, kRingPrefetch, 1>), grid, dim3(128), 0, st, d_child_cs,
-                               m, child_addr_base, rev, child_type, d_parent_cs);
+        hipLaunchKernelGGL((k_pointer_level_pc<F, kRingTile, kRingPrefetch, 1>), grid, dim3(128), 0, st, d_child_cs,
+                           m, child_addr_base, rev, child_type, d_parent_cs);
         HIP_TRY(hipGetLastError());
         return STORMCK_OK;
     }
@@ -1320,8 +1317,24 @@ int stormck_read_verify_fd(int fd, const uint64_t* addresses, const uint32_t* le
             if (!ok) return;
         }
     };
+    // STORMCK_DEBUG_READER_LIMIT=k: thread creation "fails" after k readers (tests)
+    static const long reader_limit = [] {
+        const char* e = std::getenv("STORMCK_DEBUG_READER_LIMIT");
+        return e ? std::atol(e) : -1L;
+    }();
     std::vector<std::thread> pool;
-    for (unsigned t = 0; t < std::min<uint64_t>(nt, npieces); ++t) pool.emplace_back(reader);
+    try {
+        pool.reserve(static_cast<size_t>(std::min<uint64_t>(nt, npieces)));
+        for (unsigned t = 0; t < std::min<uint64_t>(nt, npieces); ++t) {
+            if (reader_limit >= 0 && static_cast<long>(t) >= reader_limit)
+                throw std::system_error(std::make_error_code(std::errc::resource_unavailable_try_again));
+            pool.emplace_back(reader);
+        }
+    } catch (const std::exception&) {
+        // no more threads (std::system_error) or no memory for the vector: carry on with
+        // the readers already started; with none, this thread reads everything first
+        if (pool.empty()) reader();
+    }
     rc = STORMCK_OK;
     for (uint64_t sc = 0; sc < nsuper; ++sc) {
         {
@@ -1601,7 +1614,7 @@ int stormck_commit_device(void* d_arena, stormck_dirty_block* blocks, uint64_t n
             }
             const uint32_t stall = debug_stall();
             if (ring_slots && bpw == kMultiBpwWide)
-                hipLaunchKernelGGL((k_commit_level_multi<kMultiBpwWide, kRingSlots, kChunkPiecesWide>), grid,
+                hipLaunchKernelGGL((k_commit_level_multi<kMultiBpwWide, kRingSlots, kChunkPiecesWide, true>), grid,
                                    dim3(kThreads), 0, st, static_cast<uint8_t*>(d_arena), d_blocks, lo, cnt, d_cs,
                                    fault, stall);
             else if (ring_slots && bpw == kMultiBpw)

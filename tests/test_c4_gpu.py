@@ -7,7 +7,7 @@ bench.py would: the shard streams through a 4M-block arena (2 passes, the arena
 regenerated with the pass's own logical blocks), the shard tree is built on the
 device (k_pointer_level*), and the 8 roots are combined on the device
 (k_pointer_node). Checked against tests/golden/c3c4_roots.json, computed with
-libxxhash by oracle/gen_golden.py --c4 (roots for world 2, 4 and 8, and the c3 root
+libxxhash by oracle/gen_golden.py --c4 (roots for world 1, 2, 4 and 8, and the c3 root
 of the first 16M blocks), plus the digest of all 64M checksums.
 """
 import numpy as np
@@ -67,10 +67,11 @@ def test_c4_checksums_digest(c4_checksums):
     assert o.xxh64(host.astype("<u8")) == hx(fx["digest"])
 
 
-@pytest.mark.parametrize("world", [8, 4, 2])
+@pytest.mark.parametrize("world", [8, 4, 2, 1])
 def test_c4_shard_roots_and_global_root(dev, c4_checksums, world):
     """Per-shard device trees + the device combine = the libxxhash roots (world 8 is
-    c4 itself: 8 shards of 8M)."""
+    c4 itself: 8 shards of 8M; world 1 is the strong-scaling series' N = 1 point, all
+    64M leaves in one tree)."""
     from storm_amd import dist as sdist
     from storm_amd import engine
     fx = load_golden("c3c4_roots.json")["c4"]

@@ -135,6 +135,7 @@ def _registered_run(c):
     from storm_amd import blocks
 
     def run(recs, rev, last):
+        assert c.data.ctypes.data % 256 == 0  # rows at link rate (blocks.RegisterHostMemory)
         blocks.RegisterHostMemory(c.data)
         try:
             return cm.commit_device(blocks.HostDevicePointer(c.data), recs, rev, last)

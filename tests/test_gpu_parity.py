@@ -291,7 +291,7 @@ def test_wide_multi_ring_long_blocks(dev, shift, n):
     want2 = o.checksum_batch(blob[shift:], m, L, L, threads=8)
     assert np.array_equal(_u64(out2), want2), shift
     exp = want2.copy()
-    exp[[3, 777]] ^= np.uint64(1)
+    exp[[3, m - 2]] ^= np.uint64(1)
     res = torch.zeros(2, dtype=torch.int64, device=dev)
     engine.verify_device(d2.data_ptr() + shift, L, m, torch.from_numpy(exp.view(np.int64)).to(dev).data_ptr(),
                          res.data_ptr(), L)
@@ -561,8 +561,8 @@ def test_pack_pointer_blocks_materialised(dev):
 
 @pytest.mark.parametrize("m", [257 * 1200, 300 * 1200 + 1, 4000 * 1200 - 7, 320 * 1200])
 def test_pointer_level_ring_kernel(dev, m):
-    """Levels of more than 256 nodes at storm's fan-out take k_pointer_level_ring (one
-    wave per 16 nodes, premultiplied words staged in LDS). Shapes: full last wave (320
+    """Levels of more than 256 nodes at storm's fan-out take k_pointer_level_pc (a
+    producer wave and a chain wave per 16 nodes, premultiplied words staged in LDS). Shapes: full last wave (320
     nodes), a last wave holding 1 node and 15 idle quads (257), a last node with one
     child (300 + 1), and a ragged 4,000-node level; addresses and revision above 2^32.
     Equal to the materialised pointer blocks hashed by the batch kernels on every node,
@@ -734,6 +734,46 @@ def test_read_verify_fd_across_super_chunks(dev, tmp_path, monkeypatch):
             blocks.ReadVerifyBatch(fd, far, lens, expected, dst, bs, block_size=bs)
     finally:
         os.close(fd)
+
+
+READER_CHILD = r"""
+import os, sys
+import numpy as np
+sys.path.insert(0, sys.argv[1])
+from oracle import oracle as o
+from storm_amd import blocks
+rng = np.random.default_rng(5)
+nblocks, bs, n = 512, 4096, 900
+image = rng.integers(0, 256, size=(nblocks, bs), dtype=np.uint8)
+path = os.path.join(sys.argv[2], "dev.img")
+image.tofile(path)
+addresses = rng.integers(0, nblocks, size=n).astype(np.uint64)
+lens = rng.integers(1, bs + 1, size=n).astype(np.uint32)
+expected = np.array([o.xxh64(image[a, :l]) for a, l in zip(addresses, lens)], dtype=np.uint64)
+dst = np.zeros((n, bs), dtype=np.uint8)
+fd = os.open(path, os.O_RDONLY)
+ok = blocks.ReadVerifyBatch(fd, addresses, lens, expected, dst, bs, block_size=bs) == (n, 0)
+bad = expected.copy(); bad[[700, 33]] ^= 1
+ok = ok and blocks.ReadVerifyBatch(fd, addresses, lens, bad, dst, bs, block_size=bs) == (33, 2)
+print("RESULT", ok)
+"""
+
+
+@pytest.mark.parametrize("limit", ["0", "2"])
+def test_read_verify_survives_reader_thread_failure(dev, tmp_path, limit):
+    """Creating the reader pool can fail (thread limit): the call carries on with the
+    readers already started, or reads on the calling thread when there are none, and
+    never lets the exception leave the C ABI. STORMCK_DEBUG_READER_LIMIT makes creation
+    fail after `limit` readers (read once per process: a child process)."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, STORMCK_DEBUG_READER_LIMIT=limit, STORMCK_READ_SUPER_BYTES=str(64 * 4096))
+    p = subprocess.run([sys.executable, "-c", READER_CHILD, root, str(tmp_path)], env=env, capture_output=True,
+                       text=True, timeout=120)
+    assert p.returncode == 0, (p.returncode, p.stderr[-3000:])
+    assert "RESULT True" in p.stdout, p.stdout[-2000:]
 
 
 def _odirect_dir(tmp_path):

@@ -92,3 +92,37 @@ def test_errors_name_the_failing_range(dev):
     msg = _lib.last_error()
     assert "device 0 (blocks 50..100)" in msg and "stride" in msg, msg
     assert torch.cuda.current_device() == before
+
+
+def test_every_visible_device(dev):
+    """On a node with several GPUs: one range per physical device (each worker thread
+    selects its own device, cu count and staging; pinned DMA to a second device), for
+    pageable and registered buffers, and the caller's current device is unchanged.
+    Skipped on a one-GPU box (the driver's 8-GPU node runs it)."""
+    from storm_amd import blocks
+    count = torch.cuda.device_count()
+    if count < 2:
+        pytest.skip("one device")
+    devices = list(range(count))
+    n, stride = 4099, 32768
+    raw = np.empty(n * stride + 4096, dtype=np.uint8)
+    off = (-raw.ctypes.data) % 4096
+    host = raw[off:off + n * stride]
+    host[:] = np.random.default_rng(21).integers(0, 256, size=host.size, dtype=np.uint8)
+    want = o.checksum_batch(host, n, stride, stride, threads=8)
+    torch.cuda.set_device(count - 1)
+    assert np.array_equal(blocks.ChecksumBatch(host, n, stride, stride, devices=devices), want)
+    bad = want.copy()
+    bad[[n - 1, 5]] ^= np.uint64(1)
+    assert blocks.VerifyChecksumBatch(host, n, stride, bad, stride, devices=devices) == (5, 2)
+    blocks.RegisterHostMemory(host)
+    try:
+        assert np.array_equal(blocks.ChecksumBatch(host, n, stride, stride, devices=devices[::-1]), want)
+    finally:
+        blocks.UnregisterHostMemory(host)
+    assert torch.cuda.current_device() == count - 1
+    from storm_amd import _lib
+    cur = ctypes.c_int(-1)
+    torch.cuda.synchronize()
+    assert _lib.lib.stormck_device_count(ctypes.byref(cur)) == 0 and cur.value == count
+    torch.cuda.set_device(0)
