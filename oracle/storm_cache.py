@@ -130,7 +130,9 @@ class Cache:
         self.store, self.fanout, self.leaf_len = store, fanout, leaf_len
         self.bs = store.block_size
         self.n_blocks = n_slots
-        self.data = np.zeros(n_slots * self.bs, dtype=np.uint8)
+        raw = np.zeros(n_slots * self.bs + 4096, dtype=np.uint8)  # cache.data, page-aligned (as Go's large make)
+        off = (-raw.ctypes.data) % 4096
+        self.data = raw[off:off + n_slots * self.bs]
         self.blocks = [Meta(i * self.bs) for i in range(n_slots)]
         self.addressing = np.random.default_rng(seed).permutation(n_slots).astype(np.int64)
         self.dirty: Dict[Meta, None] = {}  # insertion-ordered set

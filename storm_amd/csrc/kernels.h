@@ -1105,14 +1105,181 @@ __global__ __launch_bounds__(64 * WAVES) void k_xxh64_glds_skew(const uint8_t* _
 // The starts and lengths of group g+G are loaded while group g streams, so a group
 // change waits for no memory.
 // ---------------------------------------------------------------------------
-template <int T, int AUX, bool VERIFY, int WAVES, int SKEW, bool LENS, bool OFFS>
+// Locality order of a large gather. A workgroup's 128 blocks are read in lock step, a
+// 512-byte row of each per tile. Gathered from random slots of a large arena (storm's
+// dirty slots), the rows of one step land on the HBM channels at random, unevenly, and
+// the step waits for the busiest channel: 0.76-0.78 of 8 TB/s on 4M shuffled 32 KiB slots
+// against 0.85-0.87 in slot order on the same arenas (profiles/r03d/, r03f/). Bucketing by
+// 32 MiB region alone (TLB locality) changed nothing (r03f); the blocks of a group must
+// be in address order. So: a counting sort by 32 MiB region of the offset (4,096
+// buckets, wrapping every 128 GiB): k_order_count (a histogram per part of the input,
+// in LDS), k_order_scan_rows + k_order_scan_buckets (exclusive scan of the part counts,
+// bucket-major), k_order_place (each part places its elements from its column of the
+// scanned counts, ranked with LDS atomics: no global atomics); then k_order_sort sorts
+// each bucket of up to kOrderSortMax blocks by offset in LDS (bitonic). Every checksum
+// is still written at its own index.
+constexpr uint32_t kOrderShift = 25, kOrderBuckets = 4096, kOrderParts = 128;
+
+__device__ __forceinline__ uint32_t order_bucket(uint64_t off) {
+    return static_cast<uint32_t>(off >> kOrderShift) & (kOrderBuckets - 1);
+}
+
+// The elements split into kOrderParts contiguous parts, one workgroup each. counts is a
+// bucket-major matrix: counts[b * kOrderParts + w] = elements of part w in bucket b.
+__device__ __forceinline__ void order_part(uint64_t n, uint32_t w, uint64_t* lo, uint64_t* hi) {
+    *lo = n * w / kOrderParts;
+    *hi = n * (w + 1) / kOrderParts;
+}
+
+__global__ __launch_bounds__(256) void k_order_count(const uint64_t* __restrict__ offs, uint64_t n,
+                                                     uint32_t* __restrict__ counts) {
+    __shared__ uint32_t h[kOrderBuckets];
+    for (uint32_t i = threadIdx.x; i < kOrderBuckets; i += 256) h[i] = 0;
+    __syncthreads();
+    uint64_t lo, hi;
+    order_part(n, blockIdx.x, &lo, &hi);
+    for (uint64_t i = lo + threadIdx.x; i < hi; i += 256) atomicAdd(&h[order_bucket(offs[i])], 1u);
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < kOrderBuckets; i += 256) counts[i * kOrderParts + blockIdx.x] = h[i];
+}
+
+// one wave per bucket: its row of the count matrix -> each part's offset inside the
+// bucket; the bucket's total goes to bounds[B + b]
+__global__ __launch_bounds__(256) void k_order_scan_rows(uint32_t* __restrict__ counts, uint32_t* __restrict__ bounds) {
+    static_assert(kOrderParts == 128, "two parts per lane");
+    const uint32_t lane = threadIdx.x & 63, b = blockIdx.x * 4 + (threadIdx.x >> 6);
+    uint32_t* row = counts + b * kOrderParts + lane * 2;
+    const uint32_t c0 = row[0], c1 = row[1];
+    uint32_t inc = c0 + c1;
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+        const uint32_t up = __shfl_up(inc, d);
+        if (lane >= d) inc += up;
+    }
+    const uint32_t ex = inc - c0 - c1;
+    row[0] = ex;
+    row[1] = ex + c0;
+    if (lane == 63) bounds[kOrderBuckets + b] = inc;
+}
+
+// one workgroup of 1024 threads: bucket totals -> bounds[b] / bounds[B + b] = bucket b's
+// first / one-past-last position
+__global__ __launch_bounds__(1024) void k_order_scan_buckets(uint32_t* __restrict__ bounds) {
+    constexpr uint32_t PER = kOrderBuckets / 1024;
+    __shared__ uint32_t part[1024];
+    uint32_t c[PER], sum = 0;
+    for (uint32_t k = 0; k < PER; ++k) sum += c[k] = bounds[kOrderBuckets + threadIdx.x * PER + k];
+    part[threadIdx.x] = sum;
+    __syncthreads();
+    for (uint32_t d = 1; d < 1024; d <<= 1) {  // inclusive Hillis-Steele scan of the thread sums
+        const uint32_t add = threadIdx.x >= d ? part[threadIdx.x - d] : 0;
+        __syncthreads();
+        part[threadIdx.x] += add;
+        __syncthreads();
+    }
+    uint32_t run = part[threadIdx.x] - sum;
+    for (uint32_t k = 0; k < PER; ++k) {
+        const uint32_t b = threadIdx.x * PER + k;
+        bounds[b] = run;
+        run += c[k];
+        bounds[kOrderBuckets + b] = run;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_order_place(const uint64_t* __restrict__ offs, uint64_t n,
+                                                     const uint32_t* __restrict__ counts,
+                                                     const uint32_t* __restrict__ bounds, uint32_t* __restrict__ order) {
+    __shared__ uint32_t pos[kOrderBuckets];
+    for (uint32_t i = threadIdx.x; i < kOrderBuckets; i += 256) pos[i] = bounds[i] + counts[i * kOrderParts + blockIdx.x];
+    __syncthreads();
+    uint64_t lo, hi;
+    order_part(n, blockIdx.x, &lo, &hi);
+    for (uint64_t i = lo + threadIdx.x; i < hi; i += 256)
+        order[atomicAdd(&pos[order_bucket(offs[i])], 1u)] = static_cast<uint32_t>(i);
+}
+
+constexpr uint32_t kOrderSortMax = 2048;
+
+// one workgroup per bucket: its entries order[start[b] .. end[b]) sorted by offset (larger
+// buckets stay in placement order)
+// Sort key: [offset inside the 32 MiB region] [the entry's index in the bucket], one
+// 64-bit compare-exchange per pair (bitonic, one pair per thread per pass); the index
+// finds the block's number and offset, kept in LDS. The bucket's offsets and lengths are
+// written in the new order too (s_offs, s_lens), so the hash kernel reads them
+// sequentially; only the checksum store goes through order. Grouping a region's blocks by
+// tile count first (fewer masked rows in a wave) measured worse: 0.78 against 0.85 of
+// 8 TB/s on the shuffled storm-length gather (profiles/r03k/), address order wins.
+__global__ __launch_bounds__(256) void k_order_sort(const uint64_t* __restrict__ offs, const uint32_t* __restrict__ lens,
+                                                    const uint32_t* __restrict__ bounds, uint32_t* __restrict__ order,
+                                                    uint64_t* __restrict__ s_offs, uint32_t* __restrict__ s_lens) {
+    static_assert(kOrderSortMax <= 2048 && kOrderShift + 11 <= 64, "key fields");
+    __shared__ uint64_t key[kOrderSortMax];
+    __shared__ uint64_t off[kOrderSortMax];
+    __shared__ uint32_t val[kOrderSortMax];
+    const uint32_t lo = bounds[blockIdx.x], cnt = bounds[kOrderBuckets + blockIdx.x] - lo;
+    if (cnt > kOrderSortMax) {  // left in placement order
+        for (uint32_t i = threadIdx.x; i < cnt; i += 256) {
+            const uint32_t v = order[lo + i];
+            s_offs[lo + i] = offs[v];
+            if (lens) s_lens[lo + i] = lens[v];
+        }
+        return;
+    }
+    uint32_t m = 2;
+    while (m < cnt) m <<= 1;
+    constexpr uint64_t kRegion = (uint64_t{1} << kOrderShift) - 1;
+    for (uint32_t i = threadIdx.x; i < m; i += 256) {
+        uint64_t k = ~uint64_t{0};
+        if (i < cnt) {
+            const uint32_t v = order[lo + i];
+            const uint64_t o = offs[v];
+            val[i] = v;
+            off[i] = o;
+            k = ((o & kRegion) << 11) | i;
+        }
+        key[i] = k;
+    }
+    __syncthreads();
+    for (uint32_t k = 2; k <= m; k <<= 1) {
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            for (uint32_t t = threadIdx.x; t < m / 2; t += 256) {
+                const uint32_t i = 2 * j * (t / j) + t % j, p = i + j;
+                const uint64_t a = key[i], c = key[p];
+                if ((a > c) == ((i & k) == 0)) {
+                    key[i] = c;
+                    key[p] = a;
+                }
+            }
+            __syncthreads();
+        }
+    }
+    for (uint32_t i = threadIdx.x; i < cnt; i += 256) {
+        const uint32_t e = static_cast<uint32_t>(key[i]) & 2047;
+        const uint32_t v = val[e];
+        order[lo + i] = v;
+        s_offs[lo + i] = off[e];
+        if (lens) s_lens[lo + i] = lens[v];
+    }
+}
+
+// The stripes of a block that k_xxh64_glds_var did not stage (a start that is not 16-byte
+// aligned), straight from global memory. Out of line: the kernel's hot loop stays compact.
+__device__ __noinline__ uint64_t var_stripes_from_global(const uint8_t* p, uint32_t nst, uint32_t j, uint64_t acc) {
+    if ((reinterpret_cast<uintptr_t>(p) & 7) == 0)
+        return quad_stripes_aligned<16>(reinterpret_cast<const uint64_t*>(p) + j, nst, acc);
+    return quad_stripes_unaligned(p + 8 * j, nst, acc);
+}
+
+// ORD: offs and lens are in a locality order of a large gather (k_order_*, s_offs /
+// s_lens), and order[i] is the index of the i-th block: its checksum's slot.
+template <int T, int AUX, bool VERIFY, int WAVES, int SKEW, bool LENS, bool OFFS, bool ORD = false>
 __global__ __launch_bounds__(64 * WAVES) void k_xxh64_glds_var(const uint8_t* __restrict__ base, uint64_t stride,
                                                                const uint32_t* __restrict__ lens, uint32_t len,
                                                                const uint64_t* __restrict__ offs, uint64_t n,
                                                                uint64_t* __restrict__ out,
                                                                const uint64_t* __restrict__ expected,
                                                                unsigned long long* __restrict__ first_bad,
-                                                               unsigned long long* __restrict__ n_bad) {
+                                                               unsigned long long* __restrict__ n_bad,
+                                                               const uint32_t* __restrict__ order = nullptr) {
     constexpr int BPW = 16 * WAVES;
     constexpr int ROW = 32 * T;
     constexpr int TILE = BPW * ROW;
@@ -1173,16 +1340,20 @@ __global__ __launch_bounds__(64 * WAVES) void k_xxh64_glds_var(const uint8_t* __
     uint64_t ig = blockIdx.x;
     [[maybe_unused]] uint32_t it = 0;  // tile of group ig to issue next (used by the device pass)
     uint32_t i_ntl = 0;
+    [[maybe_unused]] uint32_t i_full = 0;  // whole-tile stripe bytes of every block (device pass)
     bool i_done = false;
     auto i_switch = [&]() __attribute__((always_inline)) {  // make the prefetched group current, prefetch the one after
-        uint32_t tiles = 0;
+        uint32_t tiles = 0, lim_min = 0xffffffffu;
 #pragma unroll
         for (int k = 0; k < PER_WAVE; ++k) {
             i_src[k] = i_np[k] + pofs[k];
             i_lim[k] = staged_bytes(i_np[k], i_nl[k]);
             tiles = max(tiles, (i_lim[k] + ROW - 1) / ROW);
+            lim_min = min(lim_min, i_lim[k]);
         }
         i_ntl = wave_max(tiles);
+        // stripe bytes every block of the wave has, in whole tiles: tiles below it are full
+        i_full = ~wave_max(~lim_min) / ROW * ROW;
         i_fetch(ig + G);
     };
     auto i_next_group = [&]() __attribute__((always_inline)) {  // the next group with tiles for this wave
@@ -1200,12 +1371,19 @@ __global__ __launch_bounds__(64 * WAVES) void k_xxh64_glds_var(const uint8_t* __
     i_switch();
     if (i_ntl == 0) i_next_group();
 #if defined(__HIP_DEVICE_COMPILE__)
+    // a tile every piece of the wave has (all its blocks still have >= a whole tile left)
+    // issues unmasked, as k_xxh64_glds_skew; a block's partial last tile masks by piece
 #define STORMCK_GLDS_VAR_ISSUE(SLOT)                                                                   \
     do {                                                                                               \
         uint8_t* dst_ = lds + (SLOT) * TILE + wave * PER_WAVE * 1024;                                  \
         const uint32_t t0_ = it * ROW;                                                                 \
-        _Pragma("unroll") for (int k_ = 0; k_ < PER_WAVE; ++k_) if (t0_ + pofs[k_] < i_lim[k_])        \
-            __builtin_amdgcn_global_load_lds(i_src[k_] + t0_, dst_ + k_ * 1024, 16, 0, AUX);          \
+        if (__builtin_expect(t0_ + ROW <= i_full, 1)) {                                                \
+            _Pragma("unroll") for (int k_ = 0; k_ < PER_WAVE; ++k_)                                    \
+                __builtin_amdgcn_global_load_lds(i_src[k_] + t0_, dst_ + k_ * 1024, 16, 0, AUX);      \
+        } else {                                                                                       \
+            _Pragma("unroll") for (int k_ = 0; k_ < PER_WAVE; ++k_) if (t0_ + pofs[k_] < i_lim[k_])    \
+                __builtin_amdgcn_global_load_lds(i_src[k_] + t0_, dst_ + k_ * 1024, 16, 0, AUX);      \
+        }                                                                                              \
         ++it;                                                                                          \
     } while (0)
 #else
@@ -1217,6 +1395,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_xxh64_glds_var(const uint8_t* __
     const uint32_t rot = glds_rot<T>(b);
     const uint8_t* h_np = nullptr;  // next group, prefetched
     uint32_t h_nl = 0;
+    uint64_t h_nidx = 0;  // the block's index (its checksum's slot)
     bool h_nlive = false;
     auto h_fetch = [&](uint64_t g) __attribute__((always_inline)) {
         const uint64_t gb = g * BPW + b;
@@ -1225,9 +1404,11 @@ __global__ __launch_bounds__(64 * WAVES) void k_xxh64_glds_var(const uint8_t* __
         const uint32_t l = LENS ? lens[gc] : len;  // unconditional, as i_fetch
         h_np = block_ptr(gc);
         h_nl = h_nlive ? l : 0;
+        h_nidx = ORD ? order[gc] : gc;
     };
     uint64_t hg = blockIdx.x;
     uint32_t ht = 0, h_ntl = 0, h_L = 0, h_nst = 0, h_sst = 0;
+    uint64_t h_idx = 0;
     const uint8_t* h_p = nullptr;
     bool h_live = false, h_done = false;
     uint64_t acc = acc_seed(j);
@@ -1240,6 +1421,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_xxh64_glds_var(const uint8_t* __
         h_p = h_np;
         h_L = h_nl;
         h_live = h_nlive;
+        h_idx = h_nidx;
         h_nst = h_L >> 5;
         const uint32_t sb = staged_bytes(h_p, h_L);
         h_sst = sb >> 5;  // stripes through LDS (h_nst, or 0 if not staged)
@@ -1255,15 +1437,10 @@ __global__ __launch_bounds__(64 * WAVES) void k_xxh64_glds_var(const uint8_t* __
         h_fetch(hg + G);
     };
     auto h_finish = [&]() __attribute__((always_inline)) {  // the group's blocks are complete: unstaged stripes, tail, checksum
-        if (h_sst < h_nst) {
-            if ((reinterpret_cast<uintptr_t>(h_p) & 7) == 0)
-                acc = quad_stripes_aligned<16>(reinterpret_cast<const uint64_t*>(h_p) + j, h_nst, acc);
-            else
-                acc = quad_stripes_unaligned(h_p + 8 * j, h_nst, acc);
-        }
+        if (__builtin_expect(h_sst < h_nst, 0)) acc = var_stripes_from_global(h_p, h_nst, j, acc);
         const uint64_t v1 = quad_bcast<0>(acc), v2 = quad_bcast<1>(acc), v3 = quad_bcast<2>(acc), v4 = quad_bcast<3>(acc);
         if (j == 0 && h_live) {
-            const uint64_t gbk = hg * BPW + b;
+            const uint64_t gbk = h_idx;
             const uint64_t h0 = (h_L >= 32) ? converge(v1, v2, v3, v4) : kP5;
             const uint64_t h = h_sst == h_nst && h_L >= 32 ? finish_regs(h0, h_L, tail, h_L & 31)
                                                            : finish_fast(h0, h_L, h_p + 32 * static_cast<uint64_t>(h_nst), h_L & 31);
@@ -1312,13 +1489,13 @@ __global__ __launch_bounds__(64 * WAVES) void k_xxh64_glds_var(const uint8_t* __
         wait_vmcnt<0>();
         __builtin_amdgcn_s_barrier();
         const uint32_t finished = __hip_atomic_load(n_finished, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        if (h_fin) {
+        if (__builtin_expect(h_fin, 0)) {
             h_fin = false;
             h_finish();
             h_next_group();
         }
         if (u + 1 >= ph && !i_done) {
-            if (it == i_ntl) {
+            if (__builtin_expect(it == i_ntl, 0)) {
                 it = 0;
                 i_next_group();
             }
@@ -1336,7 +1513,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_xxh64_glds_var(const uint8_t* __
                 const uint32_t q = (2 * s + (j >> 1) + 2 * T - rot) % (2 * T);
                 w[s] = *reinterpret_cast<const uint64_t*>(row + q * 16);
             }
-            if (s0 + T <= h_sst) {
+            if (__builtin_expect(s0 + T <= h_sst, 1)) {
 #pragma unroll
                 for (int s = 0; s < T; ++s) acc = round(acc, w[s]);
             } else {

@@ -276,13 +276,14 @@ uint32_t pipe_staging() {
     return slots;
 }
 
-// 16 blocks per workgroup (one full chain wave) through 4-slot rings of 2 KiB chunks, for
-// batches of 9..16 blocks per CU. Probe knob STORMCK_WIDE16=0 sends them to the quad
-// kernel (A/B).
+// 16 blocks per workgroup (one full chain wave) through 4-slot rings of 2 KiB chunks with
+// double-buffered stagers, for batches of 9..16 blocks per CU: measured no faster than
+// the register-quad kernel (2,049 / 3,072 / 4,096 blocks of 31,808 B: 33.2 / 35.3 / 38.1
+// against 34.7 / 35.0 / 35.1 us, profiles/r03c/), so off; probe knob STORMCK_WIDE16=1.
 bool wide16_on() {
     static const bool on = [] {
         const char* e = std::getenv("STORMCK_WIDE16");
-        return !(e && e[0] == '0');
+        return e && e[0] == '1';
     }();
     return on;
 }
@@ -296,8 +297,34 @@ uint64_t multi_bpw(uint64_t n, uint64_t ncu) {
     if (ncu == 0) return 0;
     if (n <= kMultiBpw * ncu) return kMultiBpw;
     if (pipe_staging() && n <= kMultiBpwRing * ncu) return kMultiBpwRing;
-    if (pipe_staging() && n <= kMultiBpwWide * ncu && wide16_on()) return kMultiBpwWide;
+    if (pipe_staging() && n <= kMultiBpwWide * ncu && wide16_on()) return kMultiBpwWide;  // probe knob only
     return 0;
+}
+
+// The stream-ordered workspaces come from the device's default pool; keep what it has
+// reserved across calls instead of returning it at every synchronisation (once per device).
+void keep_pool_memory() {
+    static std::atomic<bool> done[64] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64 || done[dev].load()) return;
+    hipMemPool_t pool = nullptr;
+    if (hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess) {
+        uint64_t thr = UINT64_MAX;
+        (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr);
+    }
+    (void)hipGetLastError();
+    done[dev].store(true);
+}
+
+// Gathers of at least this many blocks visit them in a locality order (k_order_*); probe
+// knob STORMCK_GATHER_ORDER=0 turns it off (A/B).
+constexpr uint64_t kOrderMinBlocks = 1u << 20;
+bool order_on() {
+    static const bool on = [] {
+        const char* e = std::getenv("STORMCK_GATHER_ORDER");
+        return !(e && e[0] == '0');
+    }();
+    return on;
 }
 
 bool grid_for(uint64_t threads, dim3* grid) {
@@ -413,9 +440,52 @@ int launch_checksum(const uint8_t* base, uint64_t stride, const uint32_t* lens, 
         const uint64_t tiles = lens ? uint64_t{32768 / 32 / kTileStripes} : (uint64_t{len} / 32 + kTileStripes - 1) / kTileStripes;
         const bool persistent = big && cus > 0 && wgs >= cus && (wgs + cus - 1) / cus * tiles >= kSkewMinSteps;
         const dim3 grid(static_cast<unsigned>(persistent ? cus : wgs));
+        // large gathers visit their blocks in a locality order (kernels.h k_order_*): a
+        // stream-ordered workspace (the count matrix, the order, the offsets and lengths in
+        // that order: 16 bytes per block), freed on the stream after the launch
+        if (offs && !verify && big && n >= kOrderMinBlocks && n < (uint64_t{1} << 32) && order_on()) {
+            keep_pool_memory();
+            const uint64_t words = (uint64_t{kOrderBuckets} * (kOrderParts + 2) + n + 1) & ~uint64_t{1};
+            void* ws = nullptr;
+            HIP_TRY(hipMallocAsync(&ws, words * 4 + n * 8 + (lens ? n * 4 : 0), st));
+            uint32_t* counts = static_cast<uint32_t*>(ws);  // [bucket][part], then positions
+            uint32_t* bounds = counts + kOrderBuckets * kOrderParts;
+            uint32_t* order = bounds + 2 * kOrderBuckets;
+            uint64_t* s_offs = reinterpret_cast<uint64_t*>(counts + words);
+            uint32_t* s_lens = lens ? reinterpret_cast<uint32_t*>(s_offs + n) : nullptr;
+            hipLaunchKernelGGL(k_order_count, dim3(kOrderParts), dim3(256), 0, st, offs, n, counts);
+            hipLaunchKernelGGL(k_order_scan_rows, dim3(kOrderBuckets / 4), dim3(256), 0, st, counts, bounds);
+            hipLaunchKernelGGL(k_order_scan_buckets, dim3(1), dim3(1024), 0, st, bounds);
+            hipLaunchKernelGGL(k_order_place, dim3(kOrderParts), dim3(256), 0, st, offs, n, counts, bounds, order);
+            hipLaunchKernelGGL(k_order_sort, dim3(kOrderBuckets), dim3(256), 0, st, offs, lens, bounds, order, s_offs, s_lens);
+            lens = s_lens;
+            offs = s_offs;
+            if (persistent) {
+                if (lens)
+                    hipLaunchKernelGGL((k_xxh64_glds_var<kTileStripes, kAuxNT, false, kGldsWaves, kSkewTiles, true, true, true>),
+                                       grid, dim3(kGldsThreads), 0, st, base, stride, lens, len, offs, n, out, expected,
+                                       first_bad, n_bad, order);
+                else
+                    hipLaunchKernelGGL((k_xxh64_glds_var<kTileStripes, kAuxNT, false, kGldsWaves, kSkewTiles, false, true, true>),
+                                       grid, dim3(kGldsThreads), 0, st, base, stride, lens, len, offs, n, out, expected,
+                                       first_bad, n_bad, order);
+            } else {
+                if (lens)
+                    hipLaunchKernelGGL((k_xxh64_glds_var<kTileStripes, kAuxNT, false, kGldsWaves, 0, true, true, true>),
+                                       grid, dim3(kGldsThreads), 0, st, base, stride, lens, len, offs, n, out, expected,
+                                       first_bad, n_bad, order);
+                else
+                    hipLaunchKernelGGL((k_xxh64_glds_var<kTileStripes, kAuxNT, false, kGldsWaves, 0, false, true, true>),
+                                       grid, dim3(kGldsThreads), 0, st, base, stride, lens, len, offs, n, out, expected,
+                                       first_bad, n_bad, order);
+            }
+            HIP_TRY(hipGetLastError());
+            HIP_TRY(hipFreeAsync(ws, st));
+            return STORMCK_OK;
+        }
 #define STORMCK_VAR(VER, W, SK, LN, OF)                                                                          \
     hipLaunchKernelGGL((k_xxh64_glds_var<kTileStripes, kAuxNT, VER, W, SK, LN, OF>), grid, dim3(64 * W), 0, st, base, \
-                       stride, lens, len, offs, n, out, expected, first_bad, n_bad)
+                       stride, lens, len, offs, n, out, expected, first_bad, n_bad, nullptr)
 #define STORMCK_VAR_SHAPE(LN, OF)                                                                                \
     do {                                                                                                         \
         if (!big) {                                                                                              \
@@ -921,7 +991,13 @@ int stormck_device_alloc(uint64_t bytes, void** d_ptr) {
     if (bytes == 0) return fail(STORMCK_EINVAL, "bytes is 0");
     int rc = device_check();
     if (rc) return rc;
-    HIP_TRY(hipMalloc(d_ptr, bytes));
+    // probe knob STORMCK_ALLOC_CONTIGUOUS=1: physically contiguous (large page fragments)
+    static const bool contiguous = [] {
+        const char* e = std::getenv("STORMCK_ALLOC_CONTIGUOUS");
+        return e && e[0] == '1';
+    }();
+    if (contiguous) HIP_TRY(hipExtMallocWithFlags(d_ptr, bytes, hipDeviceMallocContiguous));
+    else HIP_TRY(hipMalloc(d_ptr, bytes));
     return STORMCK_OK;
 }
 

@@ -75,6 +75,36 @@ def main(tag, arena):
     alg = arena * (BLOCK + 8)
     stats = [r for r in rows(files["kernel_stats.csv"]) if KERNEL in r["Name"]]
     avg_ns = float(stats[0]["AverageNs"])
+    # the bench's timed launches in the same trace: the last launch_ms.n dispatches of the
+    # dominant kernel (settle and warmup launches come first), to compare with the HIP
+    # events the bench line's frac comes from
+    trace_csv = glob.glob(os.path.join(src, "trace", "**", "*kernel_trace.csv"), recursive=True)
+    timed = None
+    if trace_csv and bench_line:
+        shutil.copy(trace_csv[0], os.path.join(dst, "kernel_trace.csv"))
+        disp = [r for r in rows(trace_csv[0]) if KERNEL in r["Kernel_Name"]]
+        disp.sort(key=lambda r: int(r["Start_Timestamp"]))
+        k = bench_line["roofline"]["launch_ms"]["n"]
+        last = disp[-k:]
+        t_ms = sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in last) / len(last) * 1e-6
+        timed = {"launches": len(last), "avg_launch_ms": round(t_ms, 4),
+                 "frac": round(arena * (BLOCK + 8) / (t_ms * 1e-3) / PEAK, 4),
+                 "bench_hip_event_avg_ms": bench_line["roofline"]["avg_launch_ms"],
+                 "agreement": round(t_ms / bench_line["roofline"]["avg_launch_ms"], 4)}
+    # the spread over fresh processes of the same session (placement), if collected
+    spread = None
+    plain = sorted(glob.glob(os.path.join(src, "plain_*.log")))
+    fr = []
+    for f in plain:
+        ln = [x for x in open(f) if x.startswith("{")]
+        if ln:
+            fr.append(json.loads(ln[-1])["roofline"]["frac"])
+            shutil.copy(f, os.path.join(dst, os.path.basename(f)))
+    if fr:
+        fr_all = sorted(fr + ([bench_line["roofline"]["frac"]] if bench_line else []))
+        spread = {"processes": len(fr_all), "median": fr_all[len(fr_all) // 2], "min": fr_all[0], "max": fr_all[-1],
+                  "fracs": fr_all, "what": "bench.py c3 frac in fresh processes of one session (plain and the "
+                                           "profiled one): the spread the arena's HBM placement gives"}
     out = {"kernel": "k_xxh64_glds_skew<16,nt,8w,4KiB>", "arena_blocks": arena, "fetch_size_kb": fk,
            "write_size_kb": wk, "fetch_correction": round(corr, 4), "hbm_bytes_per_launch": int(hbm),
            "algorithmic_bytes_per_launch": alg, "traffic_over_algorithmic": round(hbm / alg, 4),
@@ -82,6 +112,7 @@ def main(tag, arena):
            "profile_min_launch_ms": round(float(stats[0]["MinNs"]) * 1e-6, 4),
            "profile_max_launch_ms": round(float(stats[0]["MaxNs"]) * 1e-6, 4),
            "profile_frac": round(alg / (avg_ns * 1e-9) / PEAK, 4),
+           "profile_timed_launches": timed, "placement_spread": spread,
            "bench_under_rocprof": {"frac": bench_line["roofline"]["frac"] if bench_line else None,
                                    "avg_launch_ms": bench_line["roofline"]["avg_launch_ms"] if bench_line else None},
            "source": os.path.relpath(dst, ROOT)}

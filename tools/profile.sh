@@ -11,8 +11,13 @@ OUT=$R/gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 cd /tmp || exit 1
+# fresh plain processes first (the placement spread the line is drawn from), then the
+# profiled one
+for i in 1 2 3; do
+  timeout -k 10 300 python3 "$R/bench.py" --steps 5 --warmup 1 --no-cpu > "$OUT/plain_$i.log" 2>&1 || { echo "plain $i failed rc=$?"; exit 1; }
+done
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o trace -- \
-    python3 "$R/bench.py" --steps 3 --warmup 1 --no-cpu > "$OUT/trace.log" 2>&1 || { echo "trace failed rc=$?"; exit 1; }
+    python3 "$R/bench.py" --steps 5 --warmup 1 --no-cpu > "$OUT/trace.log" 2>&1 || { echo "trace failed rc=$?"; exit 1; }
 timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch" -o fetch -- \
     python3 "$R/bench.py" --steps 1 --warmup 0 --no-cpu --blocks 4194304 > "$OUT/fetch.log" 2>&1 || { echo "fetch failed rc=$?"; exit 1; }
 timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write" -o write -- \
