@@ -144,3 +144,34 @@ def test_var_kernel_edges(dev, n, slot):
     want_u = o.checksum_batch(host, n, slot, L, threads=16)
     bad = np.nonzero(_u64(out) != want_u)[0]
     assert bad.size == 0, (n, slot, "uniform gather", bad.size, bad[:8])
+
+
+@pytest.mark.timeout(600)
+def test_gather_locality_order_repeats(dev):
+    """The locality order (kernels.h k_order_*) on a gather that repeats slots: 1.2M
+    draws with replacement from 1.25M slots of 16 KiB, so 32 MiB regions hold ~2,048
+    entries each, some more than the in-LDS sort takes (left in placement order) and
+    some fewer (sorted), with equal offsets in one region."""
+    from storm_amd import engine
+    slots, slot, n = 1_250_000, 16384, 1_200_000
+    rng = np.random.default_rng(11)
+    slot_len = rng.integers(0, slot + 1, size=slots).astype(np.uint32)
+    pick = rng.integers(0, slots, size=n).astype(np.uint64)
+    lens = slot_len[pick]
+    arena = torch.empty((slots, slot), dtype=torch.uint8, device=dev)
+    engine.fill_synthetic_device(arena.data_ptr(), slot, slots, 7, o.SYNTH_SEED)
+    d_offs = torch.from_numpy((pick * np.uint64(slot)).view(np.int64)).to(dev)
+    d_lens = torch.from_numpy(lens.view(np.int32)).to(dev)
+    out = torch.empty(n, dtype=torch.int64, device=dev)
+    engine.checksum_gather_device(arena.data_ptr(), d_offs.data_ptr(), n, out.data_ptr(), 0, d_lens.data_ptr())
+    torch.cuda.synchronize()
+    counts = np.bincount((pick * np.uint64(slot) >> np.uint64(25)).astype(np.int64))
+    assert counts.max() > 2048 and counts.min() <= 2048  # both sides of the sort limit
+    want_by_slot = np.empty(slots, dtype=np.uint64)
+    piece = 1 << 17
+    for c0 in range(0, slots, piece):
+        host = arena[c0:c0 + piece].cpu().numpy()
+        m = host.shape[0]
+        want_by_slot[c0:c0 + m] = o.checksum_batch(host, m, slot, 0, lens=slot_len[c0:c0 + m], threads=16)
+    bad = np.nonzero(_u64(out) != want_by_slot[pick])[0]
+    assert bad.size == 0, f"{bad.size} of {n} blocks differ from the oracle, first {int(bad[0])}"

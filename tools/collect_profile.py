@@ -7,6 +7,8 @@ From gpurun_out/prof_<tag>/:
   fetch/**/*counter_collection.csv   -> pmc_fetch_size.csv   (separate --pmc FETCH_SIZE pass)
   write/**/*counter_collection.csv   -> pmc_write_size.csv   (separate --pmc WRITE_SIZE pass)
   calib/**/*counter_collection.csv   -> pmc_fetch_calibration_probe.csv
+  gather_{trace,fetch,write}/...     -> gather_*.csv, gather_traffic.json (the gather
+                                        workload: hash kernel + locality-order kernels)
 
 traffic.json (per launch of the dominant kernel, one 4M-block arena pass):
   hbm_bytes_per_launch = FETCH_SIZE x 1024 x correction + WRITE_SIZE x 1024, where the
@@ -117,6 +119,65 @@ def main(tag, arena):
                                    "avg_launch_ms": bench_line["roofline"]["avg_launch_ms"] if bench_line else None},
            "source": os.path.relpath(dst, ROOT)}
     with open(os.path.join(ROOT, "profiles", "traffic.json"), "w") as f:
+        json.dump(out, f, indent=1)
+    print(json.dumps(out))
+    if os.path.isdir(os.path.join(src, "gather_trace")):
+        gather(src, dst, corr)
+
+
+GATHER_KERNEL = "k_xxh64_glds_var<16, 2, false, 8, 8, true, true, true>"
+
+
+def last_json(path):
+    line = None
+    with open(path) as f:
+        for x in f:
+            if x.startswith("{"):
+                line = json.loads(x)
+    return line
+
+
+def gather(src, dst, corr):
+    """The gather workload's session: per launch of the hash kernel, HBM bytes from the
+    FETCH_SIZE / WRITE_SIZE passes against the algorithmic bytes of the bench line, and
+    the locality-order kernels' share of the launch."""
+    files = {
+        "gather_kernel_stats.csv": one(os.path.join(src, "gather_trace", "**", "*kernel_stats.csv")),
+        "gather_pmc_fetch_size.csv": one(os.path.join(src, "gather_fetch", "**", "*counter_collection.csv")),
+        "gather_pmc_write_size.csv": one(os.path.join(src, "gather_write", "**", "*counter_collection.csv")),
+    }
+    for name, path in files.items():
+        shutil.copy(path, os.path.join(dst, name))
+    line = last_json(os.path.join(src, "gather_trace.log"))
+    with open(os.path.join(dst, "gather_bench_under_rocprof.json"), "w") as f:
+        json.dump(line, f, indent=1)
+    alg = line["roofline"]["algorithmic_bytes_per_launch"]
+
+    def per_kernel(path):
+        acc = {}
+        for r in rows(path):
+            name = r["Kernel_Name"]
+            acc.setdefault(name, []).append(float(r["Counter_Value"]))
+        return {k: sum(v) / len(v) for k, v in acc.items()}
+
+    fetch, write = per_kernel(files["gather_pmc_fetch_size.csv"]), per_kernel(files["gather_pmc_write_size.csv"])
+    hk = [k for k in fetch if GATHER_KERNEL in k][0]
+    hbm = fetch[hk] * 1024 * corr + write[[k for k in write if GATHER_KERNEL in k][0]] * 1024
+    stats = {r["Name"]: r for r in rows(files["gather_kernel_stats.csv"])}
+    hs = [v for k, v in stats.items() if GATHER_KERNEL in k][0]
+    order_ns = sum(float(v["AverageNs"]) for k, v in stats.items() if "k_order_" in k)
+    order_bytes = sum(fetch[k] * 1024 * corr for k in fetch if "k_order_" in k) + \
+        sum(write[k] * 1024 for k in write if "k_order_" in k)
+    out = {"kernel": "k_xxh64_glds_var<16,nt,8w,4KiB,lens,offs,ordered>",
+           "workload": line["config"]["workload"], "algorithmic_bytes_per_launch": alg,
+           "hbm_bytes_per_launch": int(hbm), "traffic_over_algorithmic": round(hbm / alg, 4),
+           "profile_calls": int(hs["Calls"]), "profile_avg_launch_ms": round(float(hs["AverageNs"]) * 1e-6, 4),
+           "profile_frac_hash_kernel": round(alg / (float(hs["AverageNs"]) * 1e-9) / PEAK, 4),
+           "order_kernels_avg_us": round(order_ns * 1e-3, 1), "order_kernels_hbm_bytes": int(order_bytes),
+           "bench_under_rocprof": {"frac": line["roofline"]["frac"], "avg_launch_ms": line["roofline"]["avg_launch_ms"],
+                                   "note": "bench launch = order kernels + hash kernel"},
+           "source": os.path.relpath(dst, ROOT)}
+    with open(os.path.join(dst, "gather_traffic.json"), "w") as f:
         json.dump(out, f, indent=1)
     print(json.dumps(out))
 

@@ -24,5 +24,13 @@ timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write"
     python3 "$R/bench.py" --steps 1 --warmup 0 --no-cpu --blocks 4194304 > "$OUT/write.log" 2>&1 || { echo "write failed rc=$?"; exit 1; }
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/calib" -o calib -- \
     "$R/tools/probe" 8 1 > "$OUT/calib.log" 2>&1 || { echo "calib failed rc=$?"; exit 1; }
+# the gather workload (storm's dirty slots: 4M storm-length blocks, shuffled slots):
+# kernel trace, FETCH_SIZE / WRITE_SIZE of one step
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/gather_trace" -o trace -- \
+    python3 "$R/bench.py" --workload gather --steps 5 --warmup 1 > "$OUT/gather_trace.log" 2>&1 || { echo "gather trace failed rc=$?"; exit 1; }
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/gather_fetch" -o fetch -- \
+    python3 "$R/bench.py" --workload gather --steps 1 --warmup 0 > "$OUT/gather_fetch.log" 2>&1 || { echo "gather fetch failed rc=$?"; exit 1; }
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/gather_write" -o write -- \
+    python3 "$R/bench.py" --workload gather --steps 1 --warmup 0 > "$OUT/gather_write.log" 2>&1 || { echo "gather write failed rc=$?"; exit 1; }
 echo "profile done"
 # then, in the build container: python tools/collect_profile.py <tag>
