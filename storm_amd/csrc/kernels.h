@@ -110,6 +110,55 @@ __device__ __forceinline__ uint64_t quad_stripes_aligned(const uint64_t* __restr
     return acc;
 }
 
+// quad_stripes_aligned with D groups of U loads in flight (D - 1 ahead of the one being
+// hashed), rotated through registers. Loads of groups past the last are clamped to it, so
+// no load sits under a branch; the last D - 1 groups hash from registers.
+template <int U, int D>
+__device__ __forceinline__ uint64_t quad_stripes_deep(const uint64_t* __restrict__ p, uint32_t nst, uint64_t acc) {
+    static_assert(D >= 2, "at least one group ahead");
+    // the scheduler would interleave the groups' loads, and the counted vmcnt wait for
+    // one group would then drain the others: sched barriers keep each group's loads
+    // together and in order
+    auto fence = []() __attribute__((always_inline)) {
+#if defined(__HIP_DEVICE_COMPILE__)
+        __builtin_amdgcn_sched_barrier(0);
+#endif
+    };
+    const uint32_t G = nst / U;
+    if (G > 0) {
+        uint64_t w[D][U];
+        const uint32_t last = G - 1;
+#pragma unroll
+        for (int d = 0; d < D - 1; ++d) {
+            const uint64_t* q = p + 4 * U * min(static_cast<uint32_t>(d), last);
+#pragma unroll
+            for (int u = 0; u < U; ++u) w[d][u] = q[4 * u];
+            fence();
+        }
+        uint32_t g = 0;
+        for (; g + D <= G; g += D) {
+#pragma unroll
+            for (int d = 0; d < D; ++d) {
+                const uint64_t* q = p + 4 * U * min(g + d + D - 1, last);
+#pragma unroll
+                for (int u = 0; u < U; ++u) w[(d + D - 1) % D][u] = q[4 * u];
+                fence();
+#pragma unroll
+                for (int u = 0; u < U; ++u) acc = round(acc, w[d][u]);
+                fence();
+            }
+        }
+#pragma unroll
+        for (int d = 0; d < D - 1; ++d)
+            if (static_cast<uint32_t>(d) < G - g) {
+#pragma unroll
+                for (int u = 0; u < U; ++u) acc = round(acc, w[d][u]);
+            }
+    }
+    for (uint32_t s = G * U; s < nst; ++s) acc = round(acc, p[4 * s]);
+    return acc;
+}
+
 // Byte-granular stripe loop for blocks whose start is not 8-byte aligned.
 __device__ __forceinline__ uint64_t quad_stripes_unaligned(const uint8_t* p, uint32_t nst, uint64_t acc) {
     for (uint32_t s = 0; s < nst; ++s) acc = round(acc, ld64_unaligned(p + 32 * s));
@@ -187,15 +236,15 @@ __device__ __forceinline__ uint64_t finish_lds16(uint64_t h, uint64_t n, const u
 // VERIFY: instead of writing the checksum, compare with expected[i]; on mismatch
 // atomically lower *first_bad to i and count into *n_bad.
 // ---------------------------------------------------------------------------
-template <int U, bool LENS, bool OFFS, bool VERIFY, bool NT = false>
-__global__ __launch_bounds__(256) void k_xxh64_quad(const uint8_t* __restrict__ base, uint64_t stride,
+template <int U, bool LENS, bool OFFS, bool VERIFY, bool NT = false, int D = 0, int TH = 256>
+__global__ __launch_bounds__(TH) void k_xxh64_quad(const uint8_t* __restrict__ base, uint64_t stride,
                                                       const uint32_t* __restrict__ lens, uint32_t len,
                                                       const uint64_t* __restrict__ offs, uint64_t n,
                                                       uint64_t* __restrict__ out,
                                                       const uint64_t* __restrict__ expected,
                                                       unsigned long long* __restrict__ first_bad,
                                                       unsigned long long* __restrict__ n_bad) {
-    const uint64_t gtid = static_cast<uint64_t>(blockIdx.x) * 256 + threadIdx.x;
+    const uint64_t gtid = static_cast<uint64_t>(blockIdx.x) * TH + threadIdx.x;
     const uint64_t blk_raw = gtid >> 2;
     const uint32_t j = threadIdx.x & 3;
     const bool live = blk_raw < n;
@@ -207,7 +256,10 @@ __global__ __launch_bounds__(256) void k_xxh64_quad(const uint8_t* __restrict__ 
     uint64_t acc = acc_seed(j);
     const bool aligned = (reinterpret_cast<uintptr_t>(src) & 7) == 0;
     if (aligned) {
-        acc = quad_stripes_aligned<U, NT>(reinterpret_cast<const uint64_t*>(src) + j, nst, acc);
+        if constexpr (D >= 2)
+            acc = quad_stripes_deep<U, D>(reinterpret_cast<const uint64_t*>(src) + j, nst, acc);
+        else
+            acc = quad_stripes_aligned<U, NT>(reinterpret_cast<const uint64_t*>(src) + j, nst, acc);
     } else {
         acc = quad_stripes_unaligned(src + 8 * j, nst, acc);
     }
@@ -1187,14 +1239,19 @@ __global__ __launch_bounds__(1024) void k_order_scan_buckets(uint32_t* __restric
 
 __global__ __launch_bounds__(256) void k_order_place(const uint64_t* __restrict__ offs, uint64_t n,
                                                      const uint32_t* __restrict__ counts,
-                                                     const uint32_t* __restrict__ bounds, uint32_t* __restrict__ order) {
+                                                     const uint32_t* __restrict__ bounds, uint32_t* __restrict__ order,
+                                                     uint64_t* __restrict__ s_offs) {
     __shared__ uint32_t pos[kOrderBuckets];
     for (uint32_t i = threadIdx.x; i < kOrderBuckets; i += 256) pos[i] = bounds[i] + counts[i * kOrderParts + blockIdx.x];
     __syncthreads();
     uint64_t lo, hi;
     order_part(n, blockIdx.x, &lo, &hi);
-    for (uint64_t i = lo + threadIdx.x; i < hi; i += 256)
-        order[atomicAdd(&pos[order_bucket(offs[i])], 1u)] = static_cast<uint32_t>(i);
+    for (uint64_t i = lo + threadIdx.x; i < hi; i += 256) {
+        const uint64_t o = offs[i];
+        const uint32_t at = atomicAdd(&pos[order_bucket(o)], 1u);
+        order[at] = static_cast<uint32_t>(i);
+        s_offs[at] = o;  // with the index: k_order_sort reads both in bucket order
+    }
 }
 
 constexpr uint32_t kOrderSortMax = 2048;
@@ -1203,25 +1260,23 @@ constexpr uint32_t kOrderSortMax = 2048;
 // buckets stay in placement order)
 // Sort key: [offset inside the 32 MiB region] [the entry's index in the bucket], one
 // 64-bit compare-exchange per pair (bitonic, one pair per thread per pass); the index
-// finds the block's number and offset, kept in LDS. The bucket's offsets and lengths are
-// written in the new order too (s_offs, s_lens), so the hash kernel reads them
-// sequentially; only the checksum store goes through order. Grouping a region's blocks by
+// finds the block's number and offset, kept in LDS. The bucket's offsets (placed beside
+// the indices by k_order_place) and lengths are written in the new order too (s_offs,
+// s_lens), so the hash kernel reads them sequentially; only the checksum store goes
+// through order. Grouping a region's blocks by
 // tile count first (fewer masked rows in a wave) measured worse: 0.78 against 0.85 of
 // 8 TB/s on the shuffled storm-length gather (profiles/r03k/), address order wins.
-__global__ __launch_bounds__(256) void k_order_sort(const uint64_t* __restrict__ offs, const uint32_t* __restrict__ lens,
-                                                    const uint32_t* __restrict__ bounds, uint32_t* __restrict__ order,
-                                                    uint64_t* __restrict__ s_offs, uint32_t* __restrict__ s_lens) {
+__global__ __launch_bounds__(256) void k_order_sort(const uint32_t* __restrict__ lens, const uint32_t* __restrict__ bounds,
+                                                    uint32_t* __restrict__ order, uint64_t* __restrict__ s_offs,
+                                                    uint32_t* __restrict__ s_lens) {
     static_assert(kOrderSortMax <= 2048 && kOrderShift + 11 <= 64, "key fields");
     __shared__ uint64_t key[kOrderSortMax];
     __shared__ uint64_t off[kOrderSortMax];
     __shared__ uint32_t val[kOrderSortMax];
     const uint32_t lo = bounds[blockIdx.x], cnt = bounds[kOrderBuckets + blockIdx.x] - lo;
     if (cnt > kOrderSortMax) {  // left in placement order
-        for (uint32_t i = threadIdx.x; i < cnt; i += 256) {
-            const uint32_t v = order[lo + i];
-            s_offs[lo + i] = offs[v];
-            if (lens) s_lens[lo + i] = lens[v];
-        }
+        if (lens)
+            for (uint32_t i = threadIdx.x; i < cnt; i += 256) s_lens[lo + i] = lens[order[lo + i]];
         return;
     }
     uint32_t m = 2;
@@ -1231,14 +1286,14 @@ __global__ __launch_bounds__(256) void k_order_sort(const uint64_t* __restrict__
         uint64_t k = ~uint64_t{0};
         if (i < cnt) {
             const uint32_t v = order[lo + i];
-            const uint64_t o = offs[v];
+            const uint64_t o = s_offs[lo + i];
             val[i] = v;
             off[i] = o;
             k = ((o & kRegion) << 11) | i;
         }
         key[i] = k;
     }
-    __syncthreads();
+    __syncthreads();  // (every thread's reads of s_offs and order are done before the writes below)
     for (uint32_t k = 2; k <= m; k <<= 1) {
         for (uint32_t j = k >> 1; j > 0; j >>= 1) {
             for (uint32_t t = threadIdx.x; t < m / 2; t += 256) {

@@ -123,6 +123,7 @@ int fail(int code, const std::string& msg) {
 // lane per pipelined group (design probe, profiles/r01_probe.txt: U=16 with plain
 // loads is the fastest quad variant; non-temporal loads cost 35%).
 constexpr int kU = 16;
+constexpr int kQuadSpreadDepth = 4;  // groups of kU loads in flight, one-wave quad workgroups
 // LDS-staged fast path: 8-wave (512-thread) workgroups of 128 blocks, tiles of 16
 // stripes (512 B per block, 64 KiB per tile), a ring of 2 tiles (128 KiB LDS, one
 // workgroup per CU), non-temporal LDS-DMA (aux = 2). Measured best of the swept
@@ -456,8 +457,8 @@ int launch_checksum(const uint8_t* base, uint64_t stride, const uint32_t* lens, 
             hipLaunchKernelGGL(k_order_count, dim3(kOrderParts), dim3(256), 0, st, offs, n, counts);
             hipLaunchKernelGGL(k_order_scan_rows, dim3(kOrderBuckets / 4), dim3(256), 0, st, counts, bounds);
             hipLaunchKernelGGL(k_order_scan_buckets, dim3(1), dim3(1024), 0, st, bounds);
-            hipLaunchKernelGGL(k_order_place, dim3(kOrderParts), dim3(256), 0, st, offs, n, counts, bounds, order);
-            hipLaunchKernelGGL(k_order_sort, dim3(kOrderBuckets), dim3(256), 0, st, offs, lens, bounds, order, s_offs, s_lens);
+            hipLaunchKernelGGL(k_order_place, dim3(kOrderParts), dim3(256), 0, st, offs, n, counts, bounds, order, s_offs);
+            hipLaunchKernelGGL(k_order_sort, dim3(kOrderBuckets), dim3(256), 0, st, lens, bounds, order, s_offs, s_lens);
             lens = s_lens;
             offs = s_offs;
             if (persistent) {
@@ -547,9 +548,40 @@ int launch_checksum(const uint8_t* base, uint64_t stride, const uint32_t* lens, 
         HIP_TRY(hipGetLastError());
         return STORMCK_OK;
     }
+    // General path (per-block lengths / explicit offsets / any alignment): register quad
+    // kernel. A batch of at most one wave per CU (16 blocks a wave) runs in one-wave
+    // workgroups, so every wave has a CU of its own, with four groups of loads in flight:
+    // the quad kernel's 16 scattered 32-byte pieces per load instruction make a CU's
+    // address path the limit, 2 waves on a CU cost as much as 4 (profiles/r03_quad/:
+    // 2,049 / 3,072 / 4,096 blocks of 31,808 B in 25.2 / 27.9 / 31.8 us against 34.6 /
+    // 35.0 / 35.1 in 256-thread workgroups). Probe knob STORMCK_QUAD_SPREAD=0 disables.
+    static const bool spread_on = [] {
+        const char* e = std::getenv("STORMCK_QUAD_SPREAD");
+        return !(e && e[0] == '0');
+    }();
+    const uint64_t ncu_q = cu_count();
+    if (spread_on && ncu_q > 0 && n <= 16 * ncu_q) {
+        const dim3 g(static_cast<unsigned>((n + 15) / 16));
+#define STORMCK_SPREAD(LENS, OFFS, VER)                                                                               \
+    hipLaunchKernelGGL((k_xxh64_quad<kU, LENS, OFFS, VER, false, kQuadSpreadDepth, 64>), g, dim3(64), 0, st, base, stride, \
+                       lens, len, offs, n, out, expected, first_bad, n_bad)
+        if (!verify) {
+            if (lens && offs) STORMCK_SPREAD(true, true, false);
+            else if (lens) STORMCK_SPREAD(true, false, false);
+            else if (offs) STORMCK_SPREAD(false, true, false);
+            else STORMCK_SPREAD(false, false, false);
+        } else {
+            if (lens && offs) STORMCK_SPREAD(true, true, true);
+            else if (lens) STORMCK_SPREAD(true, false, true);
+            else if (offs) STORMCK_SPREAD(false, true, true);
+            else STORMCK_SPREAD(false, false, true);
+        }
+#undef STORMCK_SPREAD
+        HIP_TRY(hipGetLastError());
+        return STORMCK_OK;
+    }
     dim3 grid;
     if (!grid_for(n * 4, &grid)) return fail(STORMCK_EINVAL, "batch too large for one launch");
-    // General path (per-block lengths / explicit offsets / any alignment): register quad kernel.
 #define STORMCK_LAUNCH(LENS, OFFS, VER)                                                                         \
     hipLaunchKernelGGL((k_xxh64_quad<kU, LENS, OFFS, VER>), grid, dim3(kThreads), 0, st, base, stride, lens, len, \
                        offs, n, out, expected, first_bad, n_bad)
