@@ -1832,11 +1832,11 @@ template <uint32_t F, uint32_t TS_, int D, int C, bool FULL>
 __device__ __forceinline__ void pointer_level_pc_body(const uint64_t* __restrict__ cs, uint64_t m, uint64_t pm,
                                                       uint64_t node0, uint64_t addr_base, uint64_t rev, uint8_t type,
                                                       uint64_t* __restrict__ parent_cs,
-                                                      uint64_t (*ring)[16 * C][RingShape<TS_>::RS]) {
+                                                      uint64_t (*ring)[16 * C][RingShape<TS_>::RS], uint32_t wave) {
     using P = RingProducer<F, TS_, FULL>;
     constexpr uint32_t TS = P::TS, NT = P::NT, IT = P::IT;
     static_assert(NT % D == 0 && D % 2 == 0, "tile shape / static ring slots");
-    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t lane = threadIdx.x & 63;
     if (wave >= C) {  // producer wave for chain wave (wave - C)
         const uint32_t pair = wave - C;
         const P prod(cs, m, pm, node0 + 16 * pair, addr_base, rev, lane);
@@ -1876,17 +1876,49 @@ __device__ __forceinline__ void pointer_level_pc_body(const uint64_t* __restrict
     }
 }
 
-template <uint32_t F, uint32_t TS, int D, int C>
+// Role of a wave in a workgroup of 2C waves: chain waves must not share a SIMD with each
+// other, since a chain is bounded by its wave's VALU issue ("Merkle tree
+// per step"). With SIMD roles, every wave reads the SIMD it was placed on (HW_ID bits
+// 5:4) and takes a rank among the workgroup's waves on that SIMD; the waves are then
+// ordered by (rank, SIMD) and the first C of that order are the chain waves. So the
+// chains land on C distinct SIMDs whenever the dispatcher spreads the workgroup's
+// waves over at least C of them, whatever order it placed them in. Without SIMD roles
+// the role is the wave index (chain waves first).
+template <bool SIMDROLE>
+__device__ __forceinline__ uint32_t pc_role(uint32_t* simd_cnt) {
+    const uint32_t wave = threadIdx.x >> 6;
+    if (!SIMDROLE) return wave;
+    if (threadIdx.x < 4) simd_cnt[threadIdx.x] = 0;
+    __syncthreads();
+    uint32_t hwid;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hwid));
+    const uint32_t simd = (hwid >> 4) & 3;
+    uint32_t rank = 0;
+    if ((threadIdx.x & 63) == 0) rank = atomicAdd(&simd_cnt[simd], 1u);
+    rank = __builtin_amdgcn_readfirstlane(rank);
+    __syncthreads();
+    uint32_t pos = 0;
+#pragma unroll
+    for (uint32_t s = 0; s < 4; ++s) {
+        const uint32_t c = simd_cnt[s];
+        pos += (c < rank ? c : rank) + ((s < simd && c > rank) ? 1u : 0u);
+    }
+    return pos;
+}
+
+template <uint32_t F, uint32_t TS, int D, int C, bool SIMDROLE = false>
 __global__ __launch_bounds__(128 * C) void k_pointer_level_pc(const uint64_t* __restrict__ cs, uint64_t m,
                                                               uint64_t addr_base, uint64_t rev, uint8_t type,
                                                               uint64_t* __restrict__ parent_cs) {
     __shared__ uint64_t ring[2][16 * C][RingShape<TS>::RS];  // two tiles per chain wave
+    __shared__ uint32_t simd_cnt[4];
+    const uint32_t role = pc_role<SIMDROLE>(simd_cnt);
     const uint64_t pm = (m + F - 1) / F;
     const uint64_t node0 = static_cast<uint64_t>(blockIdx.x) * 16 * C;
     if (node0 + 16 * C <= m / F)  // workgroup-uniform
-        pointer_level_pc_body<F, TS, D, C, true>(cs, m, pm, node0, addr_base, rev, type, parent_cs, ring);
+        pointer_level_pc_body<F, TS, D, C, true>(cs, m, pm, node0, addr_base, rev, type, parent_cs, ring, role);
     else
-        pointer_level_pc_body<F, TS, D, C, false>(cs, m, pm, node0, addr_base, rev, type, parent_cs, ring);
+        pointer_level_pc_body<F, TS, D, C, false>(cs, m, pm, node0, addr_base, rev, type, parent_cs, ring, role);
 }
 
 // Small levels (a handful of nodes, e.g. the top of a shard tree): one workgroup per

@@ -461,25 +461,17 @@ int launch_checksum(const uint8_t* base, uint64_t stride, const uint32_t* lens, 
             hipLaunchKernelGGL(k_order_sort, dim3(kOrderBuckets), dim3(256), 0, st, lens, bounds, order, s_offs, s_lens);
             lens = s_lens;
             offs = s_offs;
+#define STORMCK_ORD(SK, LN)                                                                                      \
+    hipLaunchKernelGGL((k_xxh64_glds_var<kTileStripes, kAuxNT, false, kGldsWaves, SK, LN, true, true>), grid,       \
+                       dim3(kGldsThreads), 0, st, base, stride, lens, len, offs, n, out, expected, first_bad, n_bad, order)
             if (persistent) {
-                if (lens)
-                    hipLaunchKernelGGL((k_xxh64_glds_var<kTileStripes, kAuxNT, false, kGldsWaves, kSkewTiles, true, true, true>),
-                                       grid, dim3(kGldsThreads), 0, st, base, stride, lens, len, offs, n, out, expected,
-                                       first_bad, n_bad, order);
-                else
-                    hipLaunchKernelGGL((k_xxh64_glds_var<kTileStripes, kAuxNT, false, kGldsWaves, kSkewTiles, false, true, true>),
-                                       grid, dim3(kGldsThreads), 0, st, base, stride, lens, len, offs, n, out, expected,
-                                       first_bad, n_bad, order);
+                if (lens) STORMCK_ORD(kSkewTiles, true);
+                else STORMCK_ORD(kSkewTiles, false);
             } else {
-                if (lens)
-                    hipLaunchKernelGGL((k_xxh64_glds_var<kTileStripes, kAuxNT, false, kGldsWaves, 0, true, true, true>),
-                                       grid, dim3(kGldsThreads), 0, st, base, stride, lens, len, offs, n, out, expected,
-                                       first_bad, n_bad, order);
-                else
-                    hipLaunchKernelGGL((k_xxh64_glds_var<kTileStripes, kAuxNT, false, kGldsWaves, 0, false, true, true>),
-                                       grid, dim3(kGldsThreads), 0, st, base, stride, lens, len, offs, n, out, expected,
-                                       first_bad, n_bad, order);
+                if (lens) STORMCK_ORD(0, true);
+                else STORMCK_ORD(0, false);
             }
+#undef STORMCK_ORD
             HIP_TRY(hipGetLastError());
             HIP_TRY(hipFreeAsync(ws, st));
             return STORMCK_OK;
@@ -554,13 +546,17 @@ int launch_checksum(const uint8_t* base, uint64_t stride, const uint32_t* lens, 
     // the quad kernel's 16 scattered 32-byte pieces per load instruction make a CU's
     // address path the limit, 2 waves on a CU cost as much as 4 (profiles/r03_quad/:
     // 2,049 / 3,072 / 4,096 blocks of 31,808 B in 25.2 / 27.9 / 31.8 us against 34.6 /
-    // 35.0 / 35.1 in 256-thread workgroups). Probe knob STORMCK_QUAD_SPREAD=0 disables.
-    static const bool spread_on = [] {
+    // 35.0 / 35.1 in 256-thread workgroups). Past one wave per CU it loses (6,144 /
+    // 8,192 blocks: 38.5 / 48.8 us against 35.8 / 39.7 in 256-thread workgroups,
+    // profiles/r03_mid/spread_*.txt), and so does a one-wave LDS-DMA ring of 4-9 tile
+    // slots (38-60 us over 2,064-8,192 blocks, profiles/r03_mid/probe_*). Probe knob
+    // STORMCK_QUAD_SPREAD = waves per CU it covers (0 disables).
+    static const uint64_t spread_mult = [] {  // batches of up to spread_mult waves per CU
         const char* e = std::getenv("STORMCK_QUAD_SPREAD");
-        return !(e && e[0] == '0');
+        return e ? static_cast<uint64_t>(std::atoi(e)) : uint64_t{1};
     }();
     const uint64_t ncu_q = cu_count();
-    if (spread_on && ncu_q > 0 && n <= 16 * ncu_q) {
+    if (ncu_q > 0 && n <= 16 * spread_mult * ncu_q) {
         const dim3 g(static_cast<unsigned>((n + 15) / 16));
 #define STORMCK_SPREAD(LENS, OFFS, VER)                                                                               \
     hipLaunchKernelGGL((k_xxh64_quad<kU, LENS, OFFS, VER, false, kQuadSpreadDepth, 64>), g, dim3(64), 0, st, base, stride, \
@@ -1227,13 +1223,36 @@ int stormck_pointer_level_device(const uint64_t* d_child_cs, uint64_t m, uint64_
     }();
     if (ring_mode != 0 && fanout == STORMCK_POINTERS_PER_BLOCK) {
         // storm's fan-out: 16 nodes per workgroup, premultiplied words staged in LDS
+        // C chain waves per workgroup (and C producers). C = 1: the dispatcher already
+        // puts the chain waves of 2-wave workgroups on distinct SIMDs at every level size
+        // (tools/hwid_probe.hip), and one workgroup per CU with C = 2 / 4 (chains on
+        // distinct SIMDs by pc_role) measured slower: 35.2 / 41.0 us against 31.7 / 37.9
+        // for the 6,991- / 13,982-node levels (profiles/r03_merkle_simd/). Probe knobs:
+        // STORMCK_POINTER_C = 2 / 4 (or 0: the fewest C that keeps one workgroup per CU),
+        // STORMCK_POINTER_SIMD=0 takes roles by wave index.
         constexpr uint32_t F = STORMCK_POINTERS_PER_BLOCK;
-        const uint64_t groups = (pm + 15) / 16;
+        static const int fixed_c = [] {
+            const char* e = std::getenv("STORMCK_POINTER_C");
+            return e ? std::atoi(e) : 1;
+        }();
+        static const bool simd_roles = [] {
+            const char* e = std::getenv("STORMCK_POINTER_SIMD");
+            return !(e && e[0] == '0');
+        }();
+        const uint64_t chains = (pm + 15) / 16, ncu = cu_count() ? cu_count() : 256;
+        const int c = fixed_c == 1 || fixed_c == 2 || fixed_c == 4 ? fixed_c
+                      : chains <= ncu ? 1 : chains <= 2 * ncu ? 2 : 4;
+        const uint64_t groups = (chains + c - 1) / c;
         if (groups > 0x7fffffffULL) return fail(STORMCK_EINVAL, "level too large");
         const dim3 grid(static_cast<unsigned>(groups));
         hipStream_t st = static_cast<hipStream_t>(stream);
-        hipLaunchKernelGGL((k_pointer_level_pc<F, kRingTile, kRingPrefetch, 1>), grid, dim3(128), 0, st, d_child_cs,
-                           m, child_addr_base, rev, child_type, d_parent_cs);
+#define STORMCK_PC(C, SR)                                                                                       \
+    hipLaunchKernelGGL((k_pointer_level_pc<F, kRingTile, kRingPrefetch, C, SR>), grid, dim3(128 * C), 0, st, \
+                       d_child_cs, m, child_addr_base, rev, child_type, d_parent_cs)
+        if (c == 1) STORMCK_PC(1, false);  // one chain wave: its producer cannot take its SIMD
+        else if (c == 2) { if (simd_roles) STORMCK_PC(2, true); else STORMCK_PC(2, false); }
+        else { if (simd_roles) STORMCK_PC(4, true); else STORMCK_PC(4, false); }
+#undef STORMCK_PC
         HIP_TRY(hipGetLastError());
         return STORMCK_OK;
     }

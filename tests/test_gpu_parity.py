@@ -588,6 +588,50 @@ def test_pointer_level_ring_kernel(dev, m):
         assert int(got[jn]) == o.xxh64(o.pack_pointer_block_py(ent, fanout)), jn
 
 
+@pytest.mark.parametrize("knobs", [{"STORMCK_POINTER_RING": "1"}, {"STORMCK_POINTER_C": "2"},
+                                   {"STORMCK_POINTER_C": "4"}, {"STORMCK_POINTER_C": "4", "STORMCK_POINTER_SIMD": "0"},
+                                   {"STORMCK_POINTER_C": "0"}])
+def test_pointer_level_probe_kernels(dev, knobs):
+    """The Merkle level kernels behind probe knobs (read once per process, so each runs
+    in a child): the 1-wave ring (STORMCK_POINTER_RING=1), 2 and 4 chain waves per
+    workgroup with SIMD-ranked roles (pc_role<true>) or by wave index, and the C chosen
+    per level (0). Ragged 13,982-, 6,991- and 300-node levels (the c3 and c4 shard
+    levels); every node equal to the default kernel's in this process."""
+    import subprocess
+    import sys
+    from oracle import oracle as o
+    from storm_amd import engine
+    from tests.conftest import ROOT
+    fanout, base, rev = 1200, (1 << 40) + 5, (1 << 33) + 1
+    sizes = [16 << 20, 8 << 20, 300 * 1200 + 1]
+    want = []
+    for m in sizes:
+        leaf = o.synth_leaf_checksums(m, 0x77 + m)
+        d_leaf = _to_dev(leaf.view(np.int64), dev)
+        par = torch.empty((m + fanout - 1) // fanout, dtype=torch.int64, device=dev)
+        engine.pointer_level_device(d_leaf.data_ptr(), m, base, rev, 2, fanout, par.data_ptr())
+        torch.cuda.synchronize()
+        want.append(_u64(par))
+    code = ("import sys, numpy as np, torch\n"
+            "from oracle import oracle as o\n"
+            "from storm_amd import engine\n"
+            f"for m in {sizes}:\n"
+            f"    leaf = o.synth_leaf_checksums(m, 0x77 + m)\n"
+            "    d = torch.from_numpy(leaf.view(np.int64)).to('cuda:0')\n"
+            "    par = torch.empty((m + 1199) // 1200, dtype=torch.int64, device='cuda:0')\n"
+            f"    engine.pointer_level_device(d.data_ptr(), m, {base}, {rev}, 2, 1200, par.data_ptr())\n"
+            "    torch.cuda.synchronize()\n"
+            "    np.save(sys.stdout.buffer, par.cpu().numpy().view(np.uint64))\n")
+    env = dict(os.environ, **knobs)
+    r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, capture_output=True, env=env, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    import io
+    buf = io.BytesIO(r.stdout)
+    for m, w in zip(sizes, want):
+        got = np.load(buf)
+        assert np.array_equal(got, w), (knobs, m, int((got != w).sum()))
+
+
 def test_combine_roots_device(dev):
     from storm_amd import engine
     g = load_golden("merkle.json")["combine"]
