@@ -500,6 +500,48 @@ int launch_checksum(const uint8_t* base, uint64_t stride, const uint32_t* lens, 
         HIP_TRY(hipGetLastError());
         return STORMCK_OK;
     }
+    // Uniform batches from about 39 blocks per CU up to kBigBatch: the LDS-DMA kernel in
+    // W-wave workgroups (16*W blocks each), W in {1, 3} chosen to minimise the blocks of
+    // the busiest CU, ceil(workgroups / CUs) * 16W (ties: 3). us per launch of 31,808 B
+    // blocks, against the 256-thread quad / 2-wave LDS-DMA kernels before (rocprof-free
+    // HIP events, profiles/r03_mid/w*): 10,000 54.2 (60.9), 10,240 54.6 (60.1), 12,288
+    // 60.3 (65.6), 16,384 77.7 (81.8), 20,000 101.7 (112.2), 24,575 122.1 (126.3). Below
+    // it the quad kernels win (8,192: 39.8 against 51-55). Probe knob STORMCK_MID_WAVES =
+    // 1-4 forces W for every batch above one wave per CU; 5 = the kernels before.
+    static const int mid_knob = [] {
+        const char* e = std::getenv("STORMCK_MID_WAVES");
+        return e ? std::atoi(e) : 0;
+    }();
+    int mid_waves = 0;
+    const uint64_t ncu_m = cu_count();
+    if (ncu_m > 0 && n < kBigBatch) {
+        if (mid_knob >= 1 && mid_knob <= 4) {
+            if (n > 16 * ncu_m) mid_waves = mid_knob;
+        } else if (mid_knob == 0 && n >= 39 * ncu_m) {
+            auto busiest = [&](uint64_t w) { return (((n + 16 * w - 1) / (16 * w)) + ncu_m - 1) / ncu_m * 16 * w; };
+            mid_waves = busiest(1) < busiest(3) ? 1 : 3;
+        }
+    }
+    if (mid_waves > 0 && !lens && !offs && (reinterpret_cast<uintptr_t>(base) & 15) == 0 && (stride & 15) == 0 &&
+        len >= 32u * kTileStripes) {
+        const dim3 g(static_cast<unsigned>((n + 16 * mid_waves - 1) / (16 * mid_waves)));
+#define STORMCK_MIDW(W, VER)                                                                                      \
+    hipLaunchKernelGGL((k_xxh64_glds<kTileStripes, kRing, kAuxNT, true, VER, W, false>), g, dim3(64 * W), 0, st, base, \
+                       stride, len, n, out, expected, first_bad, n_bad)
+        switch (mid_waves * 2 + (verify ? 1 : 0)) {
+            case 2: STORMCK_MIDW(1, false); break;
+            case 3: STORMCK_MIDW(1, true); break;
+            case 4: STORMCK_MIDW(2, false); break;
+            case 5: STORMCK_MIDW(2, true); break;
+            case 6: STORMCK_MIDW(3, false); break;
+            case 7: STORMCK_MIDW(3, true); break;
+            case 8: STORMCK_MIDW(4, false); break;
+            default: STORMCK_MIDW(4, true); break;
+        }
+#undef STORMCK_MIDW
+        HIP_TRY(hipGetLastError());
+        return STORMCK_OK;
+    }
     if (n >= kMidBatch && !lens && !offs && (reinterpret_cast<uintptr_t>(base) & 15) == 0 && (stride & 15) == 0 &&
         len >= 32u * kTileStripes) {
         if (n < kBigBatch) {
