@@ -433,7 +433,16 @@ int launch_checksum(const uint8_t* base, uint64_t stride, const uint32_t* lens, 
     if (var_on && n >= kMidBatch && (lens || offs) &&
         (offs || ((reinterpret_cast<uintptr_t>(base) & 15) == 0 && (stride & 15) == 0))) {
         const bool big = n >= kBigBatch;
-        const uint64_t per_wg = big ? kGldsBlocks : 16 * kMidWaves;
+        // below kBigBatch: 3- or 1-wave workgroups, whichever loads the busiest CU least
+        // (as the uniform path above)
+        const uint64_t ncu_v = cu_count() ? cu_count() : 256;
+        auto busiest = [&](uint64_t w) { return (((n + 16 * w - 1) / (16 * w)) + ncu_v - 1) / ncu_v * 16 * w; };
+        static const bool var_before = [] {  // probe knob STORMCK_MID_WAVES=5: 2-wave workgroups (A/B)
+            const char* e = std::getenv("STORMCK_MID_WAVES");
+            return e && e[0] == '5';
+        }();
+        const int vw = var_before ? 2 : busiest(1) < busiest(3) ? 1 : 3;
+        const uint64_t per_wg = big ? kGldsBlocks : 16 * static_cast<uint64_t>(vw);
         const uint64_t wgs = (n + per_wg - 1) / per_wg;
         if (wgs > 0x7fffffffULL) return fail(STORMCK_EINVAL, "batch too large for one launch");
         const uint64_t cus = cu_count();
@@ -481,9 +490,15 @@ int launch_checksum(const uint8_t* base, uint64_t stride, const uint32_t* lens, 
                        stride, lens, len, offs, n, out, expected, first_bad, n_bad, nullptr)
 #define STORMCK_VAR_SHAPE(LN, OF)                                                                                \
     do {                                                                                                         \
-        if (!big) {                                                                                              \
-            if (verify) STORMCK_VAR(true, kMidWaves, 0, LN, OF);                                                 \
-            else STORMCK_VAR(false, kMidWaves, 0, LN, OF);                                                       \
+        if (!big && vw == 1) {                                                                                   \
+            if (verify) STORMCK_VAR(true, 1, 0, LN, OF);                                                         \
+            else STORMCK_VAR(false, 1, 0, LN, OF);                                                               \
+        } else if (!big && vw == 2) {                                                                            \
+            if (verify) STORMCK_VAR(true, 2, 0, LN, OF);                                                         \
+            else STORMCK_VAR(false, 2, 0, LN, OF);                                                               \
+        } else if (!big) {                                                                                       \
+            if (verify) STORMCK_VAR(true, 3, 0, LN, OF);                                                         \
+            else STORMCK_VAR(false, 3, 0, LN, OF);                                                               \
         } else if (persistent) {                                                                                 \
             if (verify) STORMCK_VAR(true, kGldsWaves, kSkewTiles, LN, OF);                                       \
             else STORMCK_VAR(false, kGldsWaves, kSkewTiles, LN, OF);                                             \
