@@ -1775,8 +1775,22 @@ int stormck_commit_device(void* d_arena, stormck_dirty_block* blocks, uint64_t n
         return !(e && e[0] == '0');
     }();
     const uint64_t ncu = cu_count();
+    static const bool commit_midw = [] {  // probe knob STORMCK_COMMIT_MIDW=0: the launches before (A/B)
+        const char* e = std::getenv("STORMCK_COMMIT_MIDW");
+        return !(e && e[0] == '0');
+    }();
     auto launch_level = [&](uint64_t lo, uint64_t cnt) -> int {
-        if (aligned16 && cnt >= kStreamBatch) {
+        if (commit_midw && aligned16 && ncu > 0 && cnt >= 39 * ncu && cnt < kBigBatch) {
+            // mid-size levels: the LDS-DMA ring in 3- or 1-wave workgroups, whichever puts
+            // fewer blocks on the busiest CU (as launch_checksum's uniform path)
+            auto busiest = [&](uint64_t w) { return (((cnt + 16 * w - 1) / (16 * w)) + ncu - 1) / ncu * 16 * w; };
+            if (busiest(1) < busiest(3))
+                hipLaunchKernelGGL((k_commit_level_glds<kTileStripes, kAuxNT, 1>), dim3(static_cast<unsigned>((cnt + 15) / 16)),
+                                   dim3(64), 0, st, static_cast<uint8_t*>(d_arena), d_blocks, lo, cnt, d_cs);
+            else
+                hipLaunchKernelGGL((k_commit_level_glds<kTileStripes, kAuxNT, 3>), dim3(static_cast<unsigned>((cnt + 47) / 48)),
+                                   dim3(192), 0, st, static_cast<uint8_t*>(d_arena), d_blocks, lo, cnt, d_cs);
+        } else if (aligned16 && cnt >= kStreamBatch) {
             // LDS-DMA ring, 8 waves x 128 blocks per workgroup (as the uniform fast path)
             const uint64_t wgs = (cnt + kGldsBlocks - 1) / kGldsBlocks;
             if (wgs > 0x7fffffffULL) return fail(STORMCK_EINVAL, "level too large");

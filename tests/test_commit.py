@@ -141,12 +141,14 @@ def test_device_commit_random_forests(dev, n, fanout, slot, how):
 
 
 @pytest.mark.gpu
-def test_device_commit_streaming_level_mixed_lengths(dev):
-    """A level of >= 16384 blocks takes the LDS-DMA commit kernel: 20000 leaves of mixed
-    storm lengths (workgroups whose blocks run out of stripes at different tiles), a
-    third relocating, shuffled dirty list; vs the oracle's serial commit."""
-    rng = np.random.default_rng(20000)
-    n, slot = 20000, 32768
+@pytest.mark.parametrize("n", [12000, 20000])
+def test_device_commit_streaming_level_mixed_lengths(dev, n):
+    """Levels from 39 blocks per CU take the LDS-DMA commit kernel (on 256 CUs: 12,000
+    leaves in 3-wave workgroups, 20,000 in 1-wave ones): leaves of mixed storm lengths
+    (workgroups whose blocks run out of stripes at different tiles), a third relocating,
+    shuffled dirty list; vs the oracle's serial commit."""
+    rng = np.random.default_rng(n)
+    slot = 32768
     lens = rng.choice([72, 28808, 30000, 31808, 32768, 4097, 512], size=n)
     b, size, last = sc.pointer_forest(n, lens, 1200, slot=slot, revision=4, first_address=7)
     b["birth_revision"][::3] = 2
