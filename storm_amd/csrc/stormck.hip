@@ -149,6 +149,7 @@ constexpr uint64_t kCommitOnePiece = 4096; // f1 commits with at most this many 
 // (profiles/r01_chain/mid_sweep.txt: 16,384 blocks in 84 us instead of 110; 12,288 in 67
 // instead of the register quad's 76).
 constexpr uint64_t kMidBatch = 10240;
+constexpr uint64_t kBigW = 131072;  // uniform batches below this many blocks choose their workgroup size
 constexpr uint64_t kBigBatch = 24576;
 constexpr int kMidWaves = 2;
 constexpr unsigned kThreads = 256;
@@ -333,6 +334,14 @@ bool grid_for(uint64_t threads, dim3* grid) {
     if (blocks == 0 || blocks > 0x7fffffffULL) return false;
     *grid = dim3(static_cast<unsigned>(blocks));
     return true;
+}
+
+bool big_w_on() {  // probe knob STORMCK_BIG_W=0: batches from kBigBatch on always take 8-wave workgroups
+    static const bool on = [] {
+        const char* e = std::getenv("STORMCK_BIG_W");
+        return !(e && e[0] == '0');
+    }();
+    return on;
 }
 
 int launch_checksum(const uint8_t* base, uint64_t stride, const uint32_t* lens, uint32_t len, const uint64_t* offs,
@@ -527,15 +536,23 @@ int launch_checksum(const uint8_t* base, uint64_t stride, const uint32_t* lens, 
         const char* e = std::getenv("STORMCK_MID_WAVES");
         return e ? std::atoi(e) : 0;
     }();
+    // From kBigBatch up to kBigW blocks: 3-wave workgroups instead of the big path's
+    // 8-wave ones when that puts at most 3/4 of the blocks on the busiest CU (a batch a
+    // little above a multiple of 128 blocks per CU would leave most CUs with one 8-wave
+    // workgroup and some with two). 36,864 / 40,000 blocks: 179.8 / ~222 us against
+    // 237.3 / 240.7; 1-wave workgroups lost there (24,641: 132 against 119.6 us; 57,344:
+    // 291 against 264), profiles/r03_mid/bigw*.
     int mid_waves = 0;
     const uint64_t ncu_m = cu_count();
+    auto busiest = [&](uint64_t w) { return (((n + 16 * w - 1) / (16 * w)) + ncu_m - 1) / ncu_m * 16 * w; };
     if (ncu_m > 0 && n < kBigBatch) {
         if (mid_knob >= 1 && mid_knob <= 4) {
             if (n > 16 * ncu_m) mid_waves = mid_knob;
         } else if (mid_knob == 0 && n >= 39 * ncu_m) {
-            auto busiest = [&](uint64_t w) { return (((n + 16 * w - 1) / (16 * w)) + ncu_m - 1) / ncu_m * 16 * w; };
             mid_waves = busiest(1) < busiest(3) ? 1 : 3;
         }
+    } else if (ncu_m > 0 && n < kBigW && mid_knob == 0 && big_w_on()) {
+        if (4 * busiest(3) <= 3 * busiest(8)) mid_waves = 3;
     }
     if (mid_waves > 0 && !lens && !offs && (reinterpret_cast<uintptr_t>(base) & 15) == 0 && (stride & 15) == 0 &&
         len >= 32u * kTileStripes) {

@@ -1,0 +1,14 @@
+# Uniform batches of 24K-128K blocks: workgroup size chosen by the busiest-CU rule
+# (default) against 8-wave workgroups always (STORMCK_BIG_W=0); parity first.
+set -o pipefail
+out=gpurun_out/${1:-big_w}
+mkdir -p $out
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "uniform_fast_path or fuzz or large_batch or c2" > $out/tests.log 2>&1; rc=$?
+grep -E "passed|failed|error" $out/tests.log | tail -3; [ $rc -eq 0 ] || exit $rc
+S="24641 32768 36864 40000 45000 49152 57344 65536 98304"
+for i in 1 2; do
+  for k in 1 0; do
+    STORMCK_BIG_W=$k timeout -k 10 120 python tools/small_batch_probe.py $S > $out/bigw${k}_$i.txt 2>&1 || exit 1
+    echo "big_w=$k run $i: $(grep n= $out/bigw${k}_$i.txt | tr '\n' ' ')"
+  done
+done
