@@ -441,16 +441,18 @@ int launch_checksum(const uint8_t* base, uint64_t stride, const uint32_t* lens, 
     }();
     if (var_on && n >= kMidBatch && (lens || offs) &&
         (offs || ((reinterpret_cast<uintptr_t>(base) & 15) == 0 && (stride & 15) == 0))) {
-        const bool big = n >= kBigBatch;
-        // below kBigBatch: 3- or 1-wave workgroups, whichever loads the busiest CU least
-        // (as the uniform path above)
+        // below kBigBatch: 3- or 1-wave workgroups, whichever loads the busiest CU least;
+        // up to kBigW, 3-wave workgroups where they cut the busiest CU's blocks by a
+        // quarter against 8-wave ones (as the uniform path below)
         const uint64_t ncu_v = cu_count() ? cu_count() : 256;
         auto busiest = [&](uint64_t w) { return (((n + 16 * w - 1) / (16 * w)) + ncu_v - 1) / ncu_v * 16 * w; };
+        const bool big3 = n >= kBigBatch && n < kBigW && big_w_on() && 4 * busiest(3) <= 3 * busiest(8);
+        const bool big = n >= kBigBatch && !big3;
         static const bool var_before = [] {  // probe knob STORMCK_MID_WAVES=5: 2-wave workgroups (A/B)
             const char* e = std::getenv("STORMCK_MID_WAVES");
             return e && e[0] == '5';
         }();
-        const int vw = var_before ? 2 : busiest(1) < busiest(3) ? 1 : 3;
+        const int vw = var_before ? 2 : (big3 || busiest(3) <= busiest(1)) ? 3 : 1;
         const uint64_t per_wg = big ? kGldsBlocks : 16 * static_cast<uint64_t>(vw);
         const uint64_t wgs = (n + per_wg - 1) / per_wg;
         if (wgs > 0x7fffffffULL) return fail(STORMCK_EINVAL, "batch too large for one launch");
