@@ -1799,11 +1799,13 @@ int stormck_commit_device(void* d_arena, stormck_dirty_block* blocks, uint64_t n
         return !(e && e[0] == '0');
     }();
     auto launch_level = [&](uint64_t lo, uint64_t cnt) -> int {
-        if (commit_midw && aligned16 && ncu > 0 && cnt >= 39 * ncu && cnt < kBigBatch) {
+        auto busiest = [&](uint64_t w) { return (((cnt + 16 * w - 1) / (16 * w)) + ncu - 1) / ncu * 16 * w; };
+        if (commit_midw && aligned16 && ncu > 0 && cnt >= 39 * ncu &&
+            (cnt < kBigBatch || (cnt < kBigW && big_w_on() && 4 * busiest(3) <= 3 * busiest(8)))) {
             // mid-size levels: the LDS-DMA ring in 3- or 1-wave workgroups, whichever puts
-            // fewer blocks on the busiest CU (as launch_checksum's uniform path)
-            auto busiest = [&](uint64_t w) { return (((cnt + 16 * w - 1) / (16 * w)) + ncu - 1) / ncu * 16 * w; };
-            if (busiest(1) < busiest(3))
+            // fewer blocks on the busiest CU; from kBigBatch, 3-wave ones where they cut the
+            // busiest CU's blocks by a quarter (as launch_checksum's uniform path)
+            if (cnt < kBigBatch && busiest(1) < busiest(3))
                 hipLaunchKernelGGL((k_commit_level_glds<kTileStripes, kAuxNT, 1>), dim3(static_cast<unsigned>((cnt + 15) / 16)),
                                    dim3(64), 0, st, static_cast<uint8_t*>(d_arena), d_blocks, lo, cnt, d_cs);
             else

@@ -141,10 +141,11 @@ def test_device_commit_random_forests(dev, n, fanout, slot, how):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n", [12000, 20000])
+@pytest.mark.parametrize("n", [12000, 20000, 36864])
 def test_device_commit_streaming_level_mixed_lengths(dev, n):
     """Levels from 39 blocks per CU take the LDS-DMA commit kernel (on 256 CUs: 12,000
-    leaves in 3-wave workgroups, 20,000 in 1-wave ones): leaves of mixed storm lengths
+    leaves in 3-wave workgroups, 20,000 in 1-wave ones, 36,864 in 3-wave ones again
+    where 8-wave ones would put two workgroups on some CUs): leaves of mixed storm lengths
     (workgroups whose blocks run out of stripes at different tiles), a third relocating,
     shuffled dirty list; vs the oracle's serial commit."""
     rng = np.random.default_rng(n)

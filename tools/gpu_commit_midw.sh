@@ -7,7 +7,7 @@ timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout
 grep -E "passed|failed|error" $out/tests.log | tail -3; [ $rc -eq 0 ] || exit $rc
 for i in 1 2; do
   for k in 1 0; do
-    for n in 12288 20000; do
+    for n in 12288 20000 36864; do
       STORMCK_COMMIT_MIDW=$k timeout -k 10 200 python bench.py --workload commit --commit-leaves $n --steps 20 --warmup 3 > $out/c${k}_${n}_$i.log 2>&1 || exit 1
       python -c "import json; d=json.loads(open('$out/c${k}_${n}_$i.log').read().strip().splitlines()[-1]); print('midw=$k n=$n run $i', d['ms_per_step'], 'ms')"
     done
