@@ -793,6 +793,7 @@ def block_checksum_workload(a) -> int:
                        "total_blocks": n_total, "blocks_per_gpu": n_gpu, "block_bytes": BLOCK,
                        "arena_blocks": arena_n, "passes_per_step": passes,
                        "parallelism": f"dp{world} (contiguous block ranges)",
+                       "library": engine.library_record(),
                        "arena": {"va": "0x%x" % arena_ptr, "va_alignment": va_alignment(arena_ptr),
                                  "bytes": arena_n * BLOCK,
                                  "alloc": "hipMalloc (stormck_device_alloc), the process's first device allocation"

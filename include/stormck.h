@@ -63,6 +63,9 @@ typedef struct stormck_pointer {
 /* ---- library / device ---------------------------------------------------- */
 
 int stormck_abi_version(void);
+/* Provenance of this build: "sha256:<hex>" of the sources it was compiled from
+ * (storm_amd/build.py SOURCES), so a prebuilt library can be matched to a tree. */
+const char* stormck_build_id(void);
 const char* stormck_last_error(void);
 /* Number of visible gfx950 devices (0 on a machine without one). */
 int stormck_device_count(int* count);

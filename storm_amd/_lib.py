@@ -42,6 +42,7 @@ class PointerStruct(ctypes.Structure):
 # name -> (restype, argtypes); mirrors include/stormck.h one to one.
 SIGNATURES = {
     "stormck_abi_version": (c_int, []),
+    "stormck_build_id": (c_char_p, []),
     "stormck_last_error": (c_char_p, []),
     "stormck_device_count": (c_int, [POINTER(c_int)]),
     "stormck_init": (c_int, [c_int]),

@@ -34,15 +34,30 @@ def _newer(target: str, sources) -> bool:
     return all(os.path.getmtime(s) <= t for s in sources)
 
 
+# the sources libstormck.so is compiled from (its build id hashes them)
+SOURCES = [os.path.join(CSRC, f) for f in ("stormck.hip", "kernels.h", "xxh64_dev.h", "xxh64_host.h")] + \
+    [os.path.join(ROOT, "include", "stormck.h")]
+
+
+def sources_sha() -> str:
+    """sha256 over SOURCES (path relative to the repo, then content): the build id a
+    library built from this tree carries (stormck_build_id)."""
+    import hashlib
+    h = hashlib.sha256()
+    for path in SOURCES:
+        h.update(os.path.relpath(path, ROOT).encode() + b"\0")
+        with open(path, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()
+
+
 def build_lib(force: bool = False) -> str:
-    srcs = [os.path.join(CSRC, f) for f in ("stormck.hip", "kernels.h", "xxh64_dev.h")]
-    srcs.append(os.path.join(ROOT, "include", "stormck.h"))
-    if not force and _newer(LIB, srcs):
+    if not force and _newer(LIB, SOURCES):
         return LIB
     os.makedirs(LIB_DIR, exist_ok=True)
     tmp = LIB + ".tmp"
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall",
-           "-o", tmp, os.path.join(CSRC, "stormck.hip")]
+           f'-DSTORMCK_SRC_SHA="{sources_sha()}"', "-o", tmp, os.path.join(CSRC, "stormck.hip")]
     subprocess.run(cmd, check=True)
     os.replace(tmp, LIB)
     return LIB

@@ -1047,6 +1047,11 @@ extern "C" {
 
 int stormck_abi_version(void) { return STORMCK_ABI_VERSION; }
 
+#ifndef STORMCK_SRC_SHA
+#define STORMCK_SRC_SHA "unknown"
+#endif
+const char* stormck_build_id(void) { return "sha256:" STORMCK_SRC_SHA; }
+
 const char* stormck_last_error(void) { return g_last_error.c_str(); }
 
 int stormck_device_count(int* count) {

@@ -6,6 +6,8 @@ and launch on torch's current stream of the tensor's device.
 """
 from __future__ import annotations
 
+import os
+
 from typing import Optional, Tuple
 
 from . import _lib
@@ -64,6 +66,22 @@ def merkle_root_device(d_leaf_cs: int, n: int, leaf_addr_base: int, node_addr_ba
                        d_workspace: int, workspace_bytes: int, d_root: int, d_root_type: int, stream: int = 0) -> None:
     check(lib.stormck_merkle_root_device(d_leaf_cs or None, n, leaf_addr_base, node_addr_base, rev, fanout,
                                          d_workspace or None, workspace_bytes, d_root, d_root_type, stream or None))
+
+
+def build_id() -> str:
+    """The loaded library's provenance, "sha256:<hex>" of the sources it was built from
+    (storm_amd.build.sources_sha of a tree that matches it)."""
+    return lib.stormck_build_id().decode()
+
+
+def library_record() -> dict:
+    """Which libstormck.so this process runs: its path, build id, and whether that id is
+    the hash of the sources in this tree (a prebuilt library that travelled with them)."""
+    from storm_amd import _lib, build
+    bid = build_id()
+    tree = "sha256:" + build.sources_sha()
+    return {"path": os.path.relpath(_lib.LIB_PATH, build.ROOT), "build_id": bid, "tree_sources": tree,
+            "matches_tree": bid == tree}
 
 
 def init(device: int) -> None:

@@ -43,6 +43,16 @@ def test_abi_version():
     assert _lib.lib.stormck_abi_version() == ABI_VERSION == 2
 
 
+def test_library_build_id_is_the_tree_sources_hash():
+    """stormck_build_id() carries the sha256 of the sources the library was compiled
+    from (storm_amd/build.py), so a prebuilt libstormck.so can be matched to its tree:
+    the in-tree build must match the sources next to it."""
+    from storm_amd import engine
+    rec = engine.library_record()
+    assert rec["build_id"].startswith("sha256:") and len(rec["build_id"]) == 7 + 64
+    assert rec["matches_tree"], rec
+
+
 def test_pointer_struct_is_24_bytes():
     from storm_amd.blocks import Pointer
     assert ctypes.sizeof(Pointer) == 24
