@@ -439,7 +439,16 @@ int launch_checksum(const uint8_t* base, uint64_t stride, const uint32_t* lens, 
         const char* e = std::getenv("STORMCK_GLDS_VAR");
         return !(e && e[0] == '0');
     }();
-    if (var_on && n >= kMidBatch && (lens || offs) &&
+    // From 44 blocks per CU (11,264 on 256 CUs): storm-mix batches in us, var kernel /
+    // register quad: 9,216 69.5 / 53.4, 10,240 70.0 / 62.9, 12,288 71.8 / 79.9, 16,384
+    // 82.1 / 124, 49,152 238 / 299 (profiles/r03_mid/varlo*, varhi*). Probe knob
+    // STORMCK_VAR_LO: the smallest batch for the var kernel.
+    static const uint64_t var_lo = [] {
+        const char* e = std::getenv("STORMCK_VAR_LO");
+        return e ? std::strtoull(e, nullptr, 10) : 0;
+    }();
+    if (var_on && n >= (var_lo ? var_lo : std::max<uint64_t>(kMidBatch, 44 * cu_count())) && n > 16 * cu_count() &&
+        (lens || offs) &&
         (offs || ((reinterpret_cast<uintptr_t>(base) & 15) == 0 && (stride & 15) == 0))) {
         // below kBigBatch: 3- or 1-wave workgroups, whichever loads the busiest CU least;
         // up to kBigW, 3-wave workgroups where they cut the busiest CU's blocks by a
