@@ -535,13 +535,14 @@ int launch_checksum(const uint8_t* base, uint64_t stride, const uint32_t* lens, 
         HIP_TRY(hipGetLastError());
         return STORMCK_OK;
     }
-    // Uniform batches from about 39 blocks per CU up to kBigBatch: the LDS-DMA kernel in
+    // Uniform batches from 36 blocks per CU up to kBigBatch: the LDS-DMA kernel in
     // W-wave workgroups (16*W blocks each), W in {1, 3} chosen to minimise the blocks of
     // the busiest CU, ceil(workgroups / CUs) * 16W (ties: 3). us per launch of 31,808 B
     // blocks, against the 256-thread quad / 2-wave LDS-DMA kernels before (rocprof-free
     // HIP events, profiles/r03_mid/w*): 10,000 54.2 (60.9), 10,240 54.6 (60.1), 12,288
     // 60.3 (65.6), 16,384 77.7 (81.8), 20,000 101.7 (112.2), 24,575 122.1 (126.3). Below
-    // it the quad kernels win (8,192: 39.8 against 51-55). Probe knob STORMCK_MID_WAVES =
+    // it the quad kernels win (8,192 / 8,704: 39.9 / 47.9 against 51.6 / 52.2 for 3 waves;
+    // 9,216 / 9,728: 54.0 / 58.7 against 53.0 / 53.8, profiles/r03_mid/unilo*). Probe knob STORMCK_MID_WAVES =
     // 1-4 forces W for every batch above one wave per CU; 5 = the kernels before.
     static const int mid_knob = [] {
         const char* e = std::getenv("STORMCK_MID_WAVES");
@@ -559,7 +560,7 @@ int launch_checksum(const uint8_t* base, uint64_t stride, const uint32_t* lens, 
     if (ncu_m > 0 && n < kBigBatch) {
         if (mid_knob >= 1 && mid_knob <= 4) {
             if (n > 16 * ncu_m) mid_waves = mid_knob;
-        } else if (mid_knob == 0 && n >= 39 * ncu_m) {
+        } else if (mid_knob == 0 && n >= 36 * ncu_m) {
             mid_waves = busiest(1) < busiest(3) ? 1 : 3;
         }
     } else if (ncu_m > 0 && n < kBigW && mid_knob == 0 && big_w_on()) {

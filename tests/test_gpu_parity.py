@@ -198,7 +198,7 @@ def test_wide_path_premultiplied_staging(dev, n):
 @pytest.mark.parametrize("length", [512, 513, 520, 1000, 8192, 28808, 30000, 31808, 32768])
 def test_uniform_fast_path_lengths(dev, length):
     """Uniform-length 16-byte-aligned batches of every batch-size class: <= 128 blocks
-    (one workgroup per block), below 39 blocks per CU (register quad), up to kBigW
+    (one workgroup per block), below 36 blocks per CU (register quad), up to kBigW
     (LDS-staged streaming kernel in 8-, 3- or 1-wave workgroups, whichever loads the
     busiest CU least), then 8-wave workgroups: whole tiles, remainder stripes and tails,
     partial last workgroup."""
@@ -230,9 +230,9 @@ def test_uniform_fast_path_lengths(dev, length):
     torch.cuda.synchronize()
     assert _u64(res).tolist() == [500, 2]
     # streaming-kernel batches: device-generated blocks, partial last workgroups, then
-    # verify. On 256 CUs 10,257 takes 3-wave workgroups, 16,389 1-wave ones, 24,641 and
-    # 32,768 the 8-wave ones, 36,864 3-wave ones again.
-    for n in (10240 + 17, 16384 + 5, 24576 + 65, 32768, 36864):
+    # verify. On 256 CUs 9,300 and 10,257 take 3-wave workgroups, 16,389 1-wave ones,
+    # 24,641 and 32,768 the 8-wave ones, 36,864 3-wave ones again.
+    for n in (9300, 10240 + 17, 16384 + 5, 24576 + 65, 32768, 36864):
         big = torch.empty((n, stride), dtype=torch.uint8, device=dev)
         engine.fill_synthetic_device(big.data_ptr(), stride, n, length, 0x1234)
         out = engine.checksum_tensor(big, length=length)
