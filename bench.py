@@ -41,6 +41,8 @@ REV = 1
 C3_BLOCKS = 16 << 20  # BASELINE.json configs[2]
 C4_BLOCKS = 64 << 20  # BASELINE.json configs[3]
 SYNTH_SEED = 0x53544F524D  # synthetic block generator seed ("STORM")
+# --alloc: (stormck_device_alloc_placed mode, physical chunk bytes)
+ALLOC_MODES = {"plain": (0, 0), "vmm": (1, 0), "vmm1g": (1, 1 << 30), "contig": (2, 0)}
 KERNEL = "k_xxh64_glds_skew<16,nt,8w,4KiB>"  # dominant kernel (storm_amd/csrc/kernels.h), as named in profiles/traffic.json
 
 
@@ -53,6 +55,10 @@ def parse():
                    help="blocks per GPU per step (weak scaling); default: c3 (16M) at N = 1, c4 (64M total) at N > 1")
     p.add_argument("--total-blocks", type=int, default=0, help="blocks over all GPUs per step (strong scaling)")
     p.add_argument("--arena", type=int, default=4 << 20, help="resident arena (blocks)")
+    p.add_argument("--alloc", default="plain", choices=sorted(ALLOC_MODES),
+                   help="arena placement (stormck_device_alloc_placed): plain = hipMalloc; vmm = a 1 GiB-aligned "
+                        "VMM reservation backed by one physical allocation; vmm1g = backed by 1 GiB allocations; "
+                        "contig = hipDeviceMallocContiguous")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget (rank 0, N=1)")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--settle", type=float, default=1.0,
@@ -298,8 +304,8 @@ def c5_workload(a):
     arena = torch.zeros(size, dtype=torch.uint8, device=dev)
     engine.fill_synthetic_device(arena.data_ptr() + BLOCK, BLOCK, n_ol, 0, 0x53544F524D)
 
-    def batch():
-        engine.checksum_device(buf.data_ptr(), BLOCK, n, out.data_ptr(), 0, d_lens.data_ptr(), st)
+    def batch():  # ring-fault status checked once per series below, not per launch
+        engine.checksum_device(buf.data_ptr(), BLOCK, n, out.data_ptr(), 0, d_lens.data_ptr(), st, check_status=False)
 
     settle(batch, a.settle)
     for _ in range(a.warmup):
@@ -310,6 +316,7 @@ def c5_workload(a):
         batch()
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
+    engine.device_status(st)  # raises if a ring launch of the series stalled
     cs = np.zeros(len(b0), dtype=np.uint64)
     settle(lambda: sc.commit_device(arena.data_ptr(), b0, REV, last, out=cs), a.settle)
     tc = time.perf_counter()
@@ -674,7 +681,8 @@ def block_checksum_workload(a) -> int:
     # The arena is the process's first device allocation (at N > 1, after RCCL's own
     # buffers), taken by plain hipMalloc through the library rather than torch's caching
     # allocator, so a profiled and a plain process place it the same way.
-    arena_ptr = engine.device_alloc(arena_n * BLOCK)
+    mode, chunk = ALLOC_MODES[a.alloc]
+    arena_ptr, mapped_chunk = engine.device_alloc_placed(arena_n * BLOCK, mode, chunk)
     cs = torch.empty(n_gpu, dtype=torch.int64, device=dev)
     ws = torch.empty(max(engine.merkle_workspace_bytes(n_gpu, FANOUT) // 8, 1), dtype=torch.int64, device=dev)
     torch.cuda.synchronize()
@@ -796,8 +804,12 @@ def block_checksum_workload(a) -> int:
                        "library": engine.library_record(),
                        "arena": {"va": "0x%x" % arena_ptr, "va_alignment": va_alignment(arena_ptr),
                                  "bytes": arena_n * BLOCK,
-                                 "alloc": "hipMalloc (stormck_device_alloc), the process's first device allocation"
-                                          + (" after the process group's" if distributed else "")},
+                                 "alloc": {"plain": "hipMalloc", "vmm": "VMM reserve (1 GiB aligned) + one hipMemCreate",
+                                           "vmm1g": "VMM reserve (1 GiB aligned) + 1 GiB hipMemCreate chunks",
+                                           "contig": "hipExtMallocWithFlags(hipDeviceMallocContiguous)"}[a.alloc]
+                                          + " (stormck_device_alloc_placed), the process's first device allocation"
+                                          + (" after the process group's" if distributed else ""),
+                                 "mode": a.alloc, "mapped_chunk": mapped_chunk},
                        "timed": "K steps between barrier + synchronize, minus the on-device regeneration of "
                                 "each arena pass (its own HIP events)",
                        "ms_per_step_with_regeneration": round(wall / a.steps * 1e3, 3)},

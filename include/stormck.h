@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define STORMCK_ABI_VERSION 2
+#define STORMCK_ABI_VERSION 3
 
 #define STORMCK_OK 0
 #define STORMCK_EINVAL (-1)  /* bad argument (null pointer, n/len/stride out of range, ...) */
@@ -76,19 +76,40 @@ int stormck_init(int device);
 void stormck_shutdown(void);
 /* Ring-kernel faults. The small-batch kernels stage blocks through an LDS ring whose
  * waits are bounded; a wait that expires (a liveness bug, never expected) is an error,
- * not a value: the kernel writes no checksum (and reports no mismatch) for the blocks
- * of the stalled workgroup and records a fault for the device. Host-synchronous entry
- * points (_host, _host_multi, stormck_commit_device, stormck_read_verify_fd) check it
- * after their sync and return STORMCK_EHIP naming the kernel; their outputs are then
- * unspecified. For the asynchronous _device entry points, stormck_device_status
- * synchronises `stream` and returns STORMCK_EHIP if any ring kernel on the calling
- * thread's current device faulted since the last check (the fault is then cleared),
- * otherwise the stream's own status. */
+ * not a value: the kernel writes no checksum for the blocks of the stalled workgroup (a
+ * verify counts each of them as a mismatch, so it fails closed) and records the fault in
+ * the slot of the STREAM it was launched on. Host-synchronous entry points (_host,
+ * _host_multi, stormck_commit_device, stormck_read_verify_fd) check their own streams'
+ * slots after their sync and return STORMCK_EHIP naming the kernel; their outputs are
+ * then unspecified. For the asynchronous _device entry points, stormck_device_status
+ * synchronises `stream` and returns STORMCK_EHIP if a ring kernel launched on that
+ * stream (on the calling thread's current device) faulted since the last check (the
+ * fault is then cleared), otherwise the stream's own status. Faults never cross streams:
+ * concurrent callers on distinct streams see only their own (the legacy null stream is
+ * one stream, shared by every thread of the device). The slots are allocated by
+ * stormck_init; a first ring launch inside a stream capture without it is STORMCK_EINVAL.
+ * Up to 1024 streams per device have a slot of their own at once; past that the least
+ * recently launched stream with no pending fault gives its slot up. */
 int stormck_device_status(void* stream);
 /* Device memory for a block arena (storm's cache.data mirrored in HBM) on the calling
- * thread's current device: plain hipMalloc, outside any caching allocator, so an arena
- * taken first in a process is placed the same way whatever else the process allocates. */
+ * thread's current device, outside any caching allocator, so an arena taken first in a
+ * process is placed the same way whatever else the process allocates.
+ * stormck_device_alloc = stormck_device_alloc_placed(bytes, STORMCK_ALLOC_PLAIN, 0, ...).
+ * Placement modes ("Arena placement"):
+ *   STORMCK_ALLOC_PLAIN       hipMalloc;
+ *   STORMCK_ALLOC_VMM         a 1 GiB-aligned VA reservation (hipMemAddressReserve) mapped
+ *                             to physical allocations (hipMemCreate) of chunk_bytes each
+ *                             (0: one allocation for the whole arena), rounded up to the
+ *                             device's allocation granularity; *mapped_chunk (optional)
+ *                             receives the chunk size used;
+ *   STORMCK_ALLOC_CONTIGUOUS  hipExtMallocWithFlags(hipDeviceMallocContiguous).
+ * stormck_device_free releases an arena of any mode. */
+#define STORMCK_ALLOC_PLAIN 0u
+#define STORMCK_ALLOC_VMM 1u
+#define STORMCK_ALLOC_CONTIGUOUS 2u
 int stormck_device_alloc(uint64_t bytes, void** d_ptr);
+int stormck_device_alloc_placed(uint64_t bytes, uint32_t mode, uint64_t chunk_bytes, void** d_ptr,
+                                uint64_t* mapped_chunk);
 int stormck_device_free(void* d_ptr);
 
 /* ---- hot path: batch checksums of device-resident blocks -------------------

@@ -12,6 +12,9 @@ import os
 from ctypes import POINTER, c_char_p, c_int, c_uint8, c_uint32, c_uint64, c_void_p
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libstormck.so")
+# STORMCK_LIBRARY=<path>: load another build of the same ABI instead, e.g. the probe build
+# tools/libstormck_probes.so (storm_amd/build.py), whose design knobs the product lacks
+LIB_PATH = os.environ.get("STORMCK_LIBRARY") or LIB_PATH
 
 OK = 0
 EINVAL = -1
@@ -19,6 +22,10 @@ EHIP = -2
 ENODEV = -3
 ENOMEM = -4
 EMISMATCH = -5
+
+ALLOC_PLAIN = 0       # STORMCK_ALLOC_* (include/stormck.h): arena placement modes
+ALLOC_VMM = 1
+ALLOC_CONTIGUOUS = 2
 
 
 class StormckError(RuntimeError):
@@ -49,6 +56,7 @@ SIGNATURES = {
     "stormck_shutdown": (None, []),
     "stormck_device_status": (c_int, [c_void_p]),
     "stormck_device_alloc": (c_int, [c_uint64, POINTER(c_void_p)]),
+    "stormck_device_alloc_placed": (c_int, [c_uint64, c_uint32, c_uint64, POINTER(c_void_p), POINTER(c_uint64)]),
     "stormck_device_free": (c_int, [c_void_p]),
     "stormck_checksum_device": (c_int, [c_void_p, c_uint64, c_void_p, c_uint32, c_uint64, c_void_p, c_void_p]),
     "stormck_checksum_gather_device": (c_int, [c_void_p, c_void_p, c_void_p, c_uint32, c_uint64, c_void_p, c_void_p]),

@@ -51,16 +51,33 @@ def sources_sha() -> str:
     return h.hexdigest()
 
 
+def _compile_lib(out: str, extra, sha: str) -> None:
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    tmp = out + ".tmp"
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall",
+           f'-DSTORMCK_SRC_SHA="{sha}"', *extra, "-o", tmp, os.path.join(CSRC, "stormck.hip")]
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, out)
+
+
 def build_lib(force: bool = False) -> str:
     if not force and _newer(LIB, SOURCES):
         return LIB
-    os.makedirs(LIB_DIR, exist_ok=True)
-    tmp = LIB + ".tmp"
-    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall",
-           f'-DSTORMCK_SRC_SHA="{sources_sha()}"', "-o", tmp, os.path.join(CSRC, "stormck.hip")]
-    subprocess.run(cmd, check=True)
-    os.replace(tmp, LIB)
+    _compile_lib(LIB, [], sources_sha())
     return LIB
+
+
+# The probe build: the same sources with -DSTORMCK_PROBES, i.e. with the variants measured
+# and rejected in DESIGN.md and the environment knobs that select them (stormck.hip
+# STORMCK_KNOB). Design tools and tests/test_probe_build.py load it; the product does not.
+PROBES_LIB = os.path.join(ROOT, "tools", "libstormck_probes.so")
+
+
+def build_probes_lib(force: bool = False) -> str:
+    if not force and _newer(PROBES_LIB, SOURCES):
+        return PROBES_LIB
+    _compile_lib(PROBES_LIB, ["-DSTORMCK_PROBES"], sources_sha() + "+probes")
+    return PROBES_LIB
 
 
 def build_oracle(force: bool = False) -> str:

@@ -619,10 +619,11 @@ __device__ __forceinline__ void multi_stage_hash(uint4* buf, uint32_t nlive, Src
 // chunk that never completes (a staging/chain disagreement would be a bug) must not
 // leave a wave that never exits. An expired wait is an ERROR, never a value: the
 // waiting wave sets the workgroup's abort word (every other wait of the workgroup then
-// returns at once), the chain emits no checksum for any of its blocks, stagers stop
-// writing slots, and the kernel stores its fault code into the library's fault word
-// (pinned host memory, one per device), which every host-synchronous entry point
-// checks after its sync and stormck_device_status() reports for the async ones.
+// returns at once), the chain emits no checksum for any of its blocks (a verify counts
+// them as mismatches), stagers stop writing slots, and the kernel stores its fault code
+// into the fault slot of the stream it runs on (pinned host memory, one per stream),
+// which the host-synchronous entry points check after their sync and
+// stormck_device_status(stream) reports for the async ones.
 // fault codes: kernel id | side
 constexpr uint32_t kFaultWideMulti = 1u, kFaultCommitMulti = 2u;
 constexpr uint32_t kFaultChain = 0x100u, kFaultStager = 0x200u;
@@ -635,7 +636,7 @@ struct PipeCtl {
     uint32_t* ready;   // pipe_max_chunks(CP) LDS counters
     uint32_t* done;    // LDS: chunks the chain has finished
     uint32_t* abort;   // LDS: set by the first expired wait
-    uint32_t* fault;   // pinned host word of the device, or null
+    uint32_t* fault;   // pinned host fault slot of the launch's stream, or null
     uint32_t kernel;   // kFault* id
     uint32_t stall;    // 0 = off
 };
@@ -670,9 +671,11 @@ __device__ __forceinline__ bool pipe_wait(const PipeCtl& pc, const uint32_t* wor
 // DBL: each stager keeps two chunks in flight (loads of chunk c+1 issued before chunk c
 // is stored): with 2 KiB chunks one chunk per memory round trip is less than the chains
 // consume.
-template <int BPW, uint32_t RS, uint32_t CP, bool DBL, class Src, class Emit>
+// Void(b): block b of a stalled workgroup gets no checksum; a verify counts it as a
+// mismatch there (fails closed), a checksum or commit launch leaves it unwritten.
+template <int BPW, uint32_t RS, uint32_t CP, bool DBL, class Src, class Emit, class Void>
 __device__ __forceinline__ void multi_stage_hash_pipe(uint4* ring, const PipeCtl& pc, uint32_t nlive, Src src_of,
-                                                      Emit emit) {
+                                                      Emit emit, Void void_block) {
     static_assert(BPW <= 16 && CP <= 256 && kPipeMaxPieces % CP == 0, "one chain wave, chunks of <= 256 pieces");
     uint32_t* ready = pc.ready;
     uint32_t* done = pc.done;
@@ -846,7 +849,10 @@ __device__ __forceinline__ void multi_stage_hash_pipe(uint4* ring, const PipeCtl
     // a stager that gave up (its wait for `done` expired) also voids the workgroup:
     // it may have left a slot unwritten that the chain already passed
     if (__hip_atomic_load(pc.abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) ok = false;
-    if (!ok) return;
+    if (!ok) {
+        if (j == 0 && live) void_block(b);
+        return;
+    }
     const uint64_t v1 = quad_bcast<0>(acc), v2 = quad_bcast<1>(acc), v3 = quad_bcast<2>(acc), v4 = quad_bcast<3>(acc);
     if (j == 0 && live) {
         const uint64_t h0 = (L >= 32) ? converge(v1, v2, v3, v4) : kP5;
@@ -890,7 +896,13 @@ __global__ __launch_bounds__(256) void k_xxh64_wide_multi(const uint8_t* __restr
         __shared__ uint4 ring[BPW * ring_block_pieces(RING, CP) + kRingSlackPieces];
         __shared__ uint32_t ready[pipe_max_chunks(CP)], done[1], abort_w[1];
         const PipeCtl pc{ready, done, abort_w, fault, kFaultWideMulti, stall};
-        multi_stage_hash_pipe<BPW, RING, CP, DBL>(ring, pc, nlive, src_of, emit);
+        auto void_block = [&](uint32_t b) {
+            if (VERIFY) {  // fail closed: an unhashed block is a mismatch
+                atomicMin(first_bad, static_cast<unsigned long long>(first + b));
+                atomicAdd(n_bad, 1ULL);
+            }
+        };
+        multi_stage_hash_pipe<BPW, RING, CP, DBL>(ring, pc, nlive, src_of, emit, void_block);
     } else {
         __shared__ uint4 buf[BPW * kMultiPieces];
         multi_stage_hash<BPW>(buf, nlive, src_of, emit);
@@ -2091,7 +2103,7 @@ __global__ __launch_bounds__(256) void k_commit_level_multi(uint8_t* __restrict_
         __shared__ uint4 ring[BPW * ring_block_pieces(RING, CP) + kRingSlackPieces];
         __shared__ uint32_t ready[pipe_max_chunks(CP)], done[1], abort_w[1];
         const PipeCtl pc{ready, done, abort_w, fault, kFaultCommitMulti, stall};
-        multi_stage_hash_pipe<BPW, RING, CP, DBL>(ring, pc, nlive, src_of, emit);
+        multi_stage_hash_pipe<BPW, RING, CP, DBL>(ring, pc, nlive, src_of, emit, [](uint32_t) {});
     } else {
         __shared__ uint4 buf[BPW * kMultiPieces];
         multi_stage_hash<BPW>(buf, nlive, src_of, emit);

@@ -138,7 +138,7 @@ constexpr int kAuxNT = 2;
 constexpr uint64_t kMultiBpw = 5;          // blocks per workgroup of k_xxh64_wide_multi
 constexpr uint64_t kMultiBpwRing = 8;      // ring staging, batches above kMultiBpw per CU (133 KiB of LDS)
 constexpr uint64_t kMultiBpwWide = 16;     // ring staging in 2 KiB chunks, batches above 8 per CU (133 KiB)
-constexpr uint32_t kChunkPiecesWide = 128; // the 2 KiB chunk of kMultiBpwWide
+[[maybe_unused]] constexpr uint32_t kChunkPiecesWide = 128;  // the 2 KiB chunk of kMultiBpwWide (probe build)
 constexpr uint64_t kWideBatch = 128;      // batches up to this many blocks: k_xxh64_wide
 constexpr uint64_t kCommitWide = 256;     // f1 levels up to this many blocks: k_commit_level_wide
 constexpr uint64_t kStreamBatch = 16384;  // f1 commit levels from this many blocks: k_commit_level_glds
@@ -211,26 +211,99 @@ uint64_t cu_count() {
     return static_cast<uint64_t>(v);
 }
 
-// Fault word of each device (kernels.h PipeCtl): one pinned, device-mapped, coherent u32,
-// allocated on first use (stormck_init allocates it up front). A ring kernel whose
-// bounded wait expired stores its fault code there and writes no checksum for the
-// affected blocks; host-synchronous entry points check it after their sync
-// (take_fault), stormck_device_status() for the asynchronous ones.
-std::mutex g_fault_mu;
-uint32_t* g_fault[64] = {};
+// Fault slots of the ring kernels (kernels.h PipeCtl), one per (device, stream). A ring
+// kernel whose bounded wait expired stores its fault code into the slot of the stream it
+// was launched on and writes no checksum for the blocks of the stalled workgroup (a verify
+// counts them as mismatches). A caller reads only its own stream's slot: the
+// host-synchronous entry points after their sync (take_fault on the library's staging
+// streams, or on the commit's stream), stormck_device_status(stream) for the asynchronous
+// ones, so a fault never reaches a caller on another stream (include/stormck.h). The slots
+// are pinned, device-mapped, coherent words, allocated with the device's table by
+// stormck_init or the first call that sets up the device (never inside a stream capture).
+// A table holds kFaultSlots streams; past that, the slot of the least recently launched
+// stream whose word is clear is reused.
+constexpr uint32_t kFaultSlots = 1024;
 
-int fault_word(uint32_t** out) {
+struct FaultTable {
+    std::mutex mu;
+    uint32_t* words = nullptr;                   // kFaultSlots words
+    std::vector<hipStream_t> owner;              // slot -> stream
+    std::vector<uint64_t> last_launch;           // slot -> sequence number of its last ring launch (0: free)
+    std::vector<std::pair<hipStream_t, uint32_t>> index;  // stream -> slot, for the streams that have one
+    uint64_t clock = 0;
+
+    int find(hipStream_t st) const {
+        for (const auto& e : index)
+            if (e.first == st) return static_cast<int>(e.second);
+        return -1;
+    }
+};
+FaultTable g_faults[64];
+
+// Allocate a device's fault slots (caller holds t.mu).
+int fault_table_alloc(FaultTable& t) {
+    if (t.words) return STORMCK_OK;
+    void* p = nullptr;
+    HIP_TRY(hipHostMalloc(&p, kFaultSlots * sizeof(uint32_t),
+                          hipHostMallocMapped | hipHostMallocPortable | hipHostMallocCoherent));
+    std::memset(p, 0, kFaultSlots * sizeof(uint32_t));
+    t.words = static_cast<uint32_t*>(p);
+    t.owner.assign(kFaultSlots, nullptr);
+    t.last_launch.assign(kFaultSlots, 0);
+    return STORMCK_OK;
+}
+
+int fault_table_ready(int dev) {
+    if (dev < 0 || dev >= 64) return fail(STORMCK_EINVAL, "device index beyond 64");
+    FaultTable& t = g_faults[dev];
+    std::lock_guard<std::mutex> g(t.mu);
+    return fault_table_alloc(t);
+}
+
+// The fault slot a ring kernel launched on stream `st` of the current device writes.
+int fault_slot(hipStream_t st, uint32_t** out) {
     int dev = 0;
     HIP_TRY(hipGetDevice(&dev));
     if (dev < 0 || dev >= 64) return fail(STORMCK_EINVAL, "device index beyond 64");
-    std::lock_guard<std::mutex> g(g_fault_mu);
-    if (!g_fault[dev]) {
-        void* p = nullptr;
-        HIP_TRY(hipHostMalloc(&p, 64, hipHostMallocMapped | hipHostMallocPortable | hipHostMallocCoherent));
-        std::memset(p, 0, 64);
-        g_fault[dev] = static_cast<uint32_t*>(p);
+    FaultTable& t = g_faults[dev];
+    std::lock_guard<std::mutex> g(t.mu);
+    if (!t.words) {
+        hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+        if (hipStreamIsCapturing(st, &cap) != hipSuccess) (void)hipGetLastError();
+        if (cap != hipStreamCaptureStatusNone)
+            return fail(STORMCK_EINVAL, "first ring-kernel launch on device " + std::to_string(dev) +
+                                            " inside a stream capture: call stormck_init(" + std::to_string(dev) +
+                                            ") before capturing");
+        const int rc = fault_table_alloc(t);
+        if (rc) return rc;
     }
-    *out = g_fault[dev];
+    int s = t.find(st);
+    if (s < 0) {
+        // a free slot, else the least recently launched one whose word is clear
+        int pick = -1;
+        for (uint32_t i = 0; i < kFaultSlots && pick < 0; ++i)
+            if (t.last_launch[i] == 0) pick = static_cast<int>(i);
+        if (pick < 0) {
+            uint64_t oldest = UINT64_MAX;
+            for (uint32_t i = 0; i < kFaultSlots; ++i)
+                if (__atomic_load_n(t.words + i, __ATOMIC_ACQUIRE) == 0 && t.last_launch[i] < oldest) {
+                    oldest = t.last_launch[i];
+                    pick = static_cast<int>(i);
+                }
+            if (pick < 0) return fail(STORMCK_EHIP, "every ring-kernel fault slot holds an unreported fault");
+            for (size_t k = 0; k < t.index.size(); ++k)
+                if (t.index[k].second == static_cast<uint32_t>(pick)) {
+                    t.index[k] = t.index.back();
+                    t.index.pop_back();
+                    break;
+                }
+        }
+        s = pick;
+        t.owner[s] = st;
+        t.index.emplace_back(st, static_cast<uint32_t>(s));
+    }
+    t.last_launch[s] = ++t.clock;
+    *out = t.words + s;
     return STORMCK_OK;
 }
 
@@ -242,37 +315,57 @@ std::string fault_text(uint32_t code) {
            " expired); no checksum was written for the blocks of the stalled workgroup";
 }
 
-// After a sync on device `dev`: STORMCK_EHIP with the fault's text if a ring kernel
-// reported one since the last check (the word is then cleared), else STORMCK_OK.
-int take_fault(int dev) {
+// After a sync of stream `st` on device `dev`: STORMCK_EHIP with the fault's text if a
+// ring kernel launched on `st` reported one since the last check (the slot is then
+// cleared), else STORMCK_OK. Other streams' slots are not read.
+int take_fault(int dev, hipStream_t st) {
     if (dev < 0 || dev >= 64) return STORMCK_OK;
-    uint32_t* w = nullptr;
+    FaultTable& t = g_faults[dev];
+    uint32_t code = 0;
     {
-        std::lock_guard<std::mutex> g(g_fault_mu);
-        w = g_fault[dev];
+        std::lock_guard<std::mutex> g(t.mu);
+        if (!t.words) return STORMCK_OK;
+        const int s = t.find(st);
+        if (s < 0) return STORMCK_OK;
+        code = __atomic_exchange_n(t.words + s, 0u, __ATOMIC_ACQ_REL);
     }
-    if (!w) return STORMCK_OK;
-    const uint32_t code = __atomic_exchange_n(w, 0u, __ATOMIC_ACQ_REL);
     if (code == 0) return STORMCK_OK;
     return fail(STORMCK_EHIP, "device " + std::to_string(dev) + ": " + fault_text(code));
 }
 
 // STORMCK_DEBUG_STALL_CHUNK=c: stager wave 1 of workgroup 0 of every ring kernel never
-// reports chunk c (c >= 1), so the chain's wait expires (tests of the fault path only).
-uint32_t debug_stall() {
+// reports chunk c (c >= 1), so the chain's wait expires (tests of the fault path only);
+// with STORMCK_DEBUG_STALL_STREAM=<stream handle>, only the launches on that stream.
+uint32_t debug_stall(hipStream_t st) {
     static const uint32_t c = [] {
         const char* e = std::getenv("STORMCK_DEBUG_STALL_CHUNK");
         return e ? static_cast<uint32_t>(std::strtoul(e, nullptr, 10)) : 0u;
     }();
-    return c;
+    static const uintptr_t only = [] {
+        const char* e = std::getenv("STORMCK_DEBUG_STALL_STREAM");
+        return e ? static_cast<uintptr_t>(std::strtoull(e, nullptr, 0)) : uintptr_t{0};
+    }();
+    return (only == 0 || reinterpret_cast<uintptr_t>(st) == only) ? c : 0u;
 }
+
+// Probe knobs. The shipped library has one dispatch, fixed at compile time. The variants
+// measured and rejected in DESIGN.md, and the environment switches that select them, are
+// compiled only into the probe build (-DSTORMCK_PROBES: tools/libstormck_probes.so, which
+// the design tools and tests/test_probe_build.py load). In this build every
+// STORMCK_KNOB(...) is null, so each switch folds to its default and the rejected
+// kernels are not instantiated.
+#ifdef STORMCK_PROBES
+#define STORMCK_KNOB(NAME) std::getenv(NAME)
+#else
+#define STORMCK_KNOB(NAME) (static_cast<const char*>(nullptr))
+#endif
 
 // Ring depth of the pipelined staging in the wide-multi kernels (kernels.h
 // multi_stage_hash_pipe): kRingSlots; probe knob STORMCK_STAGE_PIPE=0 stages whole blocks
 // first (A/B). 6- and 7-slot rings were measured slower.
 uint32_t pipe_staging() {
     static const uint32_t slots = [] {
-        const char* e = std::getenv("STORMCK_STAGE_PIPE");
+        const char* e = STORMCK_KNOB("STORMCK_STAGE_PIPE");
         return (e && e[0] == '0') ? 0u : kRingSlots;
     }();
     return slots;
@@ -284,7 +377,7 @@ uint32_t pipe_staging() {
 // against 34.7 / 35.0 / 35.1 us, profiles/r03c/), so off; probe knob STORMCK_WIDE16=1.
 bool wide16_on() {
     static const bool on = [] {
-        const char* e = std::getenv("STORMCK_WIDE16");
+        const char* e = STORMCK_KNOB("STORMCK_WIDE16");
         return e && e[0] == '1';
     }();
     return on;
@@ -303,19 +396,31 @@ uint64_t multi_bpw(uint64_t n, uint64_t ncu) {
     return 0;
 }
 
-// The stream-ordered workspaces come from the device's default pool; keep what it has
-// reserved across calls instead of returning it at every synchronisation (once per device).
-void keep_pool_memory() {
-    static std::atomic<bool> done[64] = {};
+// Stream-ordered workspaces (the gather order) come from a private pool per device that
+// keeps what it has reserved across calls; the device's default pool, which other
+// libraries of the process (torch's hipMallocAsync backend) may use, is left as it is.
+int workspace_pool(hipMemPool_t* out) {
+    static std::mutex mu;
+    static hipMemPool_t pools[64] = {};
     int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64 || done[dev].load()) return;
-    hipMemPool_t pool = nullptr;
-    if (hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess) {
+    HIP_TRY(hipGetDevice(&dev));
+    if (dev < 0 || dev >= 64) return fail(STORMCK_EINVAL, "device index beyond 64");
+    std::lock_guard<std::mutex> g(mu);
+    if (!pools[dev]) {
+        hipMemPoolProps props;
+        std::memset(&props, 0, sizeof props);
+        props.allocType = hipMemAllocationTypePinned;
+        props.handleTypes = hipMemHandleTypeNone;
+        props.location.type = hipMemLocationTypeDevice;
+        props.location.id = dev;
+        hipMemPool_t p = nullptr;
+        HIP_TRY(hipMemPoolCreate(&p, &props));
         uint64_t thr = UINT64_MAX;
-        (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr);
+        HIP_TRY(hipMemPoolSetAttribute(p, hipMemPoolAttrReleaseThreshold, &thr));
+        pools[dev] = p;
     }
-    (void)hipGetLastError();
-    done[dev].store(true);
+    *out = pools[dev];
+    return STORMCK_OK;
 }
 
 // Gathers of at least this many blocks visit them in a locality order (k_order_*); probe
@@ -323,7 +428,7 @@ void keep_pool_memory() {
 constexpr uint64_t kOrderMinBlocks = 1u << 20;
 bool order_on() {
     static const bool on = [] {
-        const char* e = std::getenv("STORMCK_GATHER_ORDER");
+        const char* e = STORMCK_KNOB("STORMCK_GATHER_ORDER");
         return !(e && e[0] == '0');
     }();
     return on;
@@ -338,7 +443,7 @@ bool grid_for(uint64_t threads, dim3* grid) {
 
 bool big_w_on() {  // probe knob STORMCK_BIG_W=0: batches from kBigBatch on always take 8-wave workgroups
     static const bool on = [] {
-        const char* e = std::getenv("STORMCK_BIG_W");
+        const char* e = STORMCK_KNOB("STORMCK_BIG_W");
         return !(e && e[0] == '0');
     }();
     return on;
@@ -379,7 +484,7 @@ int launch_checksum(const uint8_t* base, uint64_t stride, const uint32_t* lens, 
     // up to 5 blocks per CU (8 with ring staging): k_xxh64_wide_multi, one workgroup per
     // CU staging 5 (8) premultiplied blocks (the c5 commit batch is one such launch)
     static const bool multi_on = [] {
-        const char* e = std::getenv("STORMCK_WIDE_MULTI");  // probe knob: "0" disables
+        const char* e = STORMCK_KNOB("STORMCK_WIDE_MULTI");  // probe knob: "0" disables
         return !(e && e[0] == '0');
     }();
     const uint32_t ring_slots = pipe_staging();
@@ -392,27 +497,34 @@ int launch_checksum(const uint8_t* base, uint64_t stride, const uint32_t* lens, 
          ((reinterpret_cast<uintptr_t>(base) & 7) == 0 && (stride & 7) == 0 &&
           ((reinterpret_cast<uintptr_t>(base) & 15) + len + 15) / 16 <= multi_pieces))) {
         const dim3 grid(static_cast<unsigned>((n + bpw - 1) / bpw));
-        uint32_t* fault = nullptr;
+        uint32_t* fault = nullptr;  // the fault slot of this launch's stream
         if (ring_slots) {
-            const int frc = fault_word(&fault);
+            const int frc = fault_slot(st, &fault);
             if (frc) return frc;
         }
-        const uint32_t stall = debug_stall();
-#define STORMCK_MULTI(LENS, OFFS, VER)                                                                         \
-    do {                                                                                                      \
+        const uint32_t stall = debug_stall(st);
+#ifdef STORMCK_PROBES  // the rejected 16-block / whole-block-staging variants
+#define STORMCK_MULTI_PROBES(LENS, OFFS, VER)                                                                  \
         if (ring_slots && bpw == kMultiBpwWide)                                                               \
             hipLaunchKernelGGL((k_xxh64_wide_multi<LENS, OFFS, VER, kMultiBpwWide, kRingSlots, kChunkPiecesWide, true>), \
                                grid, dim3(kThreads), 0, st, base, stride, lens, len, offs, n, out, expected,   \
                                first_bad, n_bad, fault, stall);                                               \
-        else if (ring_slots && bpw == kMultiBpw)                                                              \
-            hipLaunchKernelGGL((k_xxh64_wide_multi<LENS, OFFS, VER, kMultiBpw, kRingSlots>), grid, dim3(kThreads), \
-                               0, st, base, stride, lens, len, offs, n, out, expected, first_bad, n_bad, fault, stall); \
-        else if (ring_slots)                                                                                  \
-            hipLaunchKernelGGL((k_xxh64_wide_multi<LENS, OFFS, VER, kMultiBpwRing, kRingSlots>), grid, dim3(kThreads), \
-                               0, st, base, stride, lens, len, offs, n, out, expected, first_bad, n_bad, fault, stall); \
-        else                                                                                                  \
+        else if (!ring_slots)                                                                                 \
             hipLaunchKernelGGL((k_xxh64_wide_multi<LENS, OFFS, VER, kMultiBpw, 0>), grid, dim3(kThreads), 0,    \
                                st, base, stride, lens, len, offs, n, out, expected, first_bad, n_bad, fault, stall); \
+        else
+#else
+#define STORMCK_MULTI_PROBES(LENS, OFFS, VER)
+#endif
+#define STORMCK_MULTI(LENS, OFFS, VER)                                                                         \
+    do {                                                                                                      \
+        STORMCK_MULTI_PROBES(LENS, OFFS, VER)                                                                 \
+        if (bpw == kMultiBpw)                                                                                 \
+            hipLaunchKernelGGL((k_xxh64_wide_multi<LENS, OFFS, VER, kMultiBpw, kRingSlots>), grid, dim3(kThreads), \
+                               0, st, base, stride, lens, len, offs, n, out, expected, first_bad, n_bad, fault, stall); \
+        else                                                                                                  \
+            hipLaunchKernelGGL((k_xxh64_wide_multi<LENS, OFFS, VER, kMultiBpwRing, kRingSlots>), grid, dim3(kThreads), \
+                               0, st, base, stride, lens, len, offs, n, out, expected, first_bad, n_bad, fault, stall); \
     } while (0)
         if (!verify) {
             if (lens && offs) STORMCK_MULTI(true, true, false);
@@ -426,6 +538,7 @@ int launch_checksum(const uint8_t* base, uint64_t stride, const uint32_t* lens, 
             else STORMCK_MULTI(false, false, true);
         }
 #undef STORMCK_MULTI
+#undef STORMCK_MULTI_PROBES
         HIP_TRY(hipGetLastError());
         return STORMCK_OK;
     }
@@ -436,7 +549,7 @@ int launch_checksum(const uint8_t* base, uint64_t stride, const uint32_t* lens, 
     // kernel, which hashes an unaligned one from global memory. Probe knob
     // STORMCK_GLDS_VAR=0 restores the quad kernel (A/B).
     static const bool var_on = [] {
-        const char* e = std::getenv("STORMCK_GLDS_VAR");
+        const char* e = STORMCK_KNOB("STORMCK_GLDS_VAR");
         return !(e && e[0] == '0');
     }();
     // From 44 blocks per CU (11,264 on 256 CUs): storm-mix batches in us, var kernel /
@@ -444,7 +557,7 @@ int launch_checksum(const uint8_t* base, uint64_t stride, const uint32_t* lens, 
     // 82.1 / 124, 49,152 238 / 299 (profiles/r03_mid/varlo*, varhi*). Probe knob
     // STORMCK_VAR_LO: the smallest batch for the var kernel.
     static const uint64_t var_lo = [] {
-        const char* e = std::getenv("STORMCK_VAR_LO");
+        const char* e = STORMCK_KNOB("STORMCK_VAR_LO");
         return e ? std::strtoull(e, nullptr, 10) : 0;
     }();
     if (var_on && n >= (var_lo ? var_lo : std::max<uint64_t>(kMidBatch, 44 * cu_count())) && n > 16 * cu_count() &&
@@ -458,7 +571,7 @@ int launch_checksum(const uint8_t* base, uint64_t stride, const uint32_t* lens, 
         const bool big3 = n >= kBigBatch && n < kBigW && big_w_on() && 4 * busiest(3) <= 3 * busiest(8);
         const bool big = n >= kBigBatch && !big3;
         static const bool var_before = [] {  // probe knob STORMCK_MID_WAVES=5: 2-wave workgroups (A/B)
-            const char* e = std::getenv("STORMCK_MID_WAVES");
+            const char* e = STORMCK_KNOB("STORMCK_MID_WAVES");
             return e && e[0] == '5';
         }();
         const int vw = var_before ? 2 : (big3 || busiest(3) <= busiest(1)) ? 3 : 1;
@@ -471,13 +584,16 @@ int launch_checksum(const uint8_t* base, uint64_t stride, const uint32_t* lens, 
         const bool persistent = big && cus > 0 && wgs >= cus && (wgs + cus - 1) / cus * tiles >= kSkewMinSteps;
         const dim3 grid(static_cast<unsigned>(persistent ? cus : wgs));
         // large gathers visit their blocks in a locality order (kernels.h k_order_*): a
-        // stream-ordered workspace (the count matrix, the order, the offsets and lengths in
-        // that order: 16 bytes per block), freed on the stream after the launch
+        // stream-ordered workspace from the library's own pool (the count matrix, the
+        // order, the offsets and lengths in that order: 16 bytes per block), freed on the
+        // stream after the launch
         if (offs && !verify && big && n >= kOrderMinBlocks && n < (uint64_t{1} << 32) && order_on()) {
-            keep_pool_memory();
+            hipMemPool_t pool = nullptr;
+            const int prc = workspace_pool(&pool);
+            if (prc) return prc;
             const uint64_t words = (uint64_t{kOrderBuckets} * (kOrderParts + 2) + n + 1) & ~uint64_t{1};
             void* ws = nullptr;
-            HIP_TRY(hipMallocAsync(&ws, words * 4 + n * 8 + (lens ? n * 4 : 0), st));
+            HIP_TRY(hipMallocFromPoolAsync(&ws, words * 4 + n * 8 + (lens ? n * 4 : 0), pool, st));
             uint32_t* counts = static_cast<uint32_t*>(ws);  // [bucket][part], then positions
             uint32_t* bounds = counts + kOrderBuckets * kOrderParts;
             uint32_t* order = bounds + 2 * kOrderBuckets;
@@ -508,14 +624,21 @@ int launch_checksum(const uint8_t* base, uint64_t stride, const uint32_t* lens, 
 #define STORMCK_VAR(VER, W, SK, LN, OF)                                                                          \
     hipLaunchKernelGGL((k_xxh64_glds_var<kTileStripes, kAuxNT, VER, W, SK, LN, OF>), grid, dim3(64 * W), 0, st, base, \
                        stride, lens, len, offs, n, out, expected, first_bad, n_bad, nullptr)
+#ifdef STORMCK_PROBES  // the 2-wave workgroups before round 3
+#define STORMCK_VAR_PROBES(LN, OF)                                                                               \
+        if (!big && vw == 2) {                                                                                   \
+            if (verify) STORMCK_VAR(true, 2, 0, LN, OF);                                                         \
+            else STORMCK_VAR(false, 2, 0, LN, OF);                                                               \
+        } else
+#else
+#define STORMCK_VAR_PROBES(LN, OF)
+#endif
 #define STORMCK_VAR_SHAPE(LN, OF)                                                                                \
     do {                                                                                                         \
+        STORMCK_VAR_PROBES(LN, OF)                                                                               \
         if (!big && vw == 1) {                                                                                   \
             if (verify) STORMCK_VAR(true, 1, 0, LN, OF);                                                         \
             else STORMCK_VAR(false, 1, 0, LN, OF);                                                               \
-        } else if (!big && vw == 2) {                                                                            \
-            if (verify) STORMCK_VAR(true, 2, 0, LN, OF);                                                         \
-            else STORMCK_VAR(false, 2, 0, LN, OF);                                                               \
         } else if (!big) {                                                                                       \
             if (verify) STORMCK_VAR(true, 3, 0, LN, OF);                                                         \
             else STORMCK_VAR(false, 3, 0, LN, OF);                                                               \
@@ -531,6 +654,7 @@ int launch_checksum(const uint8_t* base, uint64_t stride, const uint32_t* lens, 
         else if (lens) STORMCK_VAR_SHAPE(true, false);
         else STORMCK_VAR_SHAPE(false, true);
 #undef STORMCK_VAR_SHAPE
+#undef STORMCK_VAR_PROBES
 #undef STORMCK_VAR
         HIP_TRY(hipGetLastError());
         return STORMCK_OK;
@@ -542,10 +666,11 @@ int launch_checksum(const uint8_t* base, uint64_t stride, const uint32_t* lens, 
     // HIP events, profiles/r03_mid/w*): 10,000 54.2 (60.9), 10,240 54.6 (60.1), 12,288
     // 60.3 (65.6), 16,384 77.7 (81.8), 20,000 101.7 (112.2), 24,575 122.1 (126.3). Below
     // it the quad kernels win (8,192 / 8,704: 39.9 / 47.9 against 51.6 / 52.2 for 3 waves;
-    // 9,216 / 9,728: 54.0 / 58.7 against 53.0 / 53.8, profiles/r03_mid/unilo*). Probe knob STORMCK_MID_WAVES =
-    // 1-4 forces W for every batch above one wave per CU; 5 = the kernels before.
+    // 9,216 / 9,728: 54.0 / 58.7 against 53.0 / 53.8, profiles/r03_mid/unilo*). Probe knob
+    // STORMCK_MID_WAVES = 1-4 forces W for every batch above one wave per CU; 5 = the
+    // kernels before.
     static const int mid_knob = [] {
-        const char* e = std::getenv("STORMCK_MID_WAVES");
+        const char* e = STORMCK_KNOB("STORMCK_MID_WAVES");
         return e ? std::atoi(e) : 0;
     }();
     // From kBigBatch up to kBigW blocks: 3-wave workgroups instead of the big path's
@@ -572,15 +697,20 @@ int launch_checksum(const uint8_t* base, uint64_t stride, const uint32_t* lens, 
 #define STORMCK_MIDW(W, VER)                                                                                      \
     hipLaunchKernelGGL((k_xxh64_glds<kTileStripes, kRing, kAuxNT, true, VER, W, false>), g, dim3(64 * W), 0, st, base, \
                        stride, len, n, out, expected, first_bad, n_bad)
-        switch (mid_waves * 2 + (verify ? 1 : 0)) {
-            case 2: STORMCK_MIDW(1, false); break;
-            case 3: STORMCK_MIDW(1, true); break;
-            case 4: STORMCK_MIDW(2, false); break;
-            case 5: STORMCK_MIDW(2, true); break;
-            case 6: STORMCK_MIDW(3, false); break;
-            case 7: STORMCK_MIDW(3, true); break;
-            case 8: STORMCK_MIDW(4, false); break;
-            default: STORMCK_MIDW(4, true); break;
+        if (mid_waves == 1) {
+            if (verify) STORMCK_MIDW(1, true);
+            else STORMCK_MIDW(1, false);
+        } else if (mid_waves == 2) {
+            if (verify) STORMCK_MIDW(2, true);
+            else STORMCK_MIDW(2, false);
+#ifdef STORMCK_PROBES
+        } else if (mid_waves == 4) {
+            if (verify) STORMCK_MIDW(4, true);
+            else STORMCK_MIDW(4, false);
+#endif
+        } else {
+            if (verify) STORMCK_MIDW(3, true);
+            else STORMCK_MIDW(3, false);
         }
 #undef STORMCK_MIDW
         HIP_TRY(hipGetLastError());
@@ -638,7 +768,7 @@ int launch_checksum(const uint8_t* base, uint64_t stride, const uint32_t* lens, 
     // slots (38-60 us over 2,064-8,192 blocks, profiles/r03_mid/probe_*). Probe knob
     // STORMCK_QUAD_SPREAD = waves per CU it covers (0 disables).
     static const uint64_t spread_mult = [] {  // batches of up to spread_mult waves per CU
-        const char* e = std::getenv("STORMCK_QUAD_SPREAD");
+        const char* e = STORMCK_KNOB("STORMCK_QUAD_SPREAD");
         return e ? static_cast<uint64_t>(std::atoi(e)) : uint64_t{1};
     }();
     const uint64_t ncu_q = cu_count();
@@ -755,6 +885,8 @@ int get_ctx(DeviceCtx** out) {
     if (rc) return rc;
     int dev = 0;
     HIP_TRY(hipGetDevice(&dev));
+    rc = fault_table_ready(dev);  // the ring kernels' fault slots come with the device's context
+    if (rc) return rc;
     std::lock_guard<std::mutex> g(g_ctx_mu);
     if (g_ctx.size() <= static_cast<size_t>(dev)) g_ctx.resize(dev + 1);
     if (!g_ctx[dev]) {
@@ -880,7 +1012,7 @@ int host_pipeline(const void* base, uint64_t stride, const uint32_t* lens, uint3
         s.busy = false;
         // a stalled ring kernel wrote no checksum (or no mismatch) for some blocks:
         // nothing of this stage reaches the caller
-        const int frc = take_fault(c->device);
+        const int frc = take_fault(c->device, s.stream);
         if (frc) return frc;
         if (expected) {
             if (s.h_result[1] > 0) {
@@ -1050,6 +1182,16 @@ int host_pipeline_multi(const void* base, uint64_t stride, const uint32_t* lens,
     return STORMCK_OK;
 }
 
+// Arenas from stormck_device_alloc_placed(STORMCK_ALLOC_VMM): their physical chunks, so
+// that stormck_device_free can unmap and release them.
+constexpr uint64_t kVmmAlign = 1ULL << 30;
+struct VmmArena {
+    uint64_t size = 0, chunk = 0;
+    std::vector<hipMemGenericAllocationHandle_t> handles;
+};
+std::mutex g_arena_mu;
+std::vector<std::pair<void*, VmmArena>> g_vmm;
+
 }  // namespace
 
 // ============================================================================
@@ -1091,8 +1233,7 @@ int stormck_init(int device) {
     DeviceCtx* c = nullptr;
     rc = get_ctx(&c);  // host-path staging is allocated on first host call
     if (rc) return rc;
-    uint32_t* fw = nullptr;  // the ring kernels' fault word, before any capture can start
-    return fault_word(&fw);
+    return fault_table_ready(device);  // the ring kernels' fault slots, before any capture can start
 }
 
 int stormck_device_status(void* stream) {
@@ -1101,22 +1242,87 @@ int stormck_device_status(void* stream) {
     int dev = 0;
     HIP_TRY(hipGetDevice(&dev));
     HIP_TRY(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
-    return take_fault(dev);
+    return take_fault(dev, static_cast<hipStream_t>(stream));
 }
 
 int stormck_device_alloc(uint64_t bytes, void** d_ptr) {
+    return stormck_device_alloc_placed(bytes, STORMCK_ALLOC_PLAIN, 0, d_ptr, nullptr);
+}
+
+int stormck_device_alloc_placed(uint64_t bytes, uint32_t mode, uint64_t chunk_bytes, void** d_ptr,
+                                uint64_t* mapped_chunk) {
     if (!d_ptr) return fail(STORMCK_EINVAL, "d_ptr is null");
     *d_ptr = nullptr;
+    if (mapped_chunk) *mapped_chunk = 0;
     if (bytes == 0) return fail(STORMCK_EINVAL, "bytes is 0");
+    if (mode > STORMCK_ALLOC_CONTIGUOUS) return fail(STORMCK_EINVAL, "unknown allocation mode");
     int rc = device_check();
     if (rc) return rc;
-    // probe knob STORMCK_ALLOC_CONTIGUOUS=1: physically contiguous (large page fragments)
-    static const bool contiguous = [] {
-        const char* e = std::getenv("STORMCK_ALLOC_CONTIGUOUS");
-        return e && e[0] == '1';
-    }();
-    if (contiguous) HIP_TRY(hipExtMallocWithFlags(d_ptr, bytes, hipDeviceMallocContiguous));
-    else HIP_TRY(hipMalloc(d_ptr, bytes));
+    if (mode == STORMCK_ALLOC_PLAIN) {
+        HIP_TRY(hipMalloc(d_ptr, bytes));
+        return STORMCK_OK;
+    }
+    if (mode == STORMCK_ALLOC_CONTIGUOUS) {
+        HIP_TRY(hipExtMallocWithFlags(d_ptr, bytes, hipDeviceMallocContiguous));
+        return STORMCK_OK;
+    }
+    // STORMCK_ALLOC_VMM: a 1 GiB-aligned reservation backed by physical chunks
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev));
+    hipMemAllocationProp prop;
+    std::memset(&prop, 0, sizeof prop);
+    prop.type = hipMemAllocationTypePinned;
+    prop.location.type = hipMemLocationTypeDevice;
+    prop.location.id = dev;
+    size_t gmin = 0, grec = 0;
+    HIP_TRY(hipMemGetAllocationGranularity(&gmin, &prop, hipMemAllocationGranularityMinimum));
+    HIP_TRY(hipMemGetAllocationGranularity(&grec, &prop, hipMemAllocationGranularityRecommended));
+    const uint64_t gran = std::max<uint64_t>({gmin, grec, 1});
+    auto round_up = [](uint64_t v, uint64_t m) { return (v + m - 1) / m * m; };
+    const uint64_t chunk = round_up(chunk_bytes ? chunk_bytes : bytes, gran);
+    const uint64_t size = round_up(bytes, chunk);
+    VmmArena a;
+    a.size = size;
+    void* va = nullptr;
+    HIP_TRY(hipMemAddressReserve(&va, size, kVmmAlign, nullptr, 0));
+    auto undo = [&] {
+        for (size_t k = 0; k < a.handles.size(); ++k) {
+            (void)hipMemUnmap(static_cast<uint8_t*>(va) + k * chunk, chunk);
+            (void)hipMemRelease(a.handles[k]);
+        }
+        (void)hipMemAddressFree(va, size);
+        (void)hipGetLastError();
+    };
+    for (uint64_t off = 0; off < size; off += chunk) {
+        hipMemGenericAllocationHandle_t h;
+        hipError_t e = hipMemCreate(&h, chunk, &prop, 0);
+        if (e == hipSuccess) {
+            e = hipMemMap(static_cast<uint8_t*>(va) + off, chunk, 0, h, 0);
+            if (e != hipSuccess) (void)hipMemRelease(h);
+            else a.handles.push_back(h);
+        }
+        if (e != hipSuccess) {
+            undo();
+            return fail(e == hipErrorOutOfMemory ? STORMCK_ENOMEM : STORMCK_EHIP,
+                        std::string("VMM arena: ") + hipGetErrorString(e));
+        }
+    }
+    hipMemAccessDesc acc;
+    std::memset(&acc, 0, sizeof acc);
+    acc.location = prop.location;
+    acc.flags = hipMemAccessFlagsProtReadWrite;
+    const hipError_t e = hipMemSetAccess(va, size, &acc, 1);
+    if (e != hipSuccess) {
+        undo();
+        return fail(STORMCK_EHIP, std::string("VMM arena: hipMemSetAccess: ") + hipGetErrorString(e));
+    }
+    a.chunk = chunk;
+    {
+        std::lock_guard<std::mutex> g(g_arena_mu);
+        g_vmm.emplace_back(va, std::move(a));
+    }
+    *d_ptr = va;
+    if (mapped_chunk) *mapped_chunk = chunk;
     return STORMCK_OK;
 }
 
@@ -1124,7 +1330,28 @@ int stormck_device_free(void* d_ptr) {
     if (!d_ptr) return STORMCK_OK;
     int rc = device_check();
     if (rc) return rc;
-    HIP_TRY(hipFree(d_ptr));
+    VmmArena a;
+    bool vmm = false;
+    {
+        std::lock_guard<std::mutex> g(g_arena_mu);
+        for (size_t k = 0; k < g_vmm.size(); ++k)
+            if (g_vmm[k].first == d_ptr) {
+                a = std::move(g_vmm[k].second);
+                g_vmm.erase(g_vmm.begin() + static_cast<long>(k));
+                vmm = true;
+                break;
+            }
+    }
+    if (!vmm) {
+        HIP_TRY(hipFree(d_ptr));
+        return STORMCK_OK;
+    }
+    HIP_TRY(hipDeviceSynchronize());  // hipFree's implicit wait: no kernel may still read the arena
+    for (size_t k = 0; k < a.handles.size(); ++k) {
+        HIP_TRY(hipMemUnmap(static_cast<uint8_t*>(d_ptr) + k * a.chunk, a.chunk));
+        HIP_TRY(hipMemRelease(a.handles[k]));
+    }
+    HIP_TRY(hipMemAddressFree(d_ptr, a.size));
     return STORMCK_OK;
 }
 
@@ -1227,7 +1454,7 @@ int stormck_checksum(const void* p, uint64_t n_bytes, uint64_t* out) {
     // STORMCK_SINGLE_GPU_MIN=<bytes> sends single calls of at least that many bytes to
     // the device (A/B measurement only).
     static const uint64_t gpu_min = [] {
-        const char* e = std::getenv("STORMCK_SINGLE_GPU_MIN");
+        const char* e = STORMCK_KNOB("STORMCK_SINGLE_GPU_MIN");
         return e ? std::strtoull(e, nullptr, 10) : UINT64_MAX;
     }();
     if (n_bytes >= gpu_min) return stormck_checksum_gpu(p, n_bytes, out);
@@ -1309,7 +1536,7 @@ int stormck_pointer_level_device(const uint64_t* d_child_cs, uint64_t m, uint64_
     // producing and hashing, 30- and 45-stripe tiles, prefetch 4 and 12 tiles, two pairs
     // per workgroup, one producer for two chain waves): DESIGN.md §5, profiles/r02_merkle/.
     static const int ring_mode = [] {
-        const char* e = std::getenv("STORMCK_POINTER_RING");
+        const char* e = STORMCK_KNOB("STORMCK_POINTER_RING");
         return e ? std::atoi(e) : 2;
     }();
     if (ring_mode != 0 && fanout == STORMCK_POINTERS_PER_BLOCK) {
@@ -1323,11 +1550,11 @@ int stormck_pointer_level_device(const uint64_t* d_child_cs, uint64_t m, uint64_
         // STORMCK_POINTER_SIMD=0 takes roles by wave index.
         constexpr uint32_t F = STORMCK_POINTERS_PER_BLOCK;
         static const int fixed_c = [] {
-            const char* e = std::getenv("STORMCK_POINTER_C");
+            const char* e = STORMCK_KNOB("STORMCK_POINTER_C");
             return e ? std::atoi(e) : 1;
         }();
         static const bool simd_roles = [] {
-            const char* e = std::getenv("STORMCK_POINTER_SIMD");
+            const char* e = STORMCK_KNOB("STORMCK_POINTER_SIMD");
             return !(e && e[0] == '0');
         }();
         const uint64_t chains = (pm + 15) / 16, ncu = cu_count() ? cu_count() : 256;
@@ -1340,9 +1567,14 @@ int stormck_pointer_level_device(const uint64_t* d_child_cs, uint64_t m, uint64_
 #define STORMCK_PC(C, SR)                                                                                       \
     hipLaunchKernelGGL((k_pointer_level_pc<F, kRingTile, kRingPrefetch, C, SR>), grid, dim3(128 * C), 0, st, \
                        d_child_cs, m, child_addr_base, rev, child_type, d_parent_cs)
-        if (c == 1) STORMCK_PC(1, false);  // one chain wave: its producer cannot take its SIMD
-        else if (c == 2) { if (simd_roles) STORMCK_PC(2, true); else STORMCK_PC(2, false); }
-        else { if (simd_roles) STORMCK_PC(4, true); else STORMCK_PC(4, false); }
+#ifdef STORMCK_PROBES  // 2 or 4 chain waves per workgroup (rejected)
+        if (c == 2) { if (simd_roles) STORMCK_PC(2, true); else STORMCK_PC(2, false); }
+        else if (c == 4) { if (simd_roles) STORMCK_PC(4, true); else STORMCK_PC(4, false); }
+        else
+#else
+        (void)simd_roles;
+#endif
+        STORMCK_PC(1, false);  // one chain wave: its producer cannot take its SIMD
 #undef STORMCK_PC
         HIP_TRY(hipGetLastError());
         return STORMCK_OK;
@@ -1803,14 +2035,14 @@ int stormck_commit_device(void* d_arena, stormck_dirty_block* blocks, uint64_t n
 
     hipStream_t st = static_cast<hipStream_t>(stream);
     uint64_t commit_wide = kCommitWide;
-    if (const char* e = std::getenv("STORMCK_COMMIT_WIDE")) commit_wide = std::strtoull(e, nullptr, 10);  // probe knob
+    if (const char* e = STORMCK_KNOB("STORMCK_COMMIT_WIDE")) commit_wide = std::strtoull(e, nullptr, 10);  // probe knob
     static const bool commit_multi = [] {
-        const char* e = std::getenv("STORMCK_COMMIT_MULTI");  // probe knob: "0" disables
+        const char* e = STORMCK_KNOB("STORMCK_COMMIT_MULTI");  // probe knob: "0" disables
         return !(e && e[0] == '0');
     }();
     const uint64_t ncu = cu_count();
     static const bool commit_midw = [] {  // probe knob STORMCK_COMMIT_MIDW=0: the launches before (A/B)
-        const char* e = std::getenv("STORMCK_COMMIT_MIDW");
+        const char* e = STORMCK_KNOB("STORMCK_COMMIT_MIDW");
         return !(e && e[0] == '0');
     }();
     auto launch_level = [&](uint64_t lo, uint64_t cnt) -> int {
@@ -1841,24 +2073,27 @@ int stormck_commit_device(void* d_arena, stormck_dirty_block* blocks, uint64_t n
             const uint64_t bpw = multi_bpw(cnt, ncu);
             const dim3 grid(static_cast<unsigned>((cnt + bpw - 1) / bpw));
             const uint32_t ring_slots = pipe_staging();
-            uint32_t* fault = nullptr;
+            uint32_t* fault = nullptr;  // the fault slot of the commit's stream
             if (ring_slots) {
-                const int frc = fault_word(&fault);
+                const int frc = fault_slot(st, &fault);
                 if (frc) return frc;
             }
-            const uint32_t stall = debug_stall();
+            const uint32_t stall = debug_stall(st);
+#ifdef STORMCK_PROBES  // the rejected 16-block / whole-block-staging variants
             if (ring_slots && bpw == kMultiBpwWide)
                 hipLaunchKernelGGL((k_commit_level_multi<kMultiBpwWide, kRingSlots, kChunkPiecesWide, true>), grid,
                                    dim3(kThreads), 0, st, static_cast<uint8_t*>(d_arena), d_blocks, lo, cnt, d_cs,
                                    fault, stall);
-            else if (ring_slots && bpw == kMultiBpw)
-                hipLaunchKernelGGL((k_commit_level_multi<kMultiBpw, kRingSlots>), grid, dim3(kThreads), 0, st,
-                                   static_cast<uint8_t*>(d_arena), d_blocks, lo, cnt, d_cs, fault, stall);
-            else if (ring_slots)
-                hipLaunchKernelGGL((k_commit_level_multi<kMultiBpwRing, kRingSlots>), grid, dim3(kThreads), 0, st,
+            else if (!ring_slots)
+                hipLaunchKernelGGL((k_commit_level_multi<kMultiBpw, 0>), grid, dim3(kThreads), 0, st,
                                    static_cast<uint8_t*>(d_arena), d_blocks, lo, cnt, d_cs, fault, stall);
             else
-                hipLaunchKernelGGL((k_commit_level_multi<kMultiBpw, 0>), grid, dim3(kThreads), 0, st,
+#endif
+            if (bpw == kMultiBpw)
+                hipLaunchKernelGGL((k_commit_level_multi<kMultiBpw, kRingSlots>), grid, dim3(kThreads), 0, st,
+                                   static_cast<uint8_t*>(d_arena), d_blocks, lo, cnt, d_cs, fault, stall);
+            else
+                hipLaunchKernelGGL((k_commit_level_multi<kMultiBpwRing, kRingSlots>), grid, dim3(kThreads), 0, st,
                                    static_cast<uint8_t*>(d_arena), d_blocks, lo, cnt, d_cs, fault, stall);
         } else {
             dim3 grid;
@@ -1926,7 +2161,7 @@ int stormck_commit_device(void* d_arena, stormck_dirty_block* blocks, uint64_t n
         // the previous, small enough that its records (56 B per block over PCIe) arrive
         // before the previous chunk's blocks (~32 KiB each at HBM rate) are hashed.
         uint64_t next = 2 * kStreamBatch, growth = 3;
-        if (const char* e = std::getenv("STORMCK_COMMIT_CHUNKS")) {  // tuning probe: "first,growth"
+        if (const char* e = STORMCK_KNOB("STORMCK_COMMIT_CHUNKS")) {  // tuning probe: "first,growth"
             unsigned long long f = 0, gr = 0;
             if (std::sscanf(e, "%llu,%llu", &f, &gr) == 2 && f >= 1 && gr >= 1) {
                 next = f;
@@ -2032,7 +2267,7 @@ int stormck_commit_device(void* d_arena, stormck_dirty_block* blocks, uint64_t n
                 rc = fail(STORMCK_EHIP, "commit: checksum copy-back failed");
                 break;
             }
-            rc = take_fault(c->device);  // a stalled ring level wrote no checksum for some blocks
+            rc = take_fault(c->device, st);  // a stalled ring level wrote no checksum for some blocks
             if (rc) break;
             const unsigned tn = static_cast<unsigned>(std::min<uint64_t>({8, fj.size(), x.cnt / 65536 + 1}));
             fj.run(tn, [&](unsigned t) {
@@ -2049,7 +2284,7 @@ int stormck_commit_device(void* d_arena, stormck_dirty_block* blocks, uint64_t n
     const hipError_t s1 = hipStreamSynchronize(st);
     for (Back& x : back) (void)hipEventDestroy(x.hashed);
     if (rc == STORMCK_OK && s1 != hipSuccess) rc = fail(STORMCK_EHIP, std::string("commit: ") + hipGetErrorString(s1));
-    if (rc == STORMCK_OK) rc = take_fault(c->device);
+    if (rc == STORMCK_OK) rc = take_fault(c->device, st);
     pt.mark("device");
     return rc;
 }

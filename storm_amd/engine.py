@@ -16,19 +16,54 @@ from ._lib import check, lib
 POINTERS_PER_BLOCK = 1200  # blocks/pointer/params.go:6
 
 
+# Batches the library may give to a ring-staged kernel (k_xxh64_wide_multi, whose
+# bounded waits report a stall in the stream's fault slot rather than in the output):
+# more than kWideBatch (128) blocks and at most kMultiBpwRing (8) per CU
+# (storm_amd/csrc/stormck.hip multi_bpw).
+_RING_MIN_EXCLUSIVE, _RING_PER_CU = 128, 8
+_cus = {}
+
+
+def _cu_count() -> int:
+    import torch
+    d = torch.cuda.current_device()
+    if d not in _cus:
+        _cus[d] = torch.cuda.get_device_properties(d).multi_processor_count
+    return _cus[d]
+
+
+def may_ring(n: int) -> bool:
+    """Whether a batch of n blocks can take a ring-staged kernel on the current device."""
+    return _RING_MIN_EXCLUSIVE < n <= _RING_PER_CU * _cu_count()
+
+
+def _after_launch(n: int, stream: int, check_status) -> None:
+    # check_status: True = synchronise `stream` and raise on a ring fault of this stream
+    # (stormck_device_status); None = do so when the batch could have taken a ring kernel;
+    # False = the caller checks (device_status) itself, e.g. after a series of launches.
+    if check_status or (check_status is None and may_ring(n)):
+        device_status(stream)
+
+
 def checksum_device(d_base: int, stride: int, n: int, d_out: int, length: int = 0, d_lens: int = 0,
-                    stream: int = 0) -> None:
+                    stream: int = 0, check_status=None) -> None:
     check(lib.stormck_checksum_device(d_base, stride, d_lens or None, length, n, d_out, stream or None))
+    _after_launch(n, stream, check_status)
 
 
 def checksum_gather_device(d_base: int, d_offsets: int, n: int, d_out: int, length: int = 0, d_lens: int = 0,
-                           stream: int = 0) -> None:
+                           stream: int = 0, check_status=None) -> None:
     check(lib.stormck_checksum_gather_device(d_base, d_offsets, d_lens or None, length, n, d_out, stream or None))
+    _after_launch(n, stream, check_status)
 
 
 def verify_device(d_base: int, stride: int, n: int, d_expected: int, d_result: int, length: int = 0, d_lens: int = 0,
-                  stream: int = 0) -> None:
+                  stream: int = 0, check_status=None) -> None:
+    """Batched VerifyChecksum into d_result = {first_bad, n_bad}. A stalled ring
+    workgroup counts its blocks as mismatches (fails closed); the status check also
+    raises on it."""
     check(lib.stormck_verify_device(d_base, stride, d_lens or None, length, n, d_expected, d_result, stream or None))
+    _after_launch(n, stream, check_status)
 
 
 def key_tags_device(d_keys: int, n: int, d_out: int, stride: int = 0, length: int = 0, d_offsets: int = 0,
@@ -102,6 +137,15 @@ def device_alloc(nbytes: int) -> int:
     return int(p.value)
 
 
+def device_alloc_placed(nbytes: int, mode: int, chunk_bytes: int = 0) -> Tuple[int, int]:
+    """A block arena in placement `mode` (_lib.ALLOC_PLAIN / ALLOC_VMM / ALLOC_CONTIGUOUS);
+    returns (device pointer, physical chunk bytes of a VMM arena, else 0)."""
+    import ctypes
+    p, ch = ctypes.c_void_p(), ctypes.c_uint64(0)
+    check(lib.stormck_device_alloc_placed(nbytes, mode, chunk_bytes, ctypes.byref(p), ctypes.byref(ch)))
+    return int(p.value), int(ch.value)
+
+
 def device_free(d_ptr: int) -> None:
     check(lib.stormck_device_free(d_ptr or None))
 
@@ -124,10 +168,12 @@ def _stream_of(t) -> int:
     return torch.cuda.current_stream(t.device).cuda_stream
 
 
-def checksum_tensor(blocks, length: Optional[int] = None, lens=None, out=None):
+def checksum_tensor(blocks, length: Optional[int] = None, lens=None, out=None, check_status=None):
     """Checksums of a device tensor of blocks, shape [n, stride] uint8 (row i =
     block i; ``length`` bytes of each row, default the full row, or ``lens[i]``).
-    Returns an int64 tensor [n] (bit pattern of the uint64 checksums)."""
+    Returns an int64 tensor [n] (bit pattern of the uint64 checksums). A batch that
+    could take a ring kernel is followed by a status check of the stream unless
+    ``check_status`` is False (checksum_device)."""
     torch = _torch()
     if blocks.dim() != 2 or blocks.dtype != torch.uint8 or not blocks.is_cuda:
         raise ValueError("blocks must be a 2-D uint8 CUDA tensor [n, stride]")
@@ -149,7 +195,8 @@ def checksum_tensor(blocks, length: Optional[int] = None, lens=None, out=None):
         length = width
     elif length > width:
         raise ValueError("length exceeds the row width")
-    checksum_device(blocks.data_ptr(), stride, n, out.data_ptr(), length, d_lens, _stream_of(blocks))
+    checksum_device(blocks.data_ptr(), stride, n, out.data_ptr(), length, d_lens, _stream_of(blocks),
+                    check_status=check_status)
     return out
 
 

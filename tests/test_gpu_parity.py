@@ -593,11 +593,12 @@ def test_pointer_level_ring_kernel(dev, m):
                                    {"STORMCK_POINTER_C": "4"}, {"STORMCK_POINTER_C": "4", "STORMCK_POINTER_SIMD": "0"},
                                    {"STORMCK_POINTER_C": "0"}])
 def test_pointer_level_probe_kernels(dev, knobs):
-    """The Merkle level kernels behind probe knobs (read once per process, so each runs
-    in a child): the 1-wave ring (STORMCK_POINTER_RING=1), 2 and 4 chain waves per
+    """The Merkle level kernels behind probe knobs, which only the probe build
+    (tools/libstormck_probes.so, -DSTORMCK_PROBES) has; each runs in a child that loads
+    it (STORMCK_LIBRARY): the ring mode knob (STORMCK_POINTER_RING=1), 2 and 4 chain waves per
     workgroup with SIMD-ranked roles (pc_role<true>) or by wave index, and the C chosen
     per level (0). Ragged 13,982-, 6,991- and 300-node levels (the c3 and c4 shard
-    levels); every node equal to the default kernel's in this process."""
+    levels); every node equal to the product library's default kernel in this process."""
     import subprocess
     import sys
     from oracle import oracle as o
@@ -623,7 +624,9 @@ def test_pointer_level_probe_kernels(dev, knobs):
             f"    engine.pointer_level_device(d.data_ptr(), m, {base}, {rev}, 2, 1200, par.data_ptr())\n"
             "    torch.cuda.synchronize()\n"
             "    np.save(sys.stdout.buffer, par.cpu().numpy().view(np.uint64))\n")
-    env = dict(os.environ, **knobs)
+    from storm_amd import build as sb
+    assert os.path.exists(sb.PROBES_LIB), "probe build missing: storm_amd.build.build_probes_lib()"
+    env = dict(os.environ, STORMCK_LIBRARY=sb.PROBES_LIB, **knobs)
     r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, capture_output=True, env=env, timeout=300)
     assert r.returncode == 0, r.stderr[-2000:]
     import io

@@ -17,6 +17,7 @@ rp = r.get("measured_read_peak") or {}
 out = {"log": log, "kernel": r["kernel"], "frac": r["frac"], "avg_ms": r["avg_launch_ms"],
        "min_ms": r["launch_ms"]["min"], "max_ms": r["launch_ms"]["max"],
        "va": d["config"]["arena"]["va"], "va_align": d["config"]["arena"]["va_alignment"],
+       "alloc": d["config"]["arena"].get("mode", "plain"), "mapped_chunk": d["config"]["arena"].get("mapped_chunk"),
        "read_peak_frac": rp.get("frac"), "root_check": d["root_check"]}
 if len(sys.argv) > 2:
     stats = glob.glob(sys.argv[2] + "/**/*kernel_stats.csv", recursive=True)
