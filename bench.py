@@ -71,7 +71,7 @@ def parse():
     p.add_argument("--gather-order", default="shuffled", choices=["shuffled", "sequential"],
                    help="gather workload: slot order (storm's cache slots are spread by addressingOffsets)")
     p.add_argument("--gather-lens", type=int, default=0, help="gather workload: one length for every block (A/B)")
-    p.add_argument("--workload", default="c3", choices=["c3", "commit", "keytags", "c5", "gather"],
+    p.add_argument("--workload", default="c3", choices=["c3", "commit", "keytags", "c5", "gather", "commit_e2e"],
                    help="c3 = BASELINE metric (default); commit = f1 level-synchronous Cache.Commit of a dirty "
                         "forest; keytags = f4 xxhash.Sum64 of 48-byte keys")
     p.add_argument("--commit-leaves", type=int, default=1 << 20)
@@ -363,6 +363,126 @@ def c5_workload(a):
     return rc
 
 
+def commit_e2e_workload(a):
+    """f1 end to end from host memory, in the Go binding's configuration: storm's
+    cache.data as page-aligned registered host memory (integration/go/cache/
+    commit_stormck.go newArena), each dirty forest committed by
+      dev_inplace  stormck_commit_device on the arena in place (the kernels read the
+                   blocks and write the parents' Pointers over PCIe),
+      host_1       stormck_commit_host on 1 thread (storm's serial loop: one XXH64 per
+                   block, children first),
+      host_all     stormck_commit_host on every usable thread,
+      routed       stormck_commit (the library's choice between the two),
+    and, for reference, dev_hbm: the same forest with cache.data in HBM (device-resident,
+    the north-star configuration). Forests: storm's c5 commits (BenchmarkKeyStore's
+    1,200 objectlist leaves, BenchmarkStorm's 1,200 blob leaves, each under one pointer
+    block, keystore/benchmark_test.go:58-62, benchmark_test.go), the smallest real
+    commit (2 leaves + their pointer block), a `-tags test` forest (100 leaves of 536 /
+    728 B under fan-out-10 pointer blocks of 256 B, storm_test.go:131-138), and larger
+    forests of 16K and 128K leaves. Every leg's checksums must agree. One line per run
+    with a table (median us per commit over --steps reps)."""
+    import ctypes
+    import numpy as np
+    import torch
+    from storm_amd import _lib
+    from storm_amd import commit as sc
+    from storm_amd import engine
+
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    engine.init(0)
+    L = _lib.lib
+    shapes = [
+        ("c5_keystore", 1200, 31808, FANOUT),
+        ("c5_storm", 1200, 32768, FANOUT),
+        ("three_blocks", 2, 31808, FANOUT),
+        ("test_tag", 100, np.array([536, 728] * 50, dtype=np.uint32), 10),
+        ("leaves_16k", 16384, 32768, FANOUT),
+        ("leaves_128k", 131072, 32768, FANOUT),
+    ]
+    threads = host_cpu_info()["usable_cpus"]
+    reps = max(3, a.steps)
+    rows = []
+    for name, nl, lens, fan in shapes:
+        b0, size, last = sc.pointer_forest(nl, lens, fan, slot=BLOCK, revision=REV)
+        pages = (size + 4095) // 4096 * 4096
+        raw = np.zeros(pages + 4096, dtype=np.uint8)
+        off = (-raw.ctypes.data) % 4096
+        arena = raw[off:off + pages]
+        arena[BLOCK:BLOCK + nl * BLOCK] = engine_fill_host(nl, BLOCK)
+        _lib.check(L.stormck_host_register(arena.ctypes.data, arena.nbytes))
+        d_host = ctypes.c_void_p()
+        _lib.check(L.stormck_host_device_pointer(arena.ctypes.data, ctypes.byref(d_host)))
+        hbm = torch.from_numpy(arena).to(dev)
+        torch.cuda.synchronize()
+        bytes_hashed = int(b0["length"].sum())
+        outs = {}
+
+        def run(leg):
+            b = b0.copy()
+            out = np.zeros(len(b), dtype=np.uint64)
+            la = ctypes.c_uint64(last)
+            bp, op = b.ctypes.data, out.ctypes.data
+            t0 = time.perf_counter()
+            if leg == "dev_inplace":
+                rc = L.stormck_commit_device(d_host.value, bp, len(b), REV, ctypes.byref(la), op, None)
+            elif leg == "dev_hbm":
+                rc = L.stormck_commit_device(hbm.data_ptr(), bp, len(b), REV, ctypes.byref(la), op, None)
+            elif leg == "host_1":
+                rc = L.stormck_commit_host(arena.ctypes.data, bp, len(b), REV, ctypes.byref(la), op, 1)
+            elif leg == "host_all":
+                rc = L.stormck_commit_host(arena.ctypes.data, bp, len(b), REV, ctypes.byref(la), op, threads)
+            else:
+                used = ctypes.c_uint32(9)
+                rc = L.stormck_commit(arena.ctypes.data, bp, len(b), REV, ctypes.byref(la), op, None, 0,
+                                      ctypes.byref(used))
+                outs["routed_leg"] = int(used.value)
+            dt = time.perf_counter() - t0
+            _lib.check(rc)
+            return dt, out
+
+        row = {"forest": name, "blocks": int(len(b0)), "leaves": nl, "hashed_bytes": bytes_hashed}
+        for leg in ("dev_inplace", "dev_hbm", "host_1", "host_all", "routed"):
+            n_reps = reps if not (leg == "host_1" and bytes_hashed > (1 << 30)) else 3
+            for _ in range(2):
+                run(leg)
+            ts = []
+            for _ in range(n_reps):
+                dt, out = run(leg)
+                ts.append(dt)
+            ts.sort()
+            med = ts[len(ts) // 2]
+            row[leg + "_us"] = round(med * 1e6, 1)
+            row[leg + "_GiBps"] = round(bytes_hashed / med / 2**30, 2)
+            outs[leg] = out
+        row["routed_leg"] = {1: "host", 2: "device"}.get(outs.get("routed_leg"), outs.get("routed_leg"))
+        row["agree"] = all(np.array_equal(outs["host_1"], outs[k]) for k in
+                           ("dev_inplace", "dev_hbm", "host_all", "routed"))
+        rows.append(row)
+        print(json.dumps(row), flush=True)
+        del hbm
+        _lib.check(L.stormck_host_unregister(arena.ctypes.data))
+        del raw, arena
+    res = {"metric": "us per storm Cache.Commit data phase from host memory (f1 E2E), by leg",
+           "value": rows[0]["routed_us"], "unit": "us", "n_gpus": 1, "steps": reps, "warmup": 2,
+           "higher_is_better": False, "scaling": "weak", "vs_baseline": None, "dtype": "u64", "data": "synthetic",
+           "config": {"workload": "f1 commit E2E, cache.data registered host memory; value = routed c5_keystore",
+                      "host_threads": threads, "host": host_cpu_info()},
+           "table": rows}
+    print(json.dumps(res), flush=True)
+    return 0 if all(r["agree"] for r in rows) else 3
+
+
+def engine_fill_host(n: int, stride: int):
+    """n synthetic blocks (SURVEY §8d generator) as host bytes: the library's device
+    generator, copied back."""
+    import torch
+    from storm_amd import engine
+    t = torch.empty((n, stride), dtype=torch.uint8, device="cuda")
+    engine.fill_synthetic_device(t.data_ptr(), stride, n, 0, SYNTH_SEED)
+    return t.cpu().numpy().reshape(-1)
+
+
 def gather_workload(a):
     """storm's batch shape on the LDS-DMA ring: 4M dirty blocks gathered from a 4M-slot
     arena of 32 KiB slots (cache.data, cache/cache.go:36-40) in a shuffled slot order,
@@ -629,6 +749,8 @@ def main():
         rc = c5_workload(a)
     elif a.workload == "gather":
         rc = gather_workload(a)
+    elif a.workload == "commit_e2e":
+        rc = commit_e2e_workload(a)
     else:
         rc = block_checksum_workload(a)
     if rc:

@@ -88,6 +88,9 @@ void stormck_shutdown(void);
  * concurrent callers on distinct streams see only their own (the legacy null stream is
  * one stream, shared by every thread of the device). The slots are allocated by
  * stormck_init; a first ring launch inside a stream capture without it is STORMCK_EINVAL.
+ * A ring launch captured into a graph reports into the slot of the stream it was
+ * captured on, so check that stream after replays (status on a stream that is being
+ * captured is STORMCK_EINVAL).
  * Up to 1024 streams per device have a slot of their own at once; past that the least
  * recently launched stream with no pending fault gives its slot up. */
 int stormck_device_status(void* stream);
@@ -282,6 +285,29 @@ typedef struct stormck_dirty_block {
  * then still matches the relocations already written into blocks. */
 int stormck_commit_device(void* d_arena, stormck_dirty_block* blocks, uint64_t n, uint64_t revision,
                           uint64_t* last_allocated_block, uint64_t* out_checksums, void* stream);
+
+/* The same commit on host threads (the "host leg"): identical rules, order, relocation,
+ * stores, outputs and errors as stormck_commit_device, with `arena` a HOST pointer
+ * (storm's cache.data) and the blocks of one height hashed on `threads` library pool
+ * threads (0 = all of the pool, at most 16; 1 = storm's serial loop). Needs no device:
+ * it is the leg stormck_commit picks for forests too small to repay a launch per height
+ * and the link. */
+int stormck_commit_host(void* arena, stormck_dirty_block* blocks, uint64_t n, uint64_t revision,
+                        uint64_t* last_allocated_block, uint64_t* out_checksums, uint32_t threads);
+/* Cache.Commit's data phase as storm's cache calls it (the Go binding's CommitBatch):
+ * `arena` is cache.data. An HBM arena (stormck_device_alloc) is committed by
+ * stormck_commit_device. A host arena registered with stormck_host_register is committed
+ * by whichever leg the library's measured cost model predicts is
+ * faster for this forest: the device leg in place over the link, or the host leg on
+ * host_threads threads (0 = the pool). An unregistered host arena is out of the device's
+ * reach and takes the host leg. *leg_used (optional) = STORMCK_LEG_HOST / _DEVICE.
+ * Needs a gfx950 device like every batched entry point (STORMCK_ENODEV without one). */
+#define STORMCK_LEG_NONE 0u
+#define STORMCK_LEG_HOST 1u
+#define STORMCK_LEG_DEVICE 2u
+int stormck_commit(void* arena, stormck_dirty_block* blocks, uint64_t n, uint64_t revision,
+                   uint64_t* last_allocated_block, uint64_t* out_checksums, void* stream, uint32_t host_threads,
+                   uint32_t* leg_used);
 
 /* ---- synthetic data (benchmarks / tests) -----------------------------------
  * Word w of block i = splitmix64(seed ^ (((first + i) << 20) + w)), w < stride/8,

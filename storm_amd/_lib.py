@@ -26,6 +26,7 @@ EMISMATCH = -5
 ALLOC_PLAIN = 0       # STORMCK_ALLOC_* (include/stormck.h): arena placement modes
 ALLOC_VMM = 1
 ALLOC_CONTIGUOUS = 2
+LEG_NONE, LEG_HOST, LEG_DEVICE = 0, 1, 2  # STORMCK_LEG_* (stormck_commit)
 
 
 class StormckError(RuntimeError):
@@ -84,6 +85,9 @@ SIGNATURES = {
         c_int, [c_int, c_void_p, c_void_p, c_uint64, c_uint64, c_void_p, c_uint64, c_void_p, c_uint32, c_void_p, c_void_p]),
     "stormck_key_tags_device": (c_int, [c_void_p, c_uint64, c_void_p, c_void_p, c_uint32, c_uint64, c_void_p, c_void_p]),
     "stormck_commit_device": (c_int, [c_void_p, c_void_p, c_uint64, c_uint64, POINTER(c_uint64), c_void_p, c_void_p]),
+    "stormck_commit_host": (c_int, [c_void_p, c_void_p, c_uint64, c_uint64, POINTER(c_uint64), c_void_p, c_uint32]),
+    "stormck_commit": (
+        c_int, [c_void_p, c_void_p, c_uint64, c_uint64, POINTER(c_uint64), c_void_p, c_void_p, c_uint32, POINTER(c_uint32)]),
     "stormck_fill_synthetic_device": (c_int, [c_void_p, c_uint64, c_uint64, c_uint64, c_uint64, c_void_p]),
 }
 

@@ -59,6 +59,48 @@ def commit_device(d_arena: int, blocks: np.ndarray, revision: int, last_allocate
     return out, la.value
 
 
+def commit_host(arena: np.ndarray, blocks: np.ndarray, revision: int, last_allocated: int, threads: int = 0,
+                out: Optional[np.ndarray] = None) -> Tuple[np.ndarray, int]:
+    """The host leg (stormck_commit_host) on a host uint8 arena: the same commit on
+    `threads` library pool threads (0 = the pool, 1 = storm's serial loop)."""
+    _check_blocks(blocks)
+    if arena.dtype != np.uint8 or not arena.flags["C_CONTIGUOUS"]:
+        raise ValueError("arena must be a contiguous uint8 array")
+    n = blocks.shape[0]
+    out = _out(out, n)
+    la = ctypes.c_uint64(last_allocated)
+    _lib.check(_lib.lib.stormck_commit_host(arena.ctypes.data, blocks.ctypes.data if n else None, n, revision,
+                                            ctypes.byref(la), out.ctypes.data if n else None, threads))
+    return out, la.value
+
+
+def commit(arena_ptr: int, blocks: np.ndarray, revision: int, last_allocated: int, stream: int = 0,
+           host_threads: int = 0, out: Optional[np.ndarray] = None) -> Tuple[np.ndarray, int, int]:
+    """The routed commit (stormck_commit): an HBM arena takes the device leg, a registered
+    host arena the leg the library's cost model picks, an unregistered one the host leg.
+    Returns (checksums, new last_allocated_block, leg: _lib.LEG_HOST / LEG_DEVICE)."""
+    _check_blocks(blocks)
+    n = blocks.shape[0]
+    out = _out(out, n)
+    la, leg = ctypes.c_uint64(last_allocated), ctypes.c_uint32(0)
+    _lib.check(_lib.lib.stormck_commit(arena_ptr, blocks.ctypes.data if n else None, n, revision, ctypes.byref(la),
+                                       out.ctypes.data if n else None, stream or None, host_threads, ctypes.byref(leg)))
+    return out, la.value, leg.value
+
+
+def _check_blocks(blocks: np.ndarray) -> None:
+    if blocks.dtype != DIRTY_DTYPE or not blocks.flags["C_CONTIGUOUS"]:
+        raise ValueError("blocks must be a contiguous DIRTY_DTYPE array")
+
+
+def _out(out: Optional[np.ndarray], n: int) -> np.ndarray:
+    if out is None:
+        return np.zeros(n, dtype=np.uint64)
+    if out.dtype != np.uint64 or out.shape != (n,) or not out.flags["C_CONTIGUOUS"]:
+        raise ValueError("out must be a contiguous uint64 array of len(blocks)")
+    return out
+
+
 def pointer_forest(n_leaves: int, leaf_lens, fanout: int, slot: int = 32768, revision: int = 1,
                    existing: Optional[np.ndarray] = None, first_address: int = 1) -> Tuple[np.ndarray, int, int]:
     """Dirty forest of `n_leaves` leaves under pointer blocks of `fanout`, rooted at the

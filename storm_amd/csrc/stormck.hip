@@ -1241,6 +1241,10 @@ int stormck_device_status(void* stream) {
     if (rc) return rc;
     int dev = 0;
     HIP_TRY(hipGetDevice(&dev));
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(static_cast<hipStream_t>(stream), &cap) != hipSuccess) (void)hipGetLastError();
+    if (cap != hipStreamCaptureStatusNone)
+        return fail(STORMCK_EINVAL, "stream is being captured: check its status after launching the graph");
     HIP_TRY(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
     return take_fault(dev, static_cast<hipStream_t>(stream));
 }
@@ -2287,6 +2291,190 @@ int stormck_commit_device(void* d_arena, stormck_dirty_block* blocks, uint64_t n
     if (rc == STORMCK_OK) rc = take_fault(c->device, st);
     pt.mark("device");
     return rc;
+}
+
+// ---- f1, host leg --------------------------------------------------------------
+// The same commit on host threads: what storm's own loop costs (commitData hashes one
+// block at a time on its goroutine, cache/cache.go:87-137), with the blocks of one height
+// spread over `threads` pool threads. The level-synchronous device commit pays a launch
+// and a chain per height (~20 us) and, on storm's host-resident cache.data, the PCIe
+// link for every byte; small forests are cheaper here (stormck_commit routes by the
+// measured crossover, DESIGN.md §11 f1 "End to end from host memory").
+int stormck_commit_host(void* arena, stormck_dirty_block* blocks, uint64_t n, uint64_t revision,
+                        uint64_t* last_allocated_block, uint64_t* out_checksums, uint32_t threads) {
+    if (n == 0) return STORMCK_OK;
+    if (!arena || !blocks || !last_allocated_block || !out_checksums) return fail(STORMCK_EINVAL, "null argument");
+    if (n > 0xffffffffULL) return fail(STORMCK_EINVAL, "more than 2^32 dirty blocks");
+    // validation and heights, with stormck_commit_device's rules and messages
+    std::vector<uint32_t> height(n, 0);
+    for (uint64_t i = 0; i < n; ++i) {
+        const stormck_dirty_block& b = blocks[i];
+        if (b.parent != STORMCK_NO_PARENT && (b.parent < 0 || static_cast<uint64_t>(b.parent) >= n))
+            return fail(STORMCK_EINVAL, "parent index out of range");
+        if (b.origin_pointer != STORMCK_NO_ORIGIN && (b.origin_pointer & 7) != 0)
+            return fail(STORMCK_EINVAL, "origin_pointer must be 8-byte aligned (Go blocks.Pointer alignment)");
+    }
+    uint32_t max_h = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        uint64_t cur = i;
+        uint32_t hh = 0;
+        while (blocks[cur].parent != STORMCK_NO_PARENT) {
+            cur = static_cast<uint64_t>(blocks[cur].parent);
+            if (++hh > n) return fail(STORMCK_EINVAL, "parent links form a cycle");
+            if (height[cur] >= hh) break;  // an earlier walk carries it upward
+            height[cur] = hh;
+            max_h = std::max(max_h, hh);
+        }
+    }
+    // commit order: by height, index order within a height (stormck_commit_device's)
+    std::vector<uint64_t> start(static_cast<size_t>(max_h) + 2, 0);
+    for (uint64_t i = 0; i < n; ++i) start[height[i] + 1]++;
+    if (start[1] == 0) return fail(STORMCK_EINVAL, "parent links form a cycle");
+    for (uint32_t l = 0; l <= max_h; ++l) start[l + 1] += start[l];
+    std::vector<uint32_t> order(n);
+    {
+        std::vector<uint64_t> pos(start.begin(), start.end() - 1);
+        for (uint64_t i = 0; i < n; ++i) order[pos[height[i]]++] = static_cast<uint32_t>(i);
+    }
+    // relocation in commit order (cache/cache.go:114-118)
+    uint64_t last = *last_allocated_block;
+    for (uint64_t k = 0; k < n; ++k) {
+        stormck_dirty_block& b = blocks[order[k]];
+        if (b.birth_revision <= revision) {
+            b.address = ++last;
+            b.birth_revision = revision + 1;
+        }
+    }
+    *last_allocated_block = last;
+    // one height at a time; its blocks in chunks from a shared counter
+    uint8_t* a = static_cast<uint8_t*>(arena);
+    ForkJoin& fj = ForkJoin::get();
+    const unsigned nt = threads ? std::min<unsigned>(threads, fj.size()) : fj.size();
+    for (uint32_t l = 0; l <= max_h; ++l) {
+        const uint64_t lo = start[l], cnt = start[l + 1] - lo;
+        const uint64_t chunk = std::max<uint64_t>(1, cnt / (uint64_t{nt} * 8));
+        std::atomic<uint64_t> next{0};
+        auto work = [&](unsigned) {
+            for (;;) {
+                const uint64_t k0 = next.fetch_add(chunk, std::memory_order_relaxed);
+                if (k0 >= cnt) return;
+                for (uint64_t k = k0; k < std::min(cnt, k0 + chunk); ++k) {
+                    const uint64_t i = order[lo + k];
+                    const stormck_dirty_block& b = blocks[i];
+                    const uint64_t h = host::xxh64(a + b.data_offset, b.length);
+                    out_checksums[i] = h;
+                    if (b.origin_pointer != STORMCK_NO_ORIGIN) {
+                        const uint64_t ptr[3] = {h, b.address, b.birth_revision};
+                        std::memcpy(a + b.origin_pointer, ptr, sizeof ptr);
+                        a[b.origin_type] = b.type;
+                    }
+                }
+            }
+        };
+        fj.run(static_cast<unsigned>(std::min<uint64_t>(nt, (cnt + chunk - 1) / chunk)), work);
+    }
+    return STORMCK_OK;
+}
+
+// ---- f1, the routed commit --------------------------------------------------------
+// Cost model of the two legs (us), constants measured on MI355X with the arena in
+// registered host memory ("End to end from host memory",
+// profiles/r04_commit_e2e/): the host leg hashes a height's blocks on nt threads at
+// kHostCoreBytesPerUs each, plus a fork/join per height; the device leg pays a fixed
+// call cost, then per height the longer of one XXH64 chain over its longest block and
+// its bytes over the link.
+namespace {
+constexpr double kHostCoreBytesPerUs = 9000.0;   // one host thread, XXH64
+constexpr double kHostLevelUs = 4.0;
+constexpr double kDevCallUs = 30.0;
+constexpr double kDevChainBytesPerUs = 1600.0;   // one 4-lane chain on gfx950
+constexpr double kDevLevelUs = 8.0;
+constexpr double kLinkBytesPerUs = 50000.0;      // PCIe Gen5 x16, registered host memory
+}  // namespace
+
+namespace {  // cost model helpers (internal)
+
+struct CommitShape {
+    std::vector<uint64_t> cnt, bytes, longest;  // per height
+};
+
+// Heights of a dirty forest (children first); false: malformed (the legs report why).
+bool commit_shape(const stormck_dirty_block* blocks, uint64_t n, CommitShape* s) {
+    std::vector<uint32_t> height(n, 0);
+    for (uint64_t i = 0; i < n; ++i) {
+        uint64_t cur = i;
+        uint32_t hh = 0;
+        while (blocks[cur].parent != STORMCK_NO_PARENT) {
+            if (blocks[cur].parent < 0 || static_cast<uint64_t>(blocks[cur].parent) >= n || ++hh > n) return false;
+            cur = static_cast<uint64_t>(blocks[cur].parent);
+            if (height[cur] >= hh) break;
+            height[cur] = hh;
+        }
+    }
+    for (uint64_t i = 0; i < n; ++i) {
+        const uint32_t h = height[i];
+        if (h >= s->cnt.size()) {
+            s->cnt.resize(h + 1, 0);
+            s->bytes.resize(h + 1, 0);
+            s->longest.resize(h + 1, 0);
+        }
+        s->cnt[h]++;
+        s->bytes[h] += blocks[i].length;
+        s->longest[h] = std::max<uint64_t>(s->longest[h], blocks[i].length);
+    }
+    return true;
+}
+
+double host_leg_us(const CommitShape& s, unsigned nt) {
+    double t = 0;
+    for (size_t l = 0; l < s.cnt.size(); ++l) {
+        const double per_block = static_cast<double>(s.bytes[l]) / static_cast<double>(s.cnt[l]);
+        const uint64_t rounds = (s.cnt[l] + nt - 1) / nt;
+        t += std::max(static_cast<double>(rounds) * per_block, static_cast<double>(s.longest[l])) / kHostCoreBytesPerUs +
+             (nt > 1 ? kHostLevelUs : 0.0);
+    }
+    return t;
+}
+
+double device_leg_us(const CommitShape& s) {
+    double t = kDevCallUs;
+    for (size_t l = 0; l < s.cnt.size(); ++l)
+        t += kDevLevelUs + std::max(static_cast<double>(s.longest[l]) / kDevChainBytesPerUs,
+                                    static_cast<double>(s.bytes[l]) / kLinkBytesPerUs);
+    return t;
+}
+
+}  // namespace
+
+int stormck_commit(void* arena, stormck_dirty_block* blocks, uint64_t n, uint64_t revision,
+                   uint64_t* last_allocated_block, uint64_t* out_checksums, void* stream, uint32_t host_threads,
+                   uint32_t* leg_used) {
+    if (leg_used) *leg_used = STORMCK_LEG_NONE;
+    if (n == 0) return STORMCK_OK;
+    if (!arena || !blocks || !last_allocated_block || !out_checksums) return fail(STORMCK_EINVAL, "null argument");
+    int rc = device_check();  // the routed commit is the GPU engine's: no device, no commit
+    if (rc) return rc;
+    hipPointerAttribute_t attr;
+    const bool known = hipPointerGetAttributes(&attr, arena) == hipSuccess;
+    if (!known) (void)hipGetLastError();
+    if (known && attr.type == hipMemoryTypeDevice) {  // an HBM arena: only the device reaches it
+        if (leg_used) *leg_used = STORMCK_LEG_DEVICE;
+        return stormck_commit_device(arena, blocks, n, revision, last_allocated_block, out_checksums, stream);
+    }
+    const bool registered = known && (attr.type == hipMemoryTypeHost || attr.type == hipMemoryTypeManaged) &&
+                            attr.devicePointer != nullptr;
+    const unsigned nt = host_threads ? std::min<unsigned>(host_threads, ForkJoin::get().size()) : ForkJoin::get().size();
+    CommitShape shape;
+    bool device = false;
+    if (registered && commit_shape(blocks, n, &shape)) device = device_leg_us(shape) < host_leg_us(shape, nt);
+    if (!device) {  // pageable memory, a malformed forest (the host leg says why) or the cheaper leg
+        if (leg_used) *leg_used = STORMCK_LEG_HOST;
+        return stormck_commit_host(arena, blocks, n, revision, last_allocated_block, out_checksums, nt);
+    }
+    if (leg_used) *leg_used = STORMCK_LEG_DEVICE;
+    void* d_arena = nullptr;  // the kernels read and write the registered arena in place
+    HIP_TRY(hipHostGetDevicePointer(&d_arena, arena, 0));
+    return stormck_commit_device(d_arena, blocks, n, revision, last_allocated_block, out_checksums, stream);
 }
 
 int stormck_fill_synthetic_device(void* d_dst, uint64_t stride, uint64_t n, uint64_t first, uint64_t seed,

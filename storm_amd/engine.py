@@ -39,9 +39,14 @@ def may_ring(n: int) -> bool:
 
 def _after_launch(n: int, stream: int, check_status) -> None:
     # check_status: True = synchronise `stream` and raise on a ring fault of this stream
-    # (stormck_device_status); None = do so when the batch could have taken a ring kernel;
+    # (stormck_device_status); None = do so when the batch could have taken a ring kernel
+    # and the stream is not being captured into a graph (a captured launch reports into
+    # the slot of the stream it was captured on: check that stream after a replay);
     # False = the caller checks (device_status) itself, e.g. after a series of launches.
-    if check_status or (check_status is None and may_ring(n)):
+    if check_status is None:
+        import torch
+        check_status = may_ring(n) and not torch.cuda.is_current_stream_capturing()
+    if check_status:
         device_status(stream)
 
 

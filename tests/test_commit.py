@@ -64,6 +64,66 @@ def test_forest_shape():
     assert sc.DIRTY_DTYPE.itemsize == 56
 
 
+def _random_forest(n, fanout, slot, how, rng=None):
+    rng = rng or np.random.default_rng(n * 7 + fanout)
+    choices = [72, 256, 536, 728, 1000, 1024] if slot < 2048 else [72, 28808, 30000, 31808, 32768, 4097]
+    lens = rng.choice(choices, size=n)
+    b, size, last = sc.pointer_forest(n, lens, fanout, slot=slot, revision=9, first_address=100)
+    b["birth_revision"][rng.random(len(b)) < 0.4] = 3
+    arena = np.zeros(size, dtype=np.uint8)
+    arena[slot:slot + n * slot] = rng.integers(0, 256, size=n * slot, dtype=np.uint8)
+    return arrange(b, how, rng), arena, last
+
+
+@pytest.mark.parametrize("threads", [1, 0])
+def test_host_leg_matches_fixture(threads):
+    """stormck_commit_host (the host leg of the routed commit; no device needed)."""
+    g, b, arena, last = fixture_forest()
+    cs, last2 = sc.commit_host(arena, b, g["revision"], last, threads=threads)
+    assert [int(v) for v in cs] == [hx(v) for v in g["checksums"]]
+    assert [int(v) for v in b["address"]] == g["addresses"]
+    assert last2 == g["last_allocated"]
+    assert o.xxh64(arena[72:]) == hx(g["final_arena_xxh64"])
+    assert singularity_step(arena, g["revision"], last2) == hx(g["singularity_checksum"])
+
+
+@pytest.mark.parametrize("threads", [1, 3, 0])
+@pytest.mark.parametrize("how", ["shuffled", "upper_shuffled", "children_first"])
+@pytest.mark.parametrize("n,fanout,slot", [(1, 10, 1024), (11, 10, 1024), (999, 10, 1024), (1201, 1200, 32768),
+                                            (999, 10, 1032), (20000, 10, 1024)])
+def test_host_leg_random_forests(n, fanout, slot, how, threads):
+    """The host leg against storm's serial loop (the C oracle) on the device tests'
+    forests: relocations, mixed lengths, unaligned slots, any caller order."""
+    bp, arena, last = _random_forest(n, fanout, slot, how)
+    ref_arena, ref_b = arena.copy(), bp.copy()
+    want_cs, want_last = o.commit(ref_arena, ref_b, 9, last)
+    cs, last2 = sc.commit_host(arena, bp, 9, last, threads=threads)
+    assert np.array_equal(cs, want_cs)
+    assert np.array_equal(bp["address"], ref_b["address"])
+    assert np.array_equal(bp["birth_revision"], ref_b["birth_revision"])
+    assert last2 == want_last
+    assert np.array_equal(arena, ref_arena)
+
+
+def test_host_leg_argument_errors():
+    """The device leg's validation, messages and no-change-on-error rule."""
+    from storm_amd import _lib
+    b, size, last = sc.pointer_forest(25, 100, 10, slot=1024, revision=1)
+    arena = np.zeros(size, dtype=np.uint8)
+    for field, value, text in [("parent", 10 ** 6, "parent index out of range"),
+                               ("origin_pointer", 5, "8-byte aligned")]:
+        bad = b.copy()
+        bad[field][3] = value
+        keep = bad.copy()
+        with pytest.raises(_lib.StormckError, match=text):
+            sc.commit_host(arena, bad, 1, last)
+        assert np.array_equal(bad, keep)
+    cyc = b.copy()
+    cyc["parent"][28] = 3  # root -> leaf 3 -> ... -> root
+    with pytest.raises(_lib.StormckError, match="cycle"):
+        sc.commit_host(arena, cyc, 1, last)
+
+
 # ---------------------------------------------------------------------------
 torch = pytest.importorskip("torch")
 
@@ -230,3 +290,43 @@ def test_device_commit_1m_leaves_properties(dev):
     # leaves match the oracle on a sample
     host = arena[slot:slot + 64 * slot].cpu().numpy()
     assert np.array_equal(o.checksum_batch(host, 64, slot, slot), cs[:64])
+
+
+@pytest.mark.gpu
+def test_routed_commit_legs(dev):
+    """stormck_commit (the Go binding's CommitBatch): an HBM arena takes the device leg,
+    an unregistered host arena the host leg, a registered one the leg of the cost model
+    (storm's 3-block commit: host); every leg equal to storm's serial loop (the oracle)."""
+    from storm_amd import _lib, blocks
+    cases = []
+    for n, fanout, slot in [(2, 1200, 32768), (1200, 1200, 32768), (999, 10, 1024)]:
+        bp, arena, last = _random_forest(n, fanout, slot, "shuffled")
+        ref_arena, ref_b = arena.copy(), bp.copy()
+        want_cs, want_last = o.commit(ref_arena, ref_b, 9, last)
+        cases.append((bp, arena, last, ref_arena, ref_b, want_cs, want_last))
+    for kind in ("hbm", "pageable", "registered"):
+        for k, (bp0, arena0, last, ref_arena, ref_b, want_cs, want_last) in enumerate(cases):
+            bp = bp0.copy()
+            if kind == "hbm":
+                d = torch.from_numpy(arena0.copy()).to(dev)
+                cs, last2, leg = sc.commit(d.data_ptr(), bp, 9, last)
+                got = d.cpu().numpy()
+                assert leg == _lib.LEG_DEVICE
+            else:
+                raw = np.zeros(arena0.nbytes + 8192, dtype=np.uint8)
+                off = (-raw.ctypes.data) % 4096
+                host = raw[off:off + arena0.nbytes]
+                host[:] = arena0
+                if kind == "registered":
+                    blocks.RegisterHostMemory(host)
+                try:
+                    cs, last2, leg = sc.commit(host.ctypes.data, bp, 9, last)
+                finally:
+                    if kind == "registered":
+                        blocks.UnregisterHostMemory(host)
+                got = host
+                if kind == "pageable" or k == 0:
+                    assert leg == _lib.LEG_HOST, (kind, k)
+            assert np.array_equal(cs, want_cs), (kind, k)
+            assert np.array_equal(bp["address"], ref_b["address"]) and last2 == want_last
+            assert np.array_equal(got, ref_arena), (kind, k)
