@@ -73,6 +73,19 @@ def build_lib(force: bool = False) -> str:
 PROBES_LIB = os.path.join(ROOT, "tools", "libstormck_probes.so")
 
 
+# The debug build: the product dispatch with every quad merge checked for a partially
+# active quad (kernels.h quad_bcast, -DSTORMCK_DEBUG_QUAD); tests/test_quad_debug.py runs
+# the kernel families through it.
+DEBUG_LIB = os.path.join(ROOT, "tools", "libstormck_debug.so")
+
+
+def build_debug_lib(force: bool = False) -> str:
+    if not force and _newer(DEBUG_LIB, SOURCES):
+        return DEBUG_LIB
+    _compile_lib(DEBUG_LIB, ["-DSTORMCK_DEBUG_QUAD"], sources_sha() + "+debug-quad")
+    return DEBUG_LIB
+
+
 def build_probes_lib(force: bool = False) -> str:
     if not force and _newer(PROBES_LIB, SOURCES):
         return PROBES_LIB

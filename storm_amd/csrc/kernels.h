@@ -29,9 +29,25 @@ namespace stormck {
 
 typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
 
-// Broadcast lane k of each quad (DPP quad_perm) for a 64-bit value.
+#ifdef STORMCK_DEBUG_QUAD
+// Debug build (tools/libstormck_debug.so): quad merges that ran with part of their quad
+// inactive. update_dpp with bound_ctrl = false returns `old` (0) for a source lane that
+// is not in exec, so such a merge silently reads zeros ("Quad merges").
+__device__ unsigned long long g_partial_quads;
+#endif
+
+// Broadcast lane k of each quad (DPP quad_perm) for a 64-bit value. Every lane of the
+// quad must be active: a source lane outside exec reads as 0 (bound_ctrl = false, old =
+// 0). The debug build counts every merge that breaks this (g_partial_quads).
 template <int K>
 __device__ __forceinline__ uint64_t quad_bcast(uint64_t v) {
+#ifdef STORMCK_DEBUG_QUAD
+    {
+        const uint64_t exec = __builtin_amdgcn_read_exec();
+        const uint32_t quad = __lane_id() & ~3u;
+        if (((exec >> quad) & 0xFull) != 0xFull) atomicAdd(&g_partial_quads, 1ull);
+    }
+#endif
     constexpr int ctrl = K | (K << 2) | (K << 4) | (K << 6);
     const int lo = __builtin_amdgcn_update_dpp(0, static_cast<int>(static_cast<uint32_t>(v)), ctrl, 0xF, 0xF, false);
     const int hi = __builtin_amdgcn_update_dpp(0, static_cast<int>(static_cast<uint32_t>(v >> 32)), ctrl, 0xF, 0xF, false);

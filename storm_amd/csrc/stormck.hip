@@ -2490,4 +2490,41 @@ int stormck_fill_synthetic_device(void* d_dst, uint64_t stride, uint64_t n, uint
     return STORMCK_OK;
 }
 
+#ifdef STORMCK_DEBUG_QUAD
+// Debug build only (not in include/stormck.h): the partial-quad merge counter
+// (kernels.h quad_bcast), and a self-test kernel that merges with lanes 1-3 of every
+// quad inactive, so a test can see the counter move.
+__global__ void k_debug_partial_quad(uint64_t* out) {
+    const uint32_t lane = threadIdx.x & 63;
+    if ((lane & 3) == 0) out[lane / 4] = quad_bcast<1>(0x1234 + lane);
+}
+
+int stormck_debug_partial_quads(uint64_t* count, int reset) {
+    if (!count) return fail(STORMCK_EINVAL, "count is null");
+    int rc = device_check();
+    if (rc) return rc;
+    unsigned long long v = 0;
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_partial_quads), sizeof v));
+    if (reset) {
+        const unsigned long long z = 0;
+        HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_partial_quads), &z, sizeof z));
+    }
+    *count = v;
+    return STORMCK_OK;
+}
+
+int stormck_debug_partial_quad_selftest(void) {
+    int rc = device_check();
+    if (rc) return rc;
+    uint64_t* d = nullptr;
+    HIP_TRY(hipMalloc(&d, 16 * sizeof(uint64_t)));
+    hipLaunchKernelGGL(k_debug_partial_quad, dim3(1), dim3(64), 0, nullptr, d);
+    const hipError_t e = hipDeviceSynchronize();
+    (void)hipFree(d);
+    if (e != hipSuccess) return fail(STORMCK_EHIP, hipGetErrorString(e));
+    return STORMCK_OK;
+}
+#endif
+
 }  // extern "C"
