@@ -207,32 +207,46 @@ const (
 // compile-time check that DirtyBlock has the C layout (56 bytes)
 var _ = [1]struct{}{}[unsafe.Sizeof(DirtyBlock{})-56]
 
+// CommitHostThreads is the number of host threads CommitBatch's host leg may use (0 = the
+// library's pool, up to 16). It also steers the leg choice: with fewer host threads the
+// device leg wins sooner (DESIGN.md §11 f1, "End to end from host memory").
+var CommitHostThreads uint32
+
 // CommitBatch runs Cache.Commit's data phase (cache/cache.go:87-137, trace.go:274-320)
-// for every dirty block on the GPU, children first, level by level. The arena is
-// storm's cache.data, registered with RegisterHostMemory: kernels read the blocks and
-// store each {checksum, address, birth revision} and type into the parent's origin in
-// place. Relocations are written back into dirty; out[i] is dirty[i]'s checksum.
-func CommitBatch(arena []byte, dirty []DirtyBlock, revision uint64, lastAllocated *BlockAddress, out []Hash) error {
+// for every dirty block, children first, level by level, through libstormck's routed
+// commit (stormck_commit): the arena is storm's cache.data, registered with
+// RegisterHostMemory, and the library picks the faster leg for this forest from its
+// measured cost model: the GPU reading and writing the arena in place over PCIe, one
+// launch per height, or its host leg (storm's own loop, with each height's blocks spread
+// over CommitHostThreads threads when there is enough to hash). Either leg stores each
+// {checksum, address, birth revision} and type into the parent's origin in the arena.
+// Relocations are written back into dirty; out[i] is dirty[i]'s checksum; leg reports
+// the leg taken (LegHost / LegDevice).
+func CommitBatch(arena []byte, dirty []DirtyBlock, revision uint64, lastAllocated *BlockAddress, out []Hash) (leg uint32, err error) {
 	if len(dirty) == 0 {
-		return nil
+		return LegNone, nil
 	}
 	if len(out) < len(dirty) {
-		return errors.New("CommitBatch: out too small")
-	}
-	var dArena unsafe.Pointer
-	if rc := C.stormck_host_device_pointer(bytesPtr(arena), &dArena); rc != C.STORMCK_OK {
-		return stormckError(rc)
+		return LegNone, errors.New("CommitBatch: out too small")
 	}
 	la := C.uint64_t(*lastAllocated)
-	rc := C.stormck_commit_device(dArena, (*C.stormck_dirty_block)(unsafe.Pointer(&dirty[0])), C.uint64_t(len(dirty)),
-		C.uint64_t(revision), &la, (*C.uint64_t)(unsafe.Pointer(&out[0])), nil)
+	var used C.uint32_t
+	rc := C.stormck_commit(bytesPtr(arena), (*C.stormck_dirty_block)(unsafe.Pointer(&dirty[0])), C.uint64_t(len(dirty)),
+		C.uint64_t(revision), &la, (*C.uint64_t)(unsafe.Pointer(&out[0])), nil, C.uint32_t(CommitHostThreads), &used)
 	// the library reports the relocations it applied to dirty, also on a failure part-way
 	*lastAllocated = BlockAddress(la)
 	if rc != C.STORMCK_OK {
-		return stormckError(rc)
+		return uint32(used), stormckError(rc)
 	}
-	return nil
+	return uint32(used), nil
 }
+
+// Legs of CommitBatch (STORMCK_LEG_*).
+const (
+	LegNone   = uint32(C.STORMCK_LEG_NONE)
+	LegHost   = uint32(C.STORMCK_LEG_HOST)
+	LegDevice = uint32(C.STORMCK_LEG_DEVICE)
+)
 
 // UnregisterHostMemory undoes RegisterHostMemory.
 func UnregisterHostMemory(b []byte) error {

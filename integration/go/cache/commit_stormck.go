@@ -2,16 +2,19 @@
 
 package cache
 
-// Cache.Commit's data phase on the GPU. storm commits dirty blocks one at a time,
+// Cache.Commit's data phase through libstormck. storm commits dirty blocks one at a time,
 // children first (cache/cache.go:87-137): each commitBlock relocates, writes the block,
 // and runs its PostCommitFunc, which hashes it (blocks.BlockChecksum) and stores
 // {Checksum, Address, BirthRevision} and the type into the parent through the
 // BlockOrigin (cache/trace.go:261-308). Blocks at the same height are independent, so
-// commitDirty hands the whole dirty forest to blocks.CommitBatch (libstormck's
-// stormck_commit_device): one launch per height, hashing every block of the level and
-// storing each Pointer into its parent in cache.data, in place (cache.data is
-// registered host memory, newArena). The host then finishes what storm's loop leaves
-// behind. The same steps, in the same order, are mirrored in Python by
+// commitDirty hands the whole dirty forest to blocks.CommitBatch (libstormck's routed
+// stormck_commit), which commits it height by height on the leg its measured cost model
+// picks: the GPU (one launch per height, reading cache.data in place over PCIe: it is
+// registered host memory, newArena) or the library's host leg (storm's own loop, each
+// height spread over host threads). For storm's per-revision commits the host leg wins
+// on the measured box (DESIGN.md §11 f1, "End to end from host memory"), so the stormck
+// build is never slower than storm's loop. The host then finishes what storm's loop
+// leaves behind. The same steps, in the same order, are mirrored in Python by
 // storm_amd/commit.py commit_cache and checked there against a restatement of storm's
 // own loop (tests/test_cache_commit.py).
 //
@@ -185,7 +188,7 @@ func (c *Cache) commitDirty() error {
 	out := make([]blocks.Hash, len(dirty))
 	sb := c.singularityBlock.V
 	last := sb.LastAllocatedBlock
-	err = blocks.CommitBatch(c.data, dirty, sb.Revision, &last, out)
+	_, err = blocks.CommitBatch(c.data, dirty, sb.Revision, &last, out)
 	// relocations the library applied (commitBlock, cache.go:114-118), also on a failure
 	sb.LastAllocatedBlock = last
 	for i, m := range metas {

@@ -2294,6 +2294,12 @@ int stormck_commit_device(void* d_arena, stormck_dirty_block* blocks, uint64_t n
 }
 
 // ---- f1, host leg --------------------------------------------------------------
+namespace {
+// A height is split over threads only in pieces of at least this many bytes (~10 us of
+// hashing on one core, about what the pool's fork/join costs).
+constexpr uint64_t kHostMinBytesPerThread = 256 * 1024;
+}  // namespace
+
 // The same commit on host threads: what storm's own loop costs (commitData hashes one
 // block at a time on its goroutine, cache/cache.go:87-137), with the blocks of one height
 // spread over `threads` pool threads. The level-synchronous device commit pays a launch
@@ -2352,7 +2358,11 @@ int stormck_commit_host(void* arena, stormck_dirty_block* blocks, uint64_t n, ui
     const unsigned nt = threads ? std::min<unsigned>(threads, fj.size()) : fj.size();
     for (uint32_t l = 0; l <= max_h; ++l) {
         const uint64_t lo = start[l], cnt = start[l + 1] - lo;
-        const uint64_t chunk = std::max<uint64_t>(1, cnt / (uint64_t{nt} * 8));
+        // a fork/join costs ~10 us: a height with little to hash stays on this thread
+        uint64_t level_bytes = 0;
+        for (uint64_t k = lo; k < lo + cnt; ++k) level_bytes += blocks[order[k]].length;
+        const unsigned pl = static_cast<unsigned>(std::min<uint64_t>(nt, std::max<uint64_t>(1, level_bytes / kHostMinBytesPerThread)));
+        const uint64_t chunk = std::max<uint64_t>(1, cnt / (uint64_t{pl} * 8));
         std::atomic<uint64_t> next{0};
         auto work = [&](unsigned) {
             for (;;) {
@@ -2371,25 +2381,27 @@ int stormck_commit_host(void* arena, stormck_dirty_block* blocks, uint64_t n, ui
                 }
             }
         };
-        fj.run(static_cast<unsigned>(std::min<uint64_t>(nt, (cnt + chunk - 1) / chunk)), work);
+        fj.run(static_cast<unsigned>(std::min<uint64_t>(pl, (cnt + chunk - 1) / chunk)), work);
     }
     return STORMCK_OK;
 }
 
 // ---- f1, the routed commit --------------------------------------------------------
-// Cost model of the two legs (us), constants measured on MI355X with the arena in
-// registered host memory ("End to end from host memory",
-// profiles/r04_commit_e2e/): the host leg hashes a height's blocks on nt threads at
-// kHostCoreBytesPerUs each, plus a fork/join per height; the device leg pays a fixed
-// call cost, then per height the longer of one XXH64 chain over its longest block and
-// its bytes over the link.
+// Cost model of the two legs (us), fitted to the end-to-end table measured on MI355X
+// ("End to end from host memory", profiles/r04_commit_e2e/): the host
+// leg hashes a height on one thread at kHostCoreBytesPerUs, or, when the height has at
+// least kHostMinBytesPerThread per thread, on up to nt threads plus a fork/join; the
+// device leg pays a call, then per height a launch and the longer of one XXH64 chain
+// over its longest block and its bytes over the link (in-place reads of the registered
+// arena). Measured: c5 forest 746 us device in place (link 51 GB/s), 1,740 us on one
+// host thread (25 GiB/s), 182 us on 16; the 3-block commit 62 us device, 5.3 us host.
 namespace {
-constexpr double kHostCoreBytesPerUs = 9000.0;   // one host thread, XXH64
-constexpr double kHostLevelUs = 4.0;
-constexpr double kDevCallUs = 30.0;
-constexpr double kDevChainBytesPerUs = 1600.0;   // one 4-lane chain on gfx950
-constexpr double kDevLevelUs = 8.0;
-constexpr double kLinkBytesPerUs = 50000.0;      // PCIe Gen5 x16, registered host memory
+constexpr double kHostCoreBytesPerUs = 24000.0;  // one EPYC 9575F thread, XXH64 of 32 KiB blocks
+constexpr double kHostLevelUs = 10.0;            // fork/join of a parallel height
+constexpr double kDevCallUs = 10.0;
+constexpr double kDevChainBytesPerUs = 1600.0;   // one 4-lane chain on gfx950 (32 KiB in ~20 us)
+constexpr double kDevLevelUs = 6.0;
+constexpr double kLinkBytesPerUs = 50000.0;      // PCIe Gen5 x16, in-place reads of registered host memory
 }  // namespace
 
 namespace {  // cost model helpers (internal)
@@ -2428,10 +2440,16 @@ bool commit_shape(const stormck_dirty_block* blocks, uint64_t n, CommitShape* s)
 double host_leg_us(const CommitShape& s, unsigned nt) {
     double t = 0;
     for (size_t l = 0; l < s.cnt.size(); ++l) {
+        // the split stormck_commit_host makes
+        const uint64_t pl = std::min<uint64_t>(nt, std::max<uint64_t>(1, s.bytes[l] / kHostMinBytesPerThread));
+        if (pl == 1) {
+            t += static_cast<double>(s.bytes[l]) / kHostCoreBytesPerUs;
+            continue;
+        }
         const double per_block = static_cast<double>(s.bytes[l]) / static_cast<double>(s.cnt[l]);
-        const uint64_t rounds = (s.cnt[l] + nt - 1) / nt;
+        const uint64_t rounds = (s.cnt[l] + pl - 1) / pl;
         t += std::max(static_cast<double>(rounds) * per_block, static_cast<double>(s.longest[l])) / kHostCoreBytesPerUs +
-             (nt > 1 ? kHostLevelUs : 0.0);
+             kHostLevelUs;
     }
     return t;
 }

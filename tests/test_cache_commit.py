@@ -113,6 +113,27 @@ def test_open_trace_is_refused_before_anything_changes():
         c.commit()
 
 
+# --- the host leg (stormck_commit_host): no device needed ----------------------------
+
+def _host_leg_run(c, threads):
+    """storm's cache.data committed where it lives by the library's host leg (the leg the
+    routed CommitBatch takes for storm's per-revision commits)."""
+    def run(recs, rev, last):
+        return cm.commit_host(c.data, recs, rev, last, threads=threads)
+    return run
+
+
+@pytest.mark.parametrize("threads", [1, 0])
+def test_binding_host_leg_matches_storm_commit_loop(threads):
+    a = _storm(_workload(seed=11, **SMALL))
+    c = _workload(seed=11, **SMALL)
+    b = _binding(c, _host_leg_run(c, threads))
+    assert a["sing"] == b["sing"]
+    assert a["store"] == b["store"]
+    assert a["metas"] == b["metas"]
+    assert a["data"] == b["data"]
+
+
 # --- GPU: the same through stormck_commit_device -------------------------------------
 
 torch = pytest.importorskip("torch")
@@ -153,6 +174,38 @@ def test_binding_on_gpu_matches_storm_commit_loop(arena):
     a = _storm(_workload(seed=11, **PROD))
     c = _workload(seed=11, **PROD)
     b = _binding(c, _device_run(c, dev) if arena == "hbm" else _registered_run(c))
+    assert a["sing"] == b["sing"]
+    assert a["store"] == b["store"]
+    assert a["metas"] == b["metas"]
+    assert a["data"] == b["data"]
+
+
+def _routed_run(c, legs):
+    """blocks.CommitBatch as the Go binding calls it: stormck_commit on the registered
+    cache.data, which picks the leg (recorded in `legs`)."""
+    from storm_amd import blocks
+
+    def run(recs, rev, last):
+        blocks.RegisterHostMemory(c.data)
+        try:
+            cs, last2, leg = cm.commit(c.data.ctypes.data, recs, rev, last)
+        finally:
+            blocks.UnregisterHostMemory(c.data)
+        legs.append(leg)
+        return cs, last2
+    return run
+
+
+@pytest.mark.gpu
+def test_binding_routed_matches_storm_commit_loop():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from storm_amd import _lib
+    a = _storm(_workload(seed=11, **PROD))
+    c = _workload(seed=11, **PROD)
+    legs = []
+    b = _binding(c, _routed_run(c, legs))
+    assert legs and all(x in (_lib.LEG_HOST, _lib.LEG_DEVICE) for x in legs), legs
     assert a["sing"] == b["sing"]
     assert a["store"] == b["store"]
     assert a["metas"] == b["metas"]

@@ -221,3 +221,22 @@ def test_storm_patch_applies_to_the_reference(tmp_path):
     cache = (dst / "cache.go").read_text()
     assert "c.commitDirty()" in cache and "newArena(" in cache and "c.commitData()" not in cache
     assert "commit commitRecord" in (dst / "types.go").read_text()
+
+
+def test_commit_batch_takes_the_routed_commit():
+    """CommitBatch hands storm's registered cache.data (a host pointer) to stormck_commit,
+    which picks the device or host leg by the measured crossover; it no
+    longer calls stormck_commit_device directly. The host-thread knob and the leg
+    constants are exported."""
+    text = open(SHIM).read()
+    body = text[text.index("func CommitBatch("):]
+    body = body[:body.index("\n}\n")]
+    assert "C.stormck_commit(bytesPtr(arena)" in body
+    assert "stormck_commit_device" not in body and "stormck_host_device_pointer" not in body
+    assert "C.uint32_t(CommitHostThreads)" in body
+    assert re.search(r"var CommitHostThreads uint32", text)
+    for name, c in (("LegNone", "STORMCK_LEG_NONE"), ("LegHost", "STORMCK_LEG_HOST"),
+                    ("LegDevice", "STORMCK_LEG_DEVICE")):
+        assert re.search(name + r"\s*=\s*uint32\(C\." + c + r"\)", text), name
+    stormck = _go("commit_stormck.go")
+    assert "_, err = blocks.CommitBatch(c.data, dirty, sb.Revision, &last, out)" in stormck
