@@ -890,8 +890,23 @@ def block_checksum_workload(a) -> int:
             traffic = tj.get("hbm_bytes_per_launch")
             # the committed rocprofv3 session this line's frac can be recomputed from
             # (tools/collect_profile.py): its kernel-trace average and the frac it implies
-            prof = {k: tj.get(k) for k in ("source", "profile_calls", "profile_avg_launch_ms", "profile_frac",
+            prof = {k: tj.get(k) for k in ("source", "pmc_source", "profile_calls", "profile_avg_launch_ms",
+                                           "profile_frac", "profile_timed_launches", "bench_under_rocprof",
                                            "traffic_over_algorithmic", "placement_spread")}
+
+    # The frac depends on where the arena lands in HBM (0.85-0.89 across fresh processes;
+    # neither VMM placement collapses the spread): report this line's frac
+    # beside the committed session's placement spread, the spread widened to include it.
+    placement = None
+    if prof and prof.get("placement_spread"):
+        import statistics
+        fr = list(prof["placement_spread"]["fracs"])
+        line = round(achieved / HBM_PEAK_GBS, 4)
+        placement = {"line_frac": line, "session": prof.get("source"),
+                     "session_median": round(statistics.median(fr), 4),
+                     "spread_with_line": [min(fr + [line]), max(fr + [line])],
+                     "median_with_line": round(statistics.median(fr + [line]), 4),
+                     "session_processes_below_line": sum(1 for f in fr if f < line), "session_processes": len(fr)}
 
     # also report against a measured stream-read peak. Measured here, after
     # the timed region, on the same arena: the rate depends on where the arena lands in
@@ -942,6 +957,7 @@ def block_checksum_workload(a) -> int:
                                        "median": round(kms[len(kms) // 2], 4), "max": round(kms[-1], 4),
                                        "in_order": [round(e0.elapsed_time(e1), 3) for (e0, e1, _) in hash_ev]},
                          "algorithmic_bytes_per_launch": int(alg_bytes), "profile_source": prof,
+                         "placement": placement,
                          "measured_read_peak": read_peak},
             "root": "0x%016x" % root_t[0],
             "root_pointer": ["0x%016x" % v for v in root_t[:3]] + [root_t[3]],
