@@ -373,6 +373,7 @@ def commit_e2e_workload(a):
                    block, children first),
       host_all     stormck_commit_host on every usable thread,
       routed       stormck_commit (the library's choice between the two),
+      routed_1     the same with one host thread allowed (host cores kept for storm),
     and, for reference, dev_hbm: the same forest with cache.data in HBM (device-resident,
     the north-star configuration). Forests: storm's c5 commits (BenchmarkKeyStore's
     1,200 objectlist leaves, BenchmarkStorm's 1,200 blob leaves, each under one pointer
@@ -432,17 +433,17 @@ def commit_e2e_workload(a):
                 rc = L.stormck_commit_host(arena.ctypes.data, bp, len(b), REV, ctypes.byref(la), op, 1)
             elif leg == "host_all":
                 rc = L.stormck_commit_host(arena.ctypes.data, bp, len(b), REV, ctypes.byref(la), op, threads)
-            else:
+            else:  # routed: the library's pool (0) or one host thread ("routed_1")
                 used = ctypes.c_uint32(9)
-                rc = L.stormck_commit(arena.ctypes.data, bp, len(b), REV, ctypes.byref(la), op, None, 0,
-                                      ctypes.byref(used))
-                outs["routed_leg"] = int(used.value)
+                rc = L.stormck_commit(arena.ctypes.data, bp, len(b), REV, ctypes.byref(la), op, None,
+                                      1 if leg == "routed_1" else 0, ctypes.byref(used))
+                outs[leg + "_leg"] = int(used.value)
             dt = time.perf_counter() - t0
             _lib.check(rc)
             return dt, out
 
         row = {"forest": name, "blocks": int(len(b0)), "leaves": nl, "hashed_bytes": bytes_hashed}
-        for leg in ("dev_inplace", "dev_hbm", "host_1", "host_all", "routed"):
+        for leg in ("dev_inplace", "dev_hbm", "host_1", "host_all", "routed", "routed_1"):
             n_reps = reps if not (leg == "host_1" and bytes_hashed > (1 << 30)) else 3
             for _ in range(2):
                 run(leg)
@@ -455,9 +456,10 @@ def commit_e2e_workload(a):
             row[leg + "_us"] = round(med * 1e6, 1)
             row[leg + "_GiBps"] = round(bytes_hashed / med / 2**30, 2)
             outs[leg] = out
-        row["routed_leg"] = {1: "host", 2: "device"}.get(outs.get("routed_leg"), outs.get("routed_leg"))
+        for k in ("routed_leg", "routed_1_leg"):
+            row[k] = {1: "host", 2: "device"}.get(outs.get(k), outs.get(k))
         row["agree"] = all(np.array_equal(outs["host_1"], outs[k]) for k in
-                           ("dev_inplace", "dev_hbm", "host_all", "routed"))
+                           ("dev_inplace", "dev_hbm", "host_all", "routed", "routed_1"))
         rows.append(row)
         print(json.dumps(row), flush=True)
         del hbm
