@@ -268,8 +268,8 @@ typedef struct {
     uint8_t type, reserved[3];
 } oracle_dirty_block;
 
-static const oracle_dirty_block* g_sort_blocks;
-static const uint32_t* g_sort_height;
+static _Thread_local const oracle_dirty_block* g_sort_blocks;  /* per thread: callers may run concurrently */
+static _Thread_local const uint32_t* g_sort_height;
 static int cmp_order(const void* a, const void* b) {
     size_t x = *(const size_t*)a, y = *(const size_t*)b;
     if (g_sort_height[x] != g_sort_height[y]) return g_sort_height[x] < g_sort_height[y] ? -1 : 1;

@@ -222,6 +222,47 @@ static void commit_planning(bool device) {
           STORMCK_EINVAL);
 }
 
+// f1's host leg (no device needed): stormck_commit_host on 1 thread and on the pool,
+// against the oracle's serial commit, from several caller threads at once (each height
+// fans out over the shared ForkJoin pool); with a device, the routed stormck_commit on
+// a pageable arena (the host leg by construction).
+static void commit_host_leg(bool device) {
+    auto one = [&](uint64_t nl, bool shuffle, uint32_t threads, uint64_t seed) {
+        std::mt19937_64 rng(seed);
+        const uint32_t fanout = nl > 10000 ? 100 : 10;
+        const uint64_t slot = nl > 10000 ? 4096 : 1024;
+        Forest f = make_forest(nl, fanout, slot, 5, rng, shuffle);
+        const uint64_t n = f.b.size();
+        std::vector<uint8_t> host(f.arena_bytes, 0);
+        for (uint64_t i = 0; i < n; ++i)
+            if (f.b[i].type == STORMCK_LEAF_BLOCK)
+                for (uint32_t k = 0; k < f.b[i].length; k += 8) host[f.b[i].data_offset + k] = static_cast<uint8_t>(rng());
+        auto ref_arena = host;
+        auto ref = f.b;
+        uint64_t ref_last = f.last, last = f.last;
+        std::vector<uint64_t> ref_cs(n, 0), cs(n, 0);
+        CHECK(oracle_commit(ref_arena.data(), ref.data(), n, 5, &ref_last, ref_cs.data()) == 0);
+        if (device && threads == 7) {  // the routed entry on pageable memory
+            uint32_t leg = 0;
+            CHECK(stormck_commit(host.data(), f.b.data(), n, 5, &last, cs.data(), nullptr, 0, &leg) == STORMCK_OK &&
+                  leg == STORMCK_LEG_HOST);
+        } else {
+            CHECK(stormck_commit_host(host.data(), f.b.data(), n, 5, &last, cs.data(), threads) == STORMCK_OK);
+        }
+        CHECK(last == ref_last && cs == ref_cs && host == ref_arena);
+        CHECK(std::memcmp(ref.data(), f.b.data(), n * sizeof(stormck_dirty_block)) == 0);
+    };
+    for (uint64_t nl : {uint64_t{1}, uint64_t{2}, uint64_t{137}, uint64_t{5000}, uint64_t{70000}})
+        for (bool shuffle : {false, true})
+            for (uint32_t threads : {1u, 0u}) one(nl, shuffle, threads, 21 + nl);
+    std::vector<std::thread> th;
+    for (int t = 0; t < 4; ++t)
+        th.emplace_back([&, t] {
+            for (int it = 0; it < 3; ++it) one(3000 + 977 * t, t & 1, (it == 2) ? 7u : 0u, 50 + 10 * t + it);
+        });
+    for (auto& x : th) x.join();
+}
+
 static void host_pipeline_paths() {
     std::mt19937_64 rng(3);
     const uint64_t n = 12000, stride = 32768;  // 375 MiB: two 256 MiB pipeline chunks
@@ -354,6 +395,8 @@ int main() {
     if (device) CHECK(stormck_init(0) == STORMCK_OK);
     commit_planning(device);
     std::printf("commit planning: done\n");
+    commit_host_leg(device);
+    std::printf("commit host leg: done\n");
     if (device) host_pipeline_paths();
     if (device) concurrent_callers();
     if (device) std::printf("concurrent callers: done\n");
