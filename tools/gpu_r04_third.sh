@@ -11,4 +11,6 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $out/smok
 timeout -k 10 400 python bench.py --workload commit_e2e --steps 9 > $out/commit_e2e.log 2>&1 || exit 1
 timeout -k 10 300 python bench.py > $out/bench.log 2>&1 || exit 1
 tail -c 600 $out/bench.log
+# host XXH64 rates of the box's CPU (no GPU use): scalar vs AVX-512 multi-block
+timeout -k 10 120 ./tools/host_xxh64_probe > $out/host_xxh64.txt 2>&1 && cat $out/host_xxh64.txt
 exit $rc
