@@ -2368,16 +2368,32 @@ int stormck_commit_host(void* arena, stormck_dirty_block* blocks, uint64_t n, ui
             for (;;) {
                 const uint64_t k0 = next.fetch_add(chunk, std::memory_order_relaxed);
                 if (k0 >= cnt) return;
-                for (uint64_t k = k0; k < std::min(cnt, k0 + chunk); ++k) {
-                    const uint64_t i = order[lo + k];
+                const uint64_t k1 = std::min(cnt, k0 + chunk);
+                auto store = [&](uint64_t i, uint64_t h) {
                     const stormck_dirty_block& b = blocks[i];
-                    const uint64_t h = host::xxh64(a + b.data_offset, b.length);
                     out_checksums[i] = h;
                     if (b.origin_pointer != STORMCK_NO_ORIGIN) {
                         const uint64_t ptr[3] = {h, b.address, b.birth_revision};
                         std::memcpy(a + b.origin_pointer, ptr, sizeof ptr);
                         a[b.origin_type] = b.type;
                     }
+                };
+                uint64_t k = k0;
+                for (; host::has_x4() && k + 4 <= k1; k += 4) {  // four blocks' chains at once (AVX-512)
+                    const unsigned char* p4[4];
+                    size_t n4[4];
+                    uint64_t h4[4];
+                    for (int q = 0; q < 4; ++q) {
+                        const stormck_dirty_block& b = blocks[order[lo + k + q]];
+                        p4[q] = a + b.data_offset;
+                        n4[q] = b.length;
+                    }
+                    host::xxh64_x4(p4, n4, h4);
+                    for (int q = 0; q < 4; ++q) store(order[lo + k + q], h4[q]);
+                }
+                for (; k < k1; ++k) {
+                    const uint64_t i = order[lo + k];
+                    store(i, host::xxh64(a + blocks[i].data_offset, blocks[i].length));
                 }
             }
         };

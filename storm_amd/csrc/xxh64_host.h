@@ -15,6 +15,10 @@
 #include <stddef.h>
 #include <stdint.h>
 #include <string.h>
+#if defined(__x86_64__) && !defined(__HIP_DEVICE_COMPILE__)
+#define STORMCK_HOST_X4 1
+#include <immintrin.h>
+#endif
 
 namespace stormck::host {
 
@@ -84,6 +88,89 @@ inline uint64_t xxh64(const void* data, size_t n) {
     h ^= h >> 29;
     h *= P3;
     return h ^ (h >> 32);
+}
+
+// Several buffers at once (the f1 host leg hashes a height's blocks this way). One XXH64
+// is four serial chains whose rounds each cost two 64-bit multiplies; a scalar core runs
+// them one imul at a time. With AVX-512 (F, VL, DQ) one 256-bit vpmullq does a round of
+// all four accumulators of a buffer, and four buffers' chains interleave: the rounds of
+// the stripes every buffer has run vectorised, each buffer then finishes its own stripes,
+// merge and tail on the scalar path. Results are bit-identical to xxh64().
+inline uint64_t xxh64_finish(uint64_t h, const unsigned char* p, size_t rem, size_t n) {
+    const unsigned char* const end = p + rem;
+    h += static_cast<uint64_t>(n);
+    for (; end - p >= 8; p += 8) h = rotl(h ^ lane(0, le64(p)), 27) * P1 + P4;
+    if (end - p >= 4) {
+        h = rotl(h ^ (static_cast<uint64_t>(le32(p)) * P1), 23) * P2 + P3;
+        p += 4;
+    }
+    for (; p < end; ++p) h = rotl(h ^ (*p * P5), 11) * P1;
+    h ^= h >> 33;
+    h *= P2;
+    h ^= h >> 29;
+    h *= P3;
+    return h ^ (h >> 32);
+}
+
+#ifdef STORMCK_HOST_X4
+__attribute__((target("avx512f,avx512vl,avx512dq"))) inline void xxh64_x4_avx512(const unsigned char* const* p,
+                                                                                    const size_t* n, uint64_t* out) {
+    const __m256i p1 = _mm256_set1_epi64x(static_cast<long long>(P1));
+    const __m256i p2 = _mm256_set1_epi64x(static_cast<long long>(P2));
+    const __m256i seed = _mm256_set_epi64x(static_cast<long long>(0 - P1), 0, static_cast<long long>(P2),
+                                           static_cast<long long>(P1 + P2));
+    __m256i acc[4] = {seed, seed, seed, seed};
+    size_t common = SIZE_MAX;
+    for (int k = 0; k < 4; ++k) common = n[k] < common ? n[k] : common;
+    common /= 32;
+    for (size_t s = 0; s < common; ++s) {
+        for (int k = 0; k < 4; ++k) {
+            const __m256i w = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(p[k] + 32 * s));
+            acc[k] = _mm256_mullo_epi64(_mm256_rol_epi64(_mm256_add_epi64(acc[k], _mm256_mullo_epi64(w, p2)), 31), p1);
+        }
+    }
+    for (int k = 0; k < 4; ++k) {
+        if (n[k] < 32) {
+            out[k] = xxh64_finish(P5, p[k], n[k], n[k]);
+            continue;
+        }
+        alignas(32) uint64_t a[4];
+        _mm256_store_si256(reinterpret_cast<__m256i*>(a), acc[k]);
+        const size_t ns = n[k] / 32;
+        for (size_t s = common; s < ns; ++s) {
+            const unsigned char* q = p[k] + 32 * s;
+            a[0] = lane(a[0], le64(q));
+            a[1] = lane(a[1], le64(q + 8));
+            a[2] = lane(a[2], le64(q + 16));
+            a[3] = lane(a[3], le64(q + 24));
+        }
+        uint64_t h = rotl(a[0], 1) + rotl(a[1], 7) + rotl(a[2], 12) + rotl(a[3], 18);
+        h = fold(fold(fold(fold(h, a[0]), a[1]), a[2]), a[3]);
+        out[k] = xxh64_finish(h, p[k] + 32 * ns, n[k] - 32 * ns, n[k]);
+    }
+}
+#endif
+
+// Whether xxh64_x4_avx512 can run on this CPU (checked once).
+inline bool has_x4() {
+#ifdef STORMCK_HOST_X4
+    static const bool ok = __builtin_cpu_supports("avx512f") && __builtin_cpu_supports("avx512vl") &&
+                           __builtin_cpu_supports("avx512dq");
+    return ok;
+#else
+    return false;
+#endif
+}
+
+// out[k] = xxh64(p[k], n[k]) for k < 4.
+inline void xxh64_x4(const unsigned char* const* p, const size_t* n, uint64_t* out) {
+#ifdef STORMCK_HOST_X4
+    if (has_x4()) {
+        xxh64_x4_avx512(p, n, out);
+        return;
+    }
+#endif
+    for (int k = 0; k < 4; ++k) out[k] = xxh64(p[k], n[k]);
 }
 
 }  // namespace stormck::host
