@@ -2409,10 +2409,13 @@ int stormck_commit_host(void* arena, stormck_dirty_block* blocks, uint64_t n, ui
 // least kHostMinBytesPerThread per thread, on up to nt threads plus a fork/join; the
 // device leg pays a call, then per height a launch and the longer of one XXH64 chain
 // over its longest block and its bytes over the link (in-place reads of the registered
-// arena). Measured: c5 forest 746 us device in place (link 51 GB/s), 1,740 us on one
-// host thread (25 GiB/s), 182 us on 16; the 3-block commit 62 us device, 5.3 us host.
+// arena). Measured (profiles/r04_commit_e2e/x4_host_leg.log): c5 forest 783 us device in
+// place (link 49 GB/s), 745 us on one host thread hashing four blocks at once (51 GB/s;
+// 1,740 us scalar, storm's own rate), 104-144 us on 16; the 3-block commit 63 us device,
+// 4.8 us host.
 namespace {
-constexpr double kHostCoreBytesPerUs = 24000.0;  // one EPYC 9575F thread, XXH64 of 32 KiB blocks
+constexpr double kHostCoreBytesPerUs = 24000.0;  // one EPYC 9575F thread, scalar XXH64 of 32 KiB blocks
+constexpr double kHostCoreX4BytesPerUs = 48000.0;  // the same thread hashing four blocks at once (AVX-512)
 constexpr double kHostLevelUs = 10.0;            // fork/join of a parallel height
 constexpr double kDevCallUs = 10.0;
 constexpr double kDevChainBytesPerUs = 1600.0;   // one 4-lane chain on gfx950 (32 KiB in ~20 us)
@@ -2454,18 +2457,18 @@ bool commit_shape(const stormck_dirty_block* blocks, uint64_t n, CommitShape* s)
 }
 
 double host_leg_us(const CommitShape& s, unsigned nt) {
+    const double core = host::has_x4() ? kHostCoreX4BytesPerUs : kHostCoreBytesPerUs;
     double t = 0;
     for (size_t l = 0; l < s.cnt.size(); ++l) {
         // the split stormck_commit_host makes
         const uint64_t pl = std::min<uint64_t>(nt, std::max<uint64_t>(1, s.bytes[l] / kHostMinBytesPerThread));
         if (pl == 1) {
-            t += static_cast<double>(s.bytes[l]) / kHostCoreBytesPerUs;
+            t += static_cast<double>(s.bytes[l]) / core;
             continue;
         }
         const double per_block = static_cast<double>(s.bytes[l]) / static_cast<double>(s.cnt[l]);
         const uint64_t rounds = (s.cnt[l] + pl - 1) / pl;
-        t += std::max(static_cast<double>(rounds) * per_block, static_cast<double>(s.longest[l])) / kHostCoreBytesPerUs +
-             kHostLevelUs;
+        t += std::max(static_cast<double>(rounds) * per_block, static_cast<double>(s.longest[l])) / core + kHostLevelUs;
     }
     return t;
 }
