@@ -118,6 +118,10 @@ def test_argument_errors_precede_the_device_check():
         ("register empty", lambda: L.stormck_host_register(None, 0)),
         ("alloc null", lambda: L.stormck_device_alloc(16, None)),
         ("alloc 0 bytes", lambda: L.stormck_device_alloc(0, ctypes.byref(ctypes.c_void_p()))),
+        ("placed null", lambda: L.stormck_device_alloc_placed(16, 1, 0, None, None)),
+        ("placed mode", lambda: L.stormck_device_alloc_placed(16, 7, 0, ctypes.byref(ctypes.c_void_p()), None)),
+        ("routed commit null", lambda: L.stormck_commit(None, None, 3, 1, None, None, None, 0, None)),
+        ("host leg null", lambda: L.stormck_commit_host(None, None, 3, 1, None, None, 1)),
         ("device pointer null", lambda: L.stormck_host_device_pointer(None, None)),
         ("key tags null", lambda: L.stormck_key_tags_device(None, 48, None, None, 48, 10, 1 << 20, None)),
         ("host null base", lambda: L.stormck_checksum_host(None, 32, None, 32, 4, ctypes.addressof(out))),

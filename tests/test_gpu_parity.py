@@ -955,3 +955,29 @@ def test_device_entry_points_are_graph_capturable(dev):
         want = o.checksum_batch(buf.cpu().numpy(), n, stride, stride)
         assert np.array_equal(_u64(out), want)
         assert engine.as_tuple(root) == o.merkle_root(want, 0, n, 1, 1200)
+
+
+@pytest.mark.parametrize("mode,chunk", [(1, 0), (1, 1 << 21), (2, 0), (0, 0)])
+def test_arena_placement_modes(dev, mode, chunk):
+    """stormck_device_alloc_placed: plain hipMalloc, a VMM reservation with one or several
+    physical allocations, a contiguous allocation. A 384 MiB arena in each
+    mode hashes like the oracle through the LDS-DMA kernel and frees cleanly; a VMM
+    arena's VA is the reservation's and its chunk is reported."""
+    from oracle import oracle as o
+    from storm_amd import engine
+    n, stride = 12288, 32768
+    ptr, mapped = engine.device_alloc_placed(n * stride, mode, chunk)
+    try:
+        assert ptr % 4096 == 0
+        if mode == 1:
+            assert mapped >= (chunk or n * stride) and mapped % 4096 == 0
+        else:
+            assert mapped == 0
+        engine.fill_synthetic_device(ptr, stride, n, 7, o.SYNTH_SEED)
+        out = torch.empty(n, dtype=torch.int64, device=dev)
+        engine.checksum_device(ptr, stride, n, out.data_ptr(), stride)
+        torch.cuda.synchronize()
+        want = o.checksum_batch(o.fill_synthetic(n, stride, 7), n, stride, stride, threads=8)
+        assert np.array_equal(_u64(out), want)
+    finally:
+        engine.device_free(ptr)
