@@ -1344,6 +1344,40 @@ __global__ __launch_bounds__(256) void k_order_sort(const uint32_t* __restrict__
     }
 }
 
+// Rows of a group by length, rotated per workgroup step (round 4). A wave streams as many
+// tiles as the longest of its 16 blocks, so with storm's four leaf lengths mixed at random
+// nearly every wave runs 64 tiles while its blocks average 60.75. Here the 128 blocks of a
+// group stay the same set (the group's address window is unchanged): they are only
+// re-dealt to rows so that each wave gets 16 blocks of adjacent length ranks, and the
+// rank slice a wave gets rotates with the workgroup's group counter k = g / G (the
+// persistent kernel's groups g, g + G, ...), so over 8 groups every wave gets every
+// slice once and the waves of a workgroup stay together. Within a slice, ties keep the
+// address order. Full groups only; the last partial group is left as it is. One
+// workgroup of 128 threads per group.
+__global__ __launch_bounds__(128) void k_order_rank(uint32_t* __restrict__ order, uint64_t* __restrict__ s_offs,
+                                                    uint32_t* __restrict__ s_lens, uint64_t G) {
+    __shared__ uint32_t len[128], ord[128];
+    __shared__ uint64_t off[128];
+    const uint32_t t = threadIdx.x;
+    const uint64_t g = blockIdx.x, at = g * 128 + t;
+    len[t] = s_lens[at];
+    ord[t] = order[at];
+    off[t] = s_offs[at];
+    __syncthreads();
+    const uint32_t mine = len[t];
+    uint32_t rank = 0;
+    for (uint32_t u = 0; u < 128; ++u) {
+        const uint32_t l = len[u];
+        rank += (l < mine) || (l == mine && u < t);
+    }
+    const uint32_t k = static_cast<uint32_t>((g / G) & 7);
+    const uint32_t wave = ((rank >> 4) + 8 - k) & 7;
+    const uint64_t to = g * 128 + wave * 16 + (rank & 15);
+    order[to] = ord[t];
+    s_offs[to] = off[t];
+    s_lens[to] = mine;
+}
+
 // The stripes of a block that k_xxh64_glds_var did not stage (a start that is not 16-byte
 // aligned), straight from global memory. Out of line: the kernel's hot loop stays compact.
 __device__ __noinline__ uint64_t var_stripes_from_global(const uint8_t* p, uint32_t nst, uint32_t j, uint64_t acc) {

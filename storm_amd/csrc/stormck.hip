@@ -434,6 +434,16 @@ bool order_on() {
     return on;
 }
 
+// Large gathers with per-block lengths deal each group's rows by length rank (k_order_rank);
+// probe knob STORMCK_GATHER_RANK=0 keeps the address order inside a group (A/B).
+bool rank_on() {
+    static const bool on = [] {
+        const char* e = STORMCK_KNOB("STORMCK_GATHER_RANK");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 bool grid_for(uint64_t threads, dim3* grid) {
     const uint64_t blocks = (threads + kThreads - 1) / kThreads;
     if (blocks == 0 || blocks > 0x7fffffffULL) return false;
@@ -604,6 +614,11 @@ int launch_checksum(const uint8_t* base, uint64_t stride, const uint32_t* lens, 
             hipLaunchKernelGGL(k_order_scan_buckets, dim3(1), dim3(1024), 0, st, bounds);
             hipLaunchKernelGGL(k_order_place, dim3(kOrderParts), dim3(256), 0, st, offs, n, counts, bounds, order, s_offs);
             hipLaunchKernelGGL(k_order_sort, dim3(kOrderBuckets), dim3(256), 0, st, lens, bounds, order, s_offs, s_lens);
+            // per-block lengths in the persistent form: each group's rows re-dealt by length
+            // rank, rotated per workgroup step (kernels.h k_order_rank)
+            if (lens && persistent && rank_on() && n / kGldsBlocks > 0)
+                hipLaunchKernelGGL(k_order_rank, dim3(static_cast<unsigned>(n / kGldsBlocks)), dim3(kGldsBlocks), 0, st,
+                                   order, s_offs, s_lens, static_cast<uint64_t>(grid.x));
             lens = s_lens;
             offs = s_offs;
 #define STORMCK_ORD(SK, LN)                                                                                      \

@@ -19,7 +19,8 @@ OPERATIONAL = {"STORMCK_READ_THREADS", "STORMCK_READ_SUPER_BYTES", "STORMCK_TRAC
 PROBE_KNOBS = {"STORMCK_STAGE_PIPE", "STORMCK_WIDE16", "STORMCK_WIDE_MULTI", "STORMCK_GLDS_VAR", "STORMCK_VAR_LO",
                "STORMCK_MID_WAVES", "STORMCK_BIG_W", "STORMCK_QUAD_SPREAD", "STORMCK_GATHER_ORDER",
                "STORMCK_COMMIT_WIDE", "STORMCK_COMMIT_MULTI", "STORMCK_COMMIT_MIDW", "STORMCK_COMMIT_CHUNKS",
-               "STORMCK_POINTER_RING", "STORMCK_POINTER_C", "STORMCK_POINTER_SIMD", "STORMCK_SINGLE_GPU_MIN"}
+               "STORMCK_POINTER_RING", "STORMCK_POINTER_C", "STORMCK_POINTER_SIMD", "STORMCK_SINGLE_GPU_MIN",
+               "STORMCK_GATHER_RANK"}
 
 
 def _env_strings(path):
