@@ -1312,6 +1312,10 @@ int stormck_device_alloc_placed(uint64_t bytes, uint32_t mode, uint64_t chunk_by
         (void)hipMemAddressFree(va, size);
         (void)hipGetLastError();
     };
+    hipMemAccessDesc acc;
+    std::memset(&acc, 0, sizeof acc);
+    acc.location = prop.location;
+    acc.flags = hipMemAccessFlagsProtReadWrite;
     for (uint64_t off = 0; off < size; off += chunk) {
         hipMemGenericAllocationHandle_t h;
         hipError_t e = hipMemCreate(&h, chunk, &prop, 0);
@@ -1320,20 +1324,13 @@ int stormck_device_alloc_placed(uint64_t bytes, uint32_t mode, uint64_t chunk_by
             if (e != hipSuccess) (void)hipMemRelease(h);
             else a.handles.push_back(h);
         }
+        // access per mapped chunk (one call over the whole reservation is not relied on)
+        if (e == hipSuccess) e = hipMemSetAccess(static_cast<uint8_t*>(va) + off, chunk, &acc, 1);
         if (e != hipSuccess) {
             undo();
             return fail(e == hipErrorOutOfMemory ? STORMCK_ENOMEM : STORMCK_EHIP,
                         std::string("VMM arena: ") + hipGetErrorString(e));
         }
-    }
-    hipMemAccessDesc acc;
-    std::memset(&acc, 0, sizeof acc);
-    acc.location = prop.location;
-    acc.flags = hipMemAccessFlagsProtReadWrite;
-    const hipError_t e = hipMemSetAccess(va, size, &acc, 1);
-    if (e != hipSuccess) {
-        undo();
-        return fail(STORMCK_EHIP, std::string("VMM arena: hipMemSetAccess: ") + hipGetErrorString(e));
     }
     a.chunk = chunk;
     {
