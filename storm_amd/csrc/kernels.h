@@ -1344,7 +1344,9 @@ __global__ __launch_bounds__(256) void k_order_sort(const uint32_t* __restrict__
     }
 }
 
-// Rows of a group by length, rotated per workgroup step (round 4). A wave streams as many
+// Rows of a group by length, rotated per workgroup step (round 4; probe build only: it
+// measured 0.794 against 0.848 of 8 TB/s for address order, profiles/r04_gather_rank/).
+// A wave streams as many
 // tiles as the longest of its 16 blocks, so with storm's four leaf lengths mixed at random
 // nearly every wave runs 64 tiles while its blocks average 60.75. Here the 128 blocks of a
 // group stay the same set (the group's address window is unchanged): they are only
@@ -1354,6 +1356,7 @@ __global__ __launch_bounds__(256) void k_order_sort(const uint32_t* __restrict__
 // slice once and the waves of a workgroup stay together. Within a slice, ties keep the
 // address order. Full groups only; the last partial group is left as it is. One
 // workgroup of 128 threads per group.
+#ifdef STORMCK_PROBES
 __global__ __launch_bounds__(128) void k_order_rank(uint32_t* __restrict__ order, uint64_t* __restrict__ s_offs,
                                                     uint32_t* __restrict__ s_lens, uint64_t G) {
     __shared__ uint32_t len[128], ord[128];
@@ -1377,6 +1380,7 @@ __global__ __launch_bounds__(128) void k_order_rank(uint32_t* __restrict__ order
     s_offs[to] = off[t];
     s_lens[to] = mine;
 }
+#endif
 
 // The stripes of a block that k_xxh64_glds_var did not stage (a start that is not 16-byte
 // aligned), straight from global memory. Out of line: the kernel's hot loop stays compact.

@@ -434,12 +434,12 @@ bool order_on() {
     return on;
 }
 
-// Large gathers with per-block lengths deal each group's rows by length rank (k_order_rank);
-// probe knob STORMCK_GATHER_RANK=0 keeps the address order inside a group (A/B).
-bool rank_on() {
+// Probe knob STORMCK_GATHER_RANK=1: large gathers with per-block lengths deal each group's
+// rows by length rank (k_order_rank; measured slower).
+[[maybe_unused]] bool rank_on() {
     static const bool on = [] {
         const char* e = STORMCK_KNOB("STORMCK_GATHER_RANK");
-        return !(e && e[0] == '0');
+        return e && e[0] == '1';
     }();
     return on;
 }
@@ -614,11 +614,13 @@ int launch_checksum(const uint8_t* base, uint64_t stride, const uint32_t* lens, 
             hipLaunchKernelGGL(k_order_scan_buckets, dim3(1), dim3(1024), 0, st, bounds);
             hipLaunchKernelGGL(k_order_place, dim3(kOrderParts), dim3(256), 0, st, offs, n, counts, bounds, order, s_offs);
             hipLaunchKernelGGL(k_order_sort, dim3(kOrderBuckets), dim3(256), 0, st, lens, bounds, order, s_offs, s_lens);
-            // per-block lengths in the persistent form: each group's rows re-dealt by length
-            // rank, rotated per workgroup step (kernels.h k_order_rank)
+#ifdef STORMCK_PROBES
+            // rejected (round 4): each group's rows re-dealt by length rank, rotated per
+            // workgroup step (kernels.h k_order_rank): 0.794 against 0.848 of 8 TB/s
             if (lens && persistent && rank_on() && n / kGldsBlocks > 0)
                 hipLaunchKernelGGL(k_order_rank, dim3(static_cast<unsigned>(n / kGldsBlocks)), dim3(kGldsBlocks), 0, st,
                                    order, s_offs, s_lens, static_cast<uint64_t>(grid.x));
+#endif
             lens = s_lens;
             offs = s_offs;
 #define STORMCK_ORD(SK, LN)                                                                                      \

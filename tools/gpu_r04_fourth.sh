@@ -1,6 +1,6 @@
 # Round 4, fourth GPU session: the -m gpu suite, the f1 end-to-end table again (routed
 # legs with the refit host rate), and the gather A/B of k_order_rank (rows of a group
-# dealt by length rank; probe build, STORMCK_GATHER_RANK=0 = address order), 3 fresh
+# dealt by length rank; probe build, STORMCK_GATHER_RANK=1 = by rank), 3 fresh
 # processes per side, alternating.
 # Usage: bash tools/gpu_r04_fourth.sh <tag>
 set -o pipefail
