@@ -1392,7 +1392,9 @@ __device__ __noinline__ uint64_t var_stripes_from_global(const uint8_t* p, uint3
 
 // ORD: offs and lens are in a locality order of a large gather (k_order_*, s_offs /
 // s_lens), and order[i] is the index of the i-th block: its checksum's slot.
-template <int T, int AUX, bool VERIFY, int WAVES, int SKEW, bool LENS, bool OFFS, bool ORD = false>
+// CONTIG (probe build): a persistent workgroup takes a contiguous run of groups instead of
+// every G-th group.
+template <int T, int AUX, bool VERIFY, int WAVES, int SKEW, bool LENS, bool OFFS, bool ORD = false, bool CONTIG = false>
 __global__ __launch_bounds__(64 * WAVES) void k_xxh64_glds_var(const uint8_t* __restrict__ base, uint64_t stride,
                                                                const uint32_t* __restrict__ lens, uint32_t len,
                                                                const uint64_t* __restrict__ offs, uint64_t n,
@@ -1417,7 +1419,12 @@ __global__ __launch_bounds__(64 * WAVES) void k_xxh64_glds_var(const uint8_t* __
     const uint32_t wave = tid >> 6, lane = tid & 63;
     const uint64_t ngroups = (n + BPW - 1) / BPW;
     const uint64_t G = gridDim.x;
-    if (blockIdx.x >= ngroups) return;
+    // this workgroup's groups: g_first, g_step(g_first), ... below g_end
+    const uint64_t g_per = CONTIG ? (ngroups + G - 1) / G : 0;
+    const uint64_t g_first = CONTIG ? blockIdx.x * g_per : blockIdx.x;
+    const uint64_t g_end = CONTIG ? min(ngroups, g_first + g_per) : ngroups;
+    auto g_step = [&](uint64_t g) { return CONTIG ? g + 1 : g + G; };
+    if (g_first >= g_end) return;
     const uint64_t ph = static_cast<uint64_t>(wave) * SKEW;  // this wave's start delay
     if (tid == 0) *n_finished = 0;
     __syncthreads();  // before any wave can finish
@@ -1449,7 +1456,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_xxh64_glds_var(const uint8_t* __
 #pragma unroll
         for (int k = 0; k < PER_WAVE; ++k) {
             const uint64_t gb = g * BPW + prow[k];
-            const bool live = g < ngroups && gb < n;
+            const bool live = g < g_end && gb < n;
             const uint64_t gc = live ? gb : 0;
             // unconditional loads (clamped index): a load under a branch gets its own
             // vmcnt(0) wait, which would serialise the 2 * PER_WAVE loads
@@ -1458,7 +1465,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_xxh64_glds_var(const uint8_t* __
             i_nl[k] = live ? l : 0;
         }
     };
-    uint64_t ig = blockIdx.x;
+    uint64_t ig = g_first;
     [[maybe_unused]] uint32_t it = 0;  // tile of group ig to issue next (used by the device pass)
     uint32_t i_ntl = 0;
     [[maybe_unused]] uint32_t i_full = 0;  // whole-tile stripe bytes of every block (device pass)
@@ -1475,12 +1482,12 @@ __global__ __launch_bounds__(64 * WAVES) void k_xxh64_glds_var(const uint8_t* __
         i_ntl = wave_max(tiles);
         // stripe bytes every block of the wave has, in whole tiles: tiles below it are full
         i_full = ~wave_max(~lim_min) / ROW * ROW;
-        i_fetch(ig + G);
+        i_fetch(g_step(ig));
     };
     auto i_next_group = [&]() __attribute__((always_inline)) {  // the next group with tiles for this wave
         for (;;) {
-            ig += G;
-            if (ig >= ngroups) {
+            ig = g_step(ig);
+            if (ig >= g_end) {
                 i_done = true;
                 return;
             }
@@ -1520,14 +1527,14 @@ __global__ __launch_bounds__(64 * WAVES) void k_xxh64_glds_var(const uint8_t* __
     bool h_nlive = false;
     auto h_fetch = [&](uint64_t g) __attribute__((always_inline)) {
         const uint64_t gb = g * BPW + b;
-        h_nlive = g < ngroups && gb < n;
+        h_nlive = g < g_end && gb < n;
         const uint64_t gc = h_nlive ? gb : 0;
         const uint32_t l = LENS ? lens[gc] : len;  // unconditional, as i_fetch
         h_np = block_ptr(gc);
         h_nl = h_nlive ? l : 0;
         h_nidx = ORD ? order[gc] : gc;
     };
-    uint64_t hg = blockIdx.x;
+    uint64_t hg = g_first;
     uint32_t ht = 0, h_ntl = 0, h_L = 0, h_nst = 0, h_sst = 0;
     uint64_t h_idx = 0;
     const uint8_t* h_p = nullptr;
@@ -1555,7 +1562,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_xxh64_glds_var(const uint8_t* __
             const bool use = j == 0 && sb > 0 && 8u * q < rem;  // (sb > 0: 16-byte aligned start)
             tail[q] = *reinterpret_cast<const uint64_t*>(use ? t + 8 * q : safe);
         }
-        h_fetch(hg + G);
+        h_fetch(g_step(hg));
     };
     auto h_finish = [&]() __attribute__((always_inline)) {  // the group's blocks are complete: unstaged stripes, tail, checksum
         if (__builtin_expect(h_sst < h_nst, 0)) acc = var_stripes_from_global(h_p, h_nst, j, acc);
@@ -1577,8 +1584,8 @@ __global__ __launch_bounds__(64 * WAVES) void k_xxh64_glds_var(const uint8_t* __
     };
     auto h_next_group = [&]() __attribute__((always_inline)) {  // finish groups without tiles on the way
         for (;;) {
-            hg += G;
-            if (hg >= ngroups) {
+            hg = g_step(hg);
+            if (hg >= g_end) {
                 h_done = true;
                 // count this wave out; the add lands before the next barrier, after which
                 // every wave reads the count

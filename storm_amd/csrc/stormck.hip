@@ -626,6 +626,21 @@ int launch_checksum(const uint8_t* base, uint64_t stride, const uint32_t* lens, 
 #define STORMCK_ORD(SK, LN)                                                                                      \
     hipLaunchKernelGGL((k_xxh64_glds_var<kTileStripes, kAuxNT, false, kGldsWaves, SK, LN, true, true>), grid,       \
                        dim3(kGldsThreads), 0, st, base, stride, lens, len, offs, n, out, expected, first_bad, n_bad, order)
+#ifdef STORMCK_PROBES  // probe knob STORMCK_GATHER_CONTIG=1: contiguous group runs per workgroup
+#define STORMCK_ORDC(LN)                                                                                         \
+    hipLaunchKernelGGL((k_xxh64_glds_var<kTileStripes, kAuxNT, false, kGldsWaves, kSkewTiles, LN, true, true, true>), \
+                       grid, dim3(kGldsThreads), 0, st, base, stride, lens, len, offs, n, out, expected, first_bad,    \
+                       n_bad, order)
+            static const bool contig = [] {
+                const char* e = STORMCK_KNOB("STORMCK_GATHER_CONTIG");
+                return e && e[0] == '1';
+            }();
+            if (persistent && contig) {
+                if (lens) STORMCK_ORDC(true);
+                else STORMCK_ORDC(false);
+            } else
+#undef STORMCK_ORDC
+#endif
             if (persistent) {
                 if (lens) STORMCK_ORD(kSkewTiles, true);
                 else STORMCK_ORD(kSkewTiles, false);

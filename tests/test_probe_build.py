@@ -20,7 +20,7 @@ PROBE_KNOBS = {"STORMCK_STAGE_PIPE", "STORMCK_WIDE16", "STORMCK_WIDE_MULTI", "ST
                "STORMCK_MID_WAVES", "STORMCK_BIG_W", "STORMCK_QUAD_SPREAD", "STORMCK_GATHER_ORDER",
                "STORMCK_COMMIT_WIDE", "STORMCK_COMMIT_MULTI", "STORMCK_COMMIT_MIDW", "STORMCK_COMMIT_CHUNKS",
                "STORMCK_POINTER_RING", "STORMCK_POINTER_C", "STORMCK_POINTER_SIMD", "STORMCK_SINGLE_GPU_MIN",
-               "STORMCK_GATHER_RANK"}
+               "STORMCK_GATHER_RANK", "STORMCK_GATHER_CONTIG"}
 
 
 def _env_strings(path):
