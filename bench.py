@@ -71,7 +71,7 @@ def parse():
     p.add_argument("--gather-order", default="shuffled", choices=["shuffled", "sequential"],
                    help="gather workload: slot order (storm's cache slots are spread by addressingOffsets)")
     p.add_argument("--gather-lens", type=int, default=0, help="gather workload: one length for every block (A/B)")
-    p.add_argument("--workload", default="c3", choices=["c3", "commit", "keytags", "c5", "gather", "commit_e2e"],
+    p.add_argument("--workload", default="c3", choices=["c3", "commit", "keytags", "c5", "gather", "commit_e2e", "batch_e2e"],
                    help="c3 = BASELINE metric (default); commit = f1 level-synchronous Cache.Commit of a dirty "
                         "forest; keytags = f4 xxhash.Sum64 of 48-byte keys")
     p.add_argument("--commit-leaves", type=int, default=1 << 20)
@@ -475,6 +475,107 @@ def commit_e2e_workload(a):
     return 0 if all(r["agree"] for r in rows) else 3
 
 
+def batch_e2e_workload(a):
+    """Host-memory batches end to end (the Go shim's ChecksumBatch / VerifyChecksumBatch),
+    by leg:
+      dev          stormck_checksum_host on pageable memory (staged through pinned buffers,
+                   H2D / kernel / D2H pipelined),
+      dev_reg      the same on memory registered with stormck_host_register (DMA in place),
+      host_1       stormck_checksum_host_leg on 1 thread (storm's serial xxhash.Sum64 loop
+                   costs about twice this: one scalar chain per block),
+      host_all     stormck_checksum_host_leg on every usable thread,
+      routed       stormck_checksum_batch (the library's choice), pool threads,
+      routed_1     the same with one host thread allowed (host cores kept for storm).
+    Batches: storm's c5 commit batch (1,200 objectlist leaves + a pointer block + the
+    singularity, keystore/benchmark_test.go:58-62), the c1 batch (1K x 32 KiB), 3 blocks,
+    a `-tags test` batch (100 blocks of 536 / 728 B, storm_test.go:131-138), 16K and 256K
+    blocks of 32 KiB (512 MiB, 8 GiB). Every leg's checksums must agree. One line per
+    batch with the table (median us per call over --steps reps)."""
+    import ctypes
+    import numpy as np
+    import torch
+    from storm_amd import _lib
+    from storm_amd import engine
+
+    torch.cuda.set_device(0)
+    engine.init(0)
+    L = _lib.lib
+    c5 = np.array([31808] * 1200 + [30000, 72], dtype=np.uint32)
+    shapes = [
+        ("c5_keystore", 1202, c5),
+        ("c1_1k", 1024, 32768),
+        ("three_blocks", 3, np.array([31808, 31808, 30000], dtype=np.uint32)),
+        ("test_tag", 100, np.array([536, 728] * 50, dtype=np.uint32)),
+        ("blocks_16k", 16384, 32768),
+        ("blocks_256k", 262144, 32768),
+    ]
+    threads = host_cpu_info()["usable_cpus"]
+    reps = max(3, a.steps)
+    rows = []
+    for name, n, lens in shapes:
+        stride = BLOCK
+        raw = np.zeros(n * stride + 4096, dtype=np.uint8)
+        off = (-raw.ctypes.data) % 4096
+        buf = raw[off:off + n * stride]
+        for lo in range(0, n, 16384):  # synthetic blocks, generated on the device in slices
+            hi = min(n, lo + 16384)
+            buf[lo * stride:hi * stride] = engine_fill_host(hi - lo, stride)
+        la = lens if isinstance(lens, np.ndarray) else None
+        ln = 0 if la is not None else int(lens)
+        lp = la.ctypes.data if la is not None else None
+        hashed = int(la.sum()) if la is not None else n * ln
+        outs, legs = {}, {}
+
+        def run(leg):
+            out = np.zeros(n, dtype=np.uint64)
+            op = out.ctypes.data
+            t0 = time.perf_counter()
+            if leg in ("dev", "dev_reg"):
+                rc = L.stormck_checksum_host(buf.ctypes.data, stride, lp, ln, n, op)
+            elif leg == "host_1":
+                rc = L.stormck_checksum_host_leg(buf.ctypes.data, stride, lp, ln, n, op, 1)
+            elif leg == "host_all":
+                rc = L.stormck_checksum_host_leg(buf.ctypes.data, stride, lp, ln, n, op, threads)
+            else:
+                used = ctypes.c_uint32(9)
+                rc = L.stormck_checksum_batch(buf.ctypes.data, stride, lp, ln, n, op, 1 if leg == "routed_1" else 0,
+                                              ctypes.byref(used))
+                legs[leg] = {1: "host", 2: "device"}.get(int(used.value), int(used.value))
+            dt = time.perf_counter() - t0
+            _lib.check(rc)
+            return dt, out
+
+        row = {"batch": name, "blocks": n, "hashed_bytes": hashed}
+        for leg in ("dev", "host_1", "host_all", "routed", "routed_1", "dev_reg"):
+            if leg == "dev_reg":
+                _lib.check(L.stormck_host_register(buf.ctypes.data, buf.nbytes))
+            for _ in range(2):
+                run(leg)
+            ts = []
+            for _ in range(reps if hashed < (4 << 30) else 3):
+                dt, out = run(leg)
+                ts.append(dt)
+            ts.sort()
+            med = ts[len(ts) // 2]
+            row[leg + "_us"] = round(med * 1e6, 1)
+            row[leg + "_GiBps"] = round(hashed / med / 2**30, 2)
+            outs[leg] = out
+        _lib.check(L.stormck_host_unregister(buf.ctypes.data))
+        row["routed_leg"], row["routed_1_leg"] = legs.get("routed"), legs.get("routed_1")
+        row["agree"] = all(np.array_equal(outs["host_1"], outs[k]) for k in outs)
+        rows.append(row)
+        print(json.dumps(row), flush=True)
+        del raw, buf
+    res = {"metric": "us per host-memory batch checksum (ChecksumBatch E2E), by leg",
+           "value": rows[0]["routed_us"], "unit": "us", "n_gpus": 1, "steps": reps, "warmup": 2,
+           "higher_is_better": False, "scaling": "weak", "vs_baseline": None, "dtype": "u64", "data": "synthetic",
+           "config": {"workload": "host-memory batches, pageable unless dev_reg; value = routed c5_keystore",
+                      "host_threads": threads, "host": host_cpu_info()},
+           "table": rows}
+    print(json.dumps(res), flush=True)
+    return 0 if all(r["agree"] for r in rows) else 3
+
+
 def engine_fill_host(n: int, stride: int):
     """n synthetic blocks (SURVEY §8d generator) as host bytes: the library's device
     generator, copied back."""
@@ -753,6 +854,8 @@ def main():
         rc = gather_workload(a)
     elif a.workload == "commit_e2e":
         rc = commit_e2e_workload(a)
+    elif a.workload == "batch_e2e":
+        rc = batch_e2e_workload(a)
     else:
         rc = block_checksum_workload(a)
     if rc:

@@ -12,8 +12,10 @@
 // Single calls (Checksum, BlockChecksum, VerifyChecksum) hash on the calling thread
 // through stormck_xxh64, the library's single-call leg: one buffer is four serial
 // XXH64 chains, which one host core walks faster than the GPU, and like
-// Go's Checksum it cannot fail. Batches run on the gfx950 device; a device failure
-// throws storm::blocks::DeviceError. ChecksumGPU is the single call on the device.
+// Go's Checksum it cannot fail. Batches run on the gfx950 device, or on the library's
+// host leg when its cost model predicts the PCIe link makes the device slower for a
+// host-memory batch; they need a device either way, and a failure throws
+// storm::blocks::DeviceError. ChecksumGPU / ChecksumBatchGPU are the device legs alone.
 #pragma once
 
 #include <cstddef>
@@ -105,9 +107,19 @@ inline std::optional<Error> VerifyChecksum(BlockAddress address, const void* p, 
                  ", expected: " + detail::go_hex(expectedChecksum));
 }
 
-// Batched checksums of n host blocks at base + i*stride (length bytes each, or lens[i]).
+// Batched checksums of n host blocks at base + i*stride (length bytes each, or lens[i]),
+// routed by the library's cost model (stormck_checksum_batch): the device over PCIe or
+// its host leg on host_threads threads (0 = the pool), whichever it predicts is faster.
 inline std::vector<Hash> ChecksumBatch(const void* base, size_t n, size_t stride, uint32_t length,
-                                       const uint32_t* lens = nullptr) {
+                                       const uint32_t* lens = nullptr, uint32_t host_threads = 0) {
+    std::vector<Hash> out(n);
+    if (n) detail::check(stormck_checksum_batch(base, stride, lens, length, n, out.data(), host_threads, nullptr));
+    return out;
+}
+
+// The device leg alone (stormck_checksum_host: H2D, kernel, D2H pipelined).
+inline std::vector<Hash> ChecksumBatchGPU(const void* base, size_t n, size_t stride, uint32_t length,
+                                          const uint32_t* lens = nullptr) {
     std::vector<Hash> out(n);
     if (n) detail::check(stormck_checksum_host(base, stride, lens, length, n, out.data()));
     return out;
@@ -118,11 +130,14 @@ struct VerifyResult {
     uint64_t n_bad;
 };
 
+// Routed as ChecksumBatch (stormck_verify_batch).
 inline VerifyResult VerifyChecksumBatch(const void* base, size_t n, size_t stride, uint32_t length,
-                                        const Hash* expected, const uint32_t* lens = nullptr) {
+                                        const Hash* expected, const uint32_t* lens = nullptr,
+                                        uint32_t host_threads = 0) {
     VerifyResult r{n, 0};
     if (!n) return r;
-    const int rc = stormck_verify_host(base, stride, lens, length, n, expected, &r.first_bad, &r.n_bad);
+    const int rc =
+        stormck_verify_batch(base, stride, lens, length, n, expected, &r.first_bad, &r.n_bad, host_threads, nullptr);
     if (rc != STORMCK_OK && rc != STORMCK_EMISMATCH) throw DeviceError(rc);
     return r;
 }

@@ -20,10 +20,15 @@
  * memory (H2D -> kernel -> D2H, pipelined).
  *
  * There is no CPU fallback: without a usable gfx950 device every batched, device
- * and Merkle entry point returns STORMCK_ENODEV. The one host computation is the
- * latency leg of a SINGLE call (stormck_xxh64 / stormck_checksum): one buffer is four
- * serial XXH64 chains, which one host core walks faster than the GPU at every length
- * (DESIGN.md §5), so single calls stay on the host by design.
+ * and Merkle entry point returns STORMCK_ENODEV. Host computation is a measured leg,
+ * never a substitute for a missing device:
+ *  - the latency leg of a SINGLE call (stormck_xxh64 / stormck_checksum): one buffer is
+ *    four serial XXH64 chains, which one host core walks faster than the GPU at every
+ *    length, so single calls stay on the host by design;
+ *  - the host legs of data that lives in HOST memory (stormck_commit_host,
+ *    stormck_checksum_host_leg), which the routed entry points (stormck_commit,
+ *    stormck_checksum_batch) pick when the cost model, fitted to end-to-end tables measured
+ *    on MI355X, predicts they beat the PCIe-bound device leg.
  */
 #ifndef STORMCK_H
 #define STORMCK_H
@@ -35,7 +40,7 @@
 extern "C" {
 #endif
 
-#define STORMCK_ABI_VERSION 3
+#define STORMCK_ABI_VERSION 4
 
 #define STORMCK_OK 0
 #define STORMCK_EINVAL (-1)  /* bad argument (null pointer, n/len/stride out of range, ...) */
@@ -158,6 +163,27 @@ int stormck_checksum_host_multi(const void* base, uint64_t stride, const uint32_
 int stormck_verify_host_multi(const void* base, uint64_t stride, const uint32_t* lens, uint32_t len, uint64_t n,
                               const uint64_t* expected, uint64_t* first_bad, uint64_t* n_bad, const int* devices,
                               int n_devices);
+/* A host-memory batch routed by cost (the Go shim's ChecksumBatch / VerifyChecksumBatch).
+ * Over PCIe the device leg (stormck_checksum_host / stormck_verify_host) moves about
+ * 52 GiB/s end to end, while host threads hash the same bytes four blocks at a time
+ * (AVX-512) until host memory bandwidth binds: stormck_checksum_batch runs each batch on
+ * the leg the library's measured cost model predicts is faster ("Host-memory
+ * batches, routed"), as stormck_commit does for a commit. host_threads: threads the host
+ * leg may use (0 = the library pool, at most 16; 1 = keep the other cores for the caller).
+ * *leg_used (optional) = STORMCK_LEG_HOST / STORMCK_LEG_DEVICE. Same arguments, results
+ * and errors as the _host calls; device memory is STORMCK_EINVAL (use _device). Needs a
+ * gfx950 device like every batched entry point (STORMCK_ENODEV without one).
+ * stormck_checksum_host_leg / stormck_verify_host_leg: the host leg alone, on `threads`
+ * pool threads (0 = the pool); needs no device. */
+int stormck_checksum_batch(const void* base, uint64_t stride, const uint32_t* lens, uint32_t len, uint64_t n,
+                           uint64_t* out, uint32_t host_threads, uint32_t* leg_used);
+int stormck_verify_batch(const void* base, uint64_t stride, const uint32_t* lens, uint32_t len, uint64_t n,
+                         const uint64_t* expected, uint64_t* first_bad, uint64_t* n_bad, uint32_t host_threads,
+                         uint32_t* leg_used);
+int stormck_checksum_host_leg(const void* base, uint64_t stride, const uint32_t* lens, uint32_t len, uint64_t n,
+                              uint64_t* out, uint32_t threads);
+int stormck_verify_host_leg(const void* base, uint64_t stride, const uint32_t* lens, uint32_t len, uint64_t n,
+                            const uint64_t* expected, uint64_t* first_bad, uint64_t* n_bad, uint32_t threads);
 /* ---- single calls (Go blocks.Checksum / BlockChecksum / VerifyChecksum, one block)
  * stormck_xxh64: XXH64 seed 0 of p[0..n_bytes) on the calling host thread; cannot
  * fail (p may be NULL only when n_bytes == 0). What the Go shim's Checksum calls.

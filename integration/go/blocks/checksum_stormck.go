@@ -13,7 +13,9 @@
 // what xxhash.Sum64 costs them today, and like Sum64 the call cannot fail.
 // ChecksumBatch / VerifyChecksumBatch / ReadVerifyBatch / CommitBatch are additions
 // for batched callers (level-synchronous commit, batched cold-read verify): those
-// run on the MI355X (gfx950).
+// run on the MI355X (gfx950), except that a batch or commit in host memory takes the
+// library's host leg when its measured cost model predicts that the PCIe link would
+// make the GPU slower (ChecksumBatch, CommitBatch).
 //
 // Not compiled in this repository (no Go toolchain in the build image); the C
 // side it binds is exercised by tests/test_abi.py and tests/test_cpp_mirror.py.
@@ -71,13 +73,39 @@ func VerifyChecksum(address BlockAddress, p []byte, expectedChecksum Hash) error
 		address, checksum, expectedChecksum)
 }
 
+// BatchHostThreads is the number of host threads the host leg of ChecksumBatch and
+// VerifyChecksumBatch may use (0 = the library's pool, up to 16). It also steers the leg
+// choice: with fewer host threads the device leg wins sooner (DESIGN.md §5, "Host-memory
+// batches, routed").
+var BatchHostThreads uint32
+
 // ChecksumBatch computes checksums of n blocks at data[i*stride:], length bytes each.
+// The blocks live in host memory, so libstormck routes the batch (stormck_checksum_batch)
+// to whichever leg its measured cost model predicts is faster: the GPU, through the PCIe
+// link (ChecksumBatchGPU), or its host leg on BatchHostThreads threads. Both are bit-exact.
 func ChecksumBatch(data []byte, n, stride, length int, out []Hash) error {
 	if n == 0 {
 		return nil
 	}
 	if len(out) < n || len(data) < (n-1)*stride+length {
 		return errors.New("ChecksumBatch: buffer too small")
+	}
+	rc := C.stormck_checksum_batch(bytesPtr(data), C.uint64_t(stride), nil, C.uint32_t(length), C.uint64_t(n),
+		(*C.uint64_t)(unsafe.Pointer(&out[0])), C.uint32_t(BatchHostThreads), nil)
+	if rc != C.STORMCK_OK {
+		return stormckError(rc)
+	}
+	return nil
+}
+
+// ChecksumBatchGPU is ChecksumBatch on the GPU leg alone (stormck_checksum_host: H2D,
+// kernel and D2H pipelined on the current device).
+func ChecksumBatchGPU(data []byte, n, stride, length int, out []Hash) error {
+	if n == 0 {
+		return nil
+	}
+	if len(out) < n || len(data) < (n-1)*stride+length {
+		return errors.New("ChecksumBatchGPU: buffer too small")
 	}
 	rc := C.stormck_checksum_host(bytesPtr(data), C.uint64_t(stride), nil, C.uint32_t(length), C.uint64_t(n),
 		(*C.uint64_t)(unsafe.Pointer(&out[0])))
@@ -107,7 +135,8 @@ func ChecksumBatchDevices(data []byte, n, stride, length int, out []Hash, device
 }
 
 // VerifyChecksumBatch verifies n blocks; it returns the first mismatching index
-// (n when all match) and the number of mismatches.
+// (n when all match) and the number of mismatches. Routed as ChecksumBatch
+// (stormck_verify_batch).
 func VerifyChecksumBatch(data []byte, n, stride, length int, expected []Hash) (firstBad, nBad int, err error) {
 	if n == 0 {
 		return 0, 0, nil
@@ -116,8 +145,8 @@ func VerifyChecksumBatch(data []byte, n, stride, length int, expected []Hash) (f
 		return 0, 0, errors.New("VerifyChecksumBatch: buffer too small")
 	}
 	var fb, nb C.uint64_t
-	rc := C.stormck_verify_host(bytesPtr(data), C.uint64_t(stride), nil, C.uint32_t(length), C.uint64_t(n),
-		(*C.uint64_t)(unsafe.Pointer(&expected[0])), &fb, &nb)
+	rc := C.stormck_verify_batch(bytesPtr(data), C.uint64_t(stride), nil, C.uint32_t(length), C.uint64_t(n),
+		(*C.uint64_t)(unsafe.Pointer(&expected[0])), &fb, &nb, C.uint32_t(BatchHostThreads), nil)
 	if rc != C.STORMCK_OK && rc != C.STORMCK_EMISMATCH {
 		return 0, 0, stormckError(rc)
 	}
@@ -241,7 +270,7 @@ func CommitBatch(arena []byte, dirty []DirtyBlock, revision uint64, lastAllocate
 	return uint32(used), nil
 }
 
-// Legs of CommitBatch (STORMCK_LEG_*).
+// Legs of CommitBatch and the routed batches (STORMCK_LEG_*).
 const (
 	LegNone   = uint32(C.STORMCK_LEG_NONE)
 	LegHost   = uint32(C.STORMCK_LEG_HOST)

@@ -12,6 +12,6 @@ from them, and per-shard roots gathered over RCCL. Submodules:
 * ``build``    — in-tree hipcc build of libstormck.so
 """
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 __all__ = ["ABI_VERSION"]

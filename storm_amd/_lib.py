@@ -26,7 +26,7 @@ EMISMATCH = -5
 ALLOC_PLAIN = 0       # STORMCK_ALLOC_* (include/stormck.h): arena placement modes
 ALLOC_VMM = 1
 ALLOC_CONTIGUOUS = 2
-LEG_NONE, LEG_HOST, LEG_DEVICE = 0, 1, 2  # STORMCK_LEG_* (stormck_commit)
+LEG_NONE, LEG_HOST, LEG_DEVICE = 0, 1, 2  # STORMCK_LEG_* (stormck_commit, stormck_checksum_batch)
 
 
 class StormckError(RuntimeError):
@@ -68,6 +68,14 @@ SIGNATURES = {
         c_int, [c_void_p, c_uint64, c_void_p, c_uint32, c_uint64, c_void_p, c_void_p, c_int]),
     "stormck_verify_host_multi": (
         c_int, [c_void_p, c_uint64, c_void_p, c_uint32, c_uint64, c_void_p, c_void_p, c_void_p, c_void_p, c_int]),
+    "stormck_checksum_batch": (
+        c_int, [c_void_p, c_uint64, c_void_p, c_uint32, c_uint64, c_void_p, c_uint32, POINTER(c_uint32)]),
+    "stormck_verify_batch": (
+        c_int, [c_void_p, c_uint64, c_void_p, c_uint32, c_uint64, c_void_p, c_void_p, c_void_p, c_uint32,
+                POINTER(c_uint32)]),
+    "stormck_checksum_host_leg": (c_int, [c_void_p, c_uint64, c_void_p, c_uint32, c_uint64, c_void_p, c_uint32]),
+    "stormck_verify_host_leg": (
+        c_int, [c_void_p, c_uint64, c_void_p, c_uint32, c_uint64, c_void_p, c_void_p, c_void_p, c_uint32]),
     "stormck_xxh64": (c_uint64, [c_void_p, c_uint64]),
     "stormck_checksum": (c_int, [c_void_p, c_uint64, POINTER(c_uint64)]),
     "stormck_checksum_gpu": (c_int, [c_void_p, c_uint64, POINTER(c_uint64)]),

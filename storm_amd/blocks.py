@@ -13,8 +13,10 @@ Same names, argument meaning and error behaviour as the reference:
 
 plus the batch entry points the GPU path exists for (``ChecksumBatch``,
 ``VerifyChecksumBatch``, ``ReadVerifyBatch``; f1's batched commit is in
-``storm_amd.commit``). Batches run on the gfx950 kernels in libstormck and fail
-loudly without a device. A single ``Checksum`` is one buffer, four serial XXH64
+``storm_amd.commit``). Batches fail loudly without a device. A batch in host memory
+is routed by the library's measured cost model, as the commit is: the gfx950 kernels
+over PCIe (``ChecksumBatchGPU``) or host threads (``ChecksumBatchHost``), whichever is
+faster for it. A single ``Checksum`` is one buffer, four serial XXH64
 chains: libstormck hashes it on the calling host thread (stormck_checksum, the
 latency leg SURVEY.md §8b specifies; measured faster than the device single call at
 every length). ``ChecksumGPU`` is the same call through the device
@@ -125,20 +127,58 @@ def _devices_arg(devices: Optional[Sequence[int]]):
     return d
 
 
-def ChecksumBatch(buf, n: int, stride: int, length: Optional[int] = None,
-                  lens: Optional[Sequence[int]] = None, devices: Optional[Sequence[int]] = None) -> np.ndarray:
-    """Checksums of ``n`` host blocks at ``buf + i*stride`` (``length`` bytes each or
-    ``lens[i]``). H2D -> gfx950 kernel -> D2H. Returns uint64[n]. ``devices``: spread
-    the batch over these devices in contiguous ranges, one host thread each
-    (stormck_checksum_host_multi); default: the current device."""
+def _batch_args(buf, n: int, stride: int, length, lens):
     a = _as_u8(buf)
     la, ln = _lens_arg(n, length, lens)
     if n and a.size < (n - 1) * stride + (int(la.max()) if la is not None else ln):
         raise ValueError("buffer too small for n blocks")
+    return a, la, ln, (la.ctypes.data if la is not None else None)
+
+
+def _expected_arg(n: int, expected) -> np.ndarray:
+    exp = np.ascontiguousarray(np.asarray(expected, dtype=np.uint64))
+    if exp.size != n:
+        raise ValueError("expected must have one entry per block")
+    return exp
+
+
+def ChecksumBatchLeg(buf, n: int, stride: int, length: Optional[int] = None,
+                     lens: Optional[Sequence[int]] = None, host_threads: int = 0) -> Tuple[np.ndarray, int]:
+    """ChecksumBatch, also returning the leg the library took (_lib.LEG_HOST /
+    LEG_DEVICE; LEG_NONE for an empty batch)."""
+    a, la, ln, lp = _batch_args(buf, n, stride, length, lens)
+    out = np.zeros(n, dtype=np.uint64)
+    leg = ctypes.c_uint32(_lib.LEG_NONE)
+    if n == 0:
+        return out, leg.value
+    _lib.check(_lib.lib.stormck_checksum_batch(a.ctypes.data, stride, lp, ln, n, out.ctypes.data, host_threads,
+                                               ctypes.byref(leg)))
+    return out, leg.value
+
+
+def ChecksumBatch(buf, n: int, stride: int, length: Optional[int] = None,
+                  lens: Optional[Sequence[int]] = None, devices: Optional[Sequence[int]] = None,
+                  host_threads: int = 0) -> np.ndarray:
+    """Checksums of ``n`` host blocks at ``buf + i*stride`` (``length`` bytes each or
+    ``lens[i]``). Returns uint64[n]. The library routes the batch (stormck_checksum_batch):
+    the device leg over PCIe (ChecksumBatchGPU) or the host leg on ``host_threads``
+    threads (ChecksumBatchHost; 0 = the library pool), whichever its measured cost model
+    predicts is faster. ``devices``: hash on these devices in contiguous ranges, one host
+    thread each (stormck_checksum_host_multi) instead of routing."""
+    if devices is not None:
+        return ChecksumBatchGPU(buf, n, stride, length, lens, devices)
+    return ChecksumBatchLeg(buf, n, stride, length, lens, host_threads)[0]
+
+
+def ChecksumBatchGPU(buf, n: int, stride: int, length: Optional[int] = None,
+                     lens: Optional[Sequence[int]] = None, devices: Optional[Sequence[int]] = None) -> np.ndarray:
+    """The device leg of ChecksumBatch: H2D -> gfx950 kernel -> D2H, pipelined
+    (stormck_checksum_host); ``devices``: spread over these devices
+    (stormck_checksum_host_multi); default: the current device."""
+    a, la, ln, lp = _batch_args(buf, n, stride, length, lens)
     out = np.zeros(n, dtype=np.uint64)
     if n == 0:
         return out
-    lp = la.ctypes.data if la is not None else None
     d = _devices_arg(devices)
     if d is None:
         _lib.check(_lib.lib.stormck_checksum_host(a.ctypes.data, stride, lp, ln, n, out.ctypes.data))
@@ -147,20 +187,56 @@ def ChecksumBatch(buf, n: int, stride: int, length: Optional[int] = None,
     return out
 
 
+def ChecksumBatchHost(buf, n: int, stride: int, length: Optional[int] = None,
+                      lens: Optional[Sequence[int]] = None, threads: int = 0) -> np.ndarray:
+    """The host leg of ChecksumBatch (stormck_checksum_host_leg): the blocks hashed on
+    ``threads`` library pool threads (0 = the pool), four at a time with AVX-512; needs
+    no device."""
+    a, la, ln, lp = _batch_args(buf, n, stride, length, lens)
+    out = np.zeros(n, dtype=np.uint64)
+    if n:
+        _lib.check(_lib.lib.stormck_checksum_host_leg(a.ctypes.data, stride, lp, ln, n, out.ctypes.data, threads))
+    return out
+
+
+def _verify_rc(rc: int, fb, nb) -> Tuple[int, int]:
+    if rc != _lib.EMISMATCH:
+        _lib.check(rc)
+    return fb.value, nb.value
+
+
+def VerifyChecksumBatchLeg(buf, n: int, stride: int, expected: Sequence[int], length: Optional[int] = None,
+                           lens: Optional[Sequence[int]] = None, host_threads: int = 0) -> Tuple[int, int, int]:
+    """VerifyChecksumBatch, also returning the leg taken: (first_bad, n_bad, leg)."""
+    a, la, ln, lp = _batch_args(buf, n, stride, length, lens)
+    exp = _expected_arg(n, expected)
+    if n == 0:
+        return 0, 0, _lib.LEG_NONE
+    fb, nb, leg = ctypes.c_uint64(0), ctypes.c_uint64(0), ctypes.c_uint32(_lib.LEG_NONE)
+    rc = _lib.lib.stormck_verify_batch(a.ctypes.data, stride, lp, ln, n, exp.ctypes.data, ctypes.byref(fb),
+                                       ctypes.byref(nb), host_threads, ctypes.byref(leg))
+    return _verify_rc(rc, fb, nb) + (leg.value,)
+
+
 def VerifyChecksumBatch(buf, n: int, stride: int, expected: Sequence[int], length: Optional[int] = None,
                         lens: Optional[Sequence[int]] = None,
-                        devices: Optional[Sequence[int]] = None) -> Tuple[int, int]:
+                        devices: Optional[Sequence[int]] = None, host_threads: int = 0) -> Tuple[int, int]:
     """Batched VerifyChecksum. Returns (first_bad, n_bad); first_bad == n when all match.
-    ``devices`` as in ChecksumBatch."""
-    a = _as_u8(buf)
-    la, ln = _lens_arg(n, length, lens)
-    exp = np.ascontiguousarray(np.asarray(expected, dtype=np.uint64))
-    if exp.size != n:
-        raise ValueError("expected must have one entry per block")
+    Routed as ChecksumBatch (stormck_verify_batch); ``devices`` as in ChecksumBatch."""
+    if devices is not None:
+        return VerifyChecksumBatchGPU(buf, n, stride, expected, length, lens, devices)
+    return VerifyChecksumBatchLeg(buf, n, stride, expected, length, lens, host_threads)[:2]
+
+
+def VerifyChecksumBatchGPU(buf, n: int, stride: int, expected: Sequence[int], length: Optional[int] = None,
+                           lens: Optional[Sequence[int]] = None,
+                           devices: Optional[Sequence[int]] = None) -> Tuple[int, int]:
+    """The device leg of VerifyChecksumBatch (stormck_verify_host / _host_multi)."""
+    a, la, ln, lp = _batch_args(buf, n, stride, length, lens)
+    exp = _expected_arg(n, expected)
     if n == 0:
         return 0, 0
     fb, nb = ctypes.c_uint64(0), ctypes.c_uint64(0)
-    lp = la.ctypes.data if la is not None else None
     d = _devices_arg(devices)
     if d is None:
         rc = _lib.lib.stormck_verify_host(a.ctypes.data, stride, lp, ln, n, exp.ctypes.data, ctypes.byref(fb),
@@ -168,9 +244,20 @@ def VerifyChecksumBatch(buf, n: int, stride: int, expected: Sequence[int], lengt
     else:
         rc = _lib.lib.stormck_verify_host_multi(a.ctypes.data, stride, lp, ln, n, exp.ctypes.data, ctypes.byref(fb),
                                                 ctypes.byref(nb), d, len(d))
-    if rc != _lib.EMISMATCH:
-        _lib.check(rc)
-    return fb.value, nb.value
+    return _verify_rc(rc, fb, nb)
+
+
+def VerifyChecksumBatchHost(buf, n: int, stride: int, expected: Sequence[int], length: Optional[int] = None,
+                            lens: Optional[Sequence[int]] = None, threads: int = 0) -> Tuple[int, int]:
+    """The host leg of VerifyChecksumBatch (stormck_verify_host_leg); needs no device."""
+    a, la, ln, lp = _batch_args(buf, n, stride, length, lens)
+    exp = _expected_arg(n, expected)
+    if n == 0:
+        return 0, 0
+    fb, nb = ctypes.c_uint64(0), ctypes.c_uint64(0)
+    rc = _lib.lib.stormck_verify_host_leg(a.ctypes.data, stride, lp, ln, n, exp.ctypes.data, ctypes.byref(fb),
+                                          ctypes.byref(nb), threads)
+    return _verify_rc(rc, fb, nb)
 
 
 READ_FULL_BLOCK = 1  # STORMCK_READ_FULL_BLOCK

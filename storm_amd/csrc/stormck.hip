@@ -2543,6 +2543,192 @@ int stormck_commit(void* arena, stormck_dirty_block* blocks, uint64_t n, uint64_
     return stormck_commit_device(d_arena, blocks, n, revision, last_allocated_block, out_checksums, stream);
 }
 
+// ---- host-memory batches: the host leg and the routed batch ------------------------
+// A batch that lives in host memory (the Go shim's ChecksumBatch / VerifyChecksumBatch)
+// crosses the PCIe link on the device leg (stormck_checksum_host: ~52 GiB/s end to end,
+// DESIGN.md §5), while the host's own threads hash the same bytes four blocks at a time
+// (AVX-512) until host memory bandwidth binds. stormck_checksum_batch routes each batch
+// to the leg the cost model below predicts is faster, as stormck_commit routes a commit.
+namespace {
+// The 16-thread host leg reads host memory at about this rate on the MI355X box's EPYC
+// 9575F (its 128K-leaf commit: 4.3 GB in 14.5 ms; the batch table in
+// §5 "Host-memory batches, routed"), below 16 x kHostCoreX4BytesPerUs.
+constexpr double kHostMemBytesPerUs = 280000.0;
+constexpr double kDevBatchCallUs = 16.0;  // stage, launch, copy back, sync of one small pipelined batch
+
+struct BatchShape {
+    uint64_t bytes = 0, longest = 0;
+};
+
+// Bytes hashed and the longest block; false: blocks overlap (stride below a length).
+bool batch_shape(uint64_t stride, const uint32_t* lens, uint32_t len, uint64_t n, BatchShape* s) {
+    if (lens) {
+        for (uint64_t i = 0; i < n; ++i) {
+            s->bytes += lens[i];
+            s->longest = std::max<uint64_t>(s->longest, lens[i]);
+        }
+    } else {
+        s->bytes = uint64_t{len} * n;
+        s->longest = len;
+    }
+    return n <= 1 || stride >= s->longest;
+}
+
+unsigned batch_threads(const BatchShape& s, unsigned nt) {
+    return static_cast<unsigned>(std::min<uint64_t>(nt, std::max<uint64_t>(1, s.bytes / kHostMinBytesPerThread)));
+}
+
+double batch_host_us(const BatchShape& s, unsigned nt) {
+    const double core = host::has_x4() ? kHostCoreX4BytesPerUs : kHostCoreBytesPerUs;
+    const unsigned pl = batch_threads(s, nt);
+    if (pl == 1) return static_cast<double>(s.bytes) / core;
+    return static_cast<double>(s.bytes) / std::min(core * pl, kHostMemBytesPerUs) + kHostLevelUs;
+}
+
+double batch_device_us(const BatchShape& s) {
+    return kDevBatchCallUs + static_cast<double>(s.longest) / kDevChainBytesPerUs +
+           static_cast<double>(s.bytes) / kLinkBytesPerUs;
+}
+
+// The host leg: blocks in pieces from a shared counter on `threads` pool threads (0 = the
+// pool), four at a time where the CPU has AVX-512. Verify mode (expected != null) counts
+// mismatches and keeps the lowest failing index, as the device kernels do.
+int batch_host_leg(const uint8_t* base, uint64_t stride, const uint32_t* lens, uint32_t len, uint64_t n,
+                   uint64_t* out, const uint64_t* expected, uint64_t* first_bad, uint64_t* n_bad, unsigned threads) {
+    BatchShape s;
+    if (!batch_shape(stride, lens, len, n, &s)) return fail(STORMCK_EINVAL, "stride smaller than a block length (blocks overlap)");
+    ForkJoin& fj = ForkJoin::get();
+    const unsigned nt = threads ? std::min<unsigned>(threads, fj.size()) : fj.size();
+    const unsigned pl = batch_threads(s, nt);
+    const uint64_t piece = std::max<uint64_t>(4, (n / (uint64_t{pl} * 8) + 3) / 4 * 4);
+    std::atomic<uint64_t> next{0}, bad_n{0}, bad_first{n};
+    auto work = [&](unsigned) {
+        uint64_t my_n = 0, my_first = n;
+        auto take = [&](uint64_t i, uint64_t h) {
+            if (!expected) {
+                out[i] = h;
+            } else if (h != expected[i]) {
+                ++my_n;
+                my_first = std::min(my_first, i);
+            }
+        };
+        for (;;) {
+            const uint64_t i0 = next.fetch_add(piece, std::memory_order_relaxed);
+            if (i0 >= n) break;
+            const uint64_t i1 = std::min(n, i0 + piece);
+            uint64_t i = i0;
+            for (; host::has_x4() && i + 4 <= i1; i += 4) {
+                const unsigned char* p4[4];
+                size_t n4[4];
+                uint64_t h4[4];
+                for (int q = 0; q < 4; ++q) {
+                    p4[q] = base + (i + q) * stride;
+                    n4[q] = lens ? lens[i + q] : len;
+                }
+                host::xxh64_x4(p4, n4, h4);
+                for (int q = 0; q < 4; ++q) take(i + q, h4[q]);
+            }
+            for (; i < i1; ++i) take(i, host::xxh64(base + i * stride, lens ? lens[i] : len));
+        }
+        if (my_n) {
+            bad_n.fetch_add(my_n, std::memory_order_relaxed);
+            uint64_t cur = bad_first.load(std::memory_order_relaxed);
+            while (my_first < cur && !bad_first.compare_exchange_weak(cur, my_first, std::memory_order_relaxed)) {
+            }
+        }
+    };
+    fj.run(static_cast<unsigned>(std::min<uint64_t>(pl, (n + piece - 1) / piece)), work);
+    if (first_bad) *first_bad = bad_first.load();
+    if (n_bad) *n_bad = bad_n.load();
+    return STORMCK_OK;
+}
+
+// Host arguments of the batch entry points, checked the same way for both legs.
+int batch_args(const void* base, uint64_t n, const uint64_t* out_or_expected) {
+    if (n == 0) return STORMCK_OK;
+    if (!base) return fail(STORMCK_EINVAL, "base is null");
+    if (!out_or_expected) return fail(STORMCK_EINVAL, "null argument");
+    return STORMCK_OK;
+}
+
+// Whether `p` is device memory, which host threads cannot read.
+bool on_device(const void* p) {
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return a.type == hipMemoryTypeDevice;
+}
+
+// The routed batch: the leg the cost model predicts is faster (*leg_used).
+int batch_routed(const void* base, uint64_t stride, const uint32_t* lens, uint32_t len, uint64_t n, uint64_t* out,
+                 const uint64_t* expected, uint64_t* first_bad, uint64_t* n_bad, uint32_t host_threads,
+                 uint32_t* leg_used) {
+    if (leg_used) *leg_used = STORMCK_LEG_NONE;
+    int rc = batch_args(base, n, expected ? expected : out);
+    if (rc) return rc;
+    BatchShape s;
+    if (!batch_shape(stride, lens, len, n, &s)) return fail(STORMCK_EINVAL, "stride smaller than a block length (blocks overlap)");
+    rc = device_check();  // a batch entry point of the GPU engine: no device, no batch
+    if (rc) return rc;
+    if (n == 0) {
+        if (first_bad) *first_bad = 0;
+        if (n_bad) *n_bad = 0;
+        return STORMCK_OK;
+    }
+    if (on_device(base)) return fail(STORMCK_EINVAL, "base is device memory: use the _device entry points");
+    const unsigned nt = host_threads ? std::min<unsigned>(host_threads, ForkJoin::get().size()) : ForkJoin::get().size();
+    // the device pipeline stages whole blocks through 256 MiB chunks
+    const uint64_t step = n == 1 ? std::max<uint64_t>(s.longest, 8) : std::max<uint64_t>(stride, 8);
+    const bool device = step <= kChunkBytes && batch_device_us(s) < batch_host_us(s, nt);
+    if (!device) {
+        if (leg_used) *leg_used = STORMCK_LEG_HOST;
+        return batch_host_leg(static_cast<const uint8_t*>(base), stride, lens, len, n, out, expected, first_bad, n_bad, nt);
+    }
+    if (leg_used) *leg_used = STORMCK_LEG_DEVICE;
+    return host_pipeline(base, stride, lens, len, n, out, expected, first_bad, n_bad);
+}
+
+}  // namespace
+
+int stormck_checksum_host_leg(const void* base, uint64_t stride, const uint32_t* lens, uint32_t len, uint64_t n,
+                              uint64_t* out, uint32_t threads) {
+    const int rc = batch_args(base, n, out);
+    if (rc || n == 0) return rc;
+    return batch_host_leg(static_cast<const uint8_t*>(base), stride, lens, len, n, out, nullptr, nullptr, nullptr, threads);
+}
+
+int stormck_verify_host_leg(const void* base, uint64_t stride, const uint32_t* lens, uint32_t len, uint64_t n,
+                            const uint64_t* expected, uint64_t* first_bad, uint64_t* n_bad, uint32_t threads) {
+    if (!first_bad || !n_bad) return fail(STORMCK_EINVAL, "null argument");
+    *first_bad = n;
+    *n_bad = 0;
+    int rc = batch_args(base, n, expected);
+    if (rc || n == 0) return rc;
+    rc = batch_host_leg(static_cast<const uint8_t*>(base), stride, lens, len, n, nullptr, expected, first_bad, n_bad,
+                        threads);
+    if (rc) return rc;
+    if (*n_bad > 0) return fail(STORMCK_EMISMATCH, "checksum mismatch");
+    return STORMCK_OK;
+}
+
+int stormck_checksum_batch(const void* base, uint64_t stride, const uint32_t* lens, uint32_t len, uint64_t n,
+                           uint64_t* out, uint32_t host_threads, uint32_t* leg_used) {
+    return batch_routed(base, stride, lens, len, n, out, nullptr, nullptr, nullptr, host_threads, leg_used);
+}
+
+int stormck_verify_batch(const void* base, uint64_t stride, const uint32_t* lens, uint32_t len, uint64_t n,
+                         const uint64_t* expected, uint64_t* first_bad, uint64_t* n_bad, uint32_t host_threads,
+                         uint32_t* leg_used) {
+    if (leg_used) *leg_used = STORMCK_LEG_NONE;
+    if (!first_bad || !n_bad) return fail(STORMCK_EINVAL, "null argument");
+    const int rc = batch_routed(base, stride, lens, len, n, nullptr, expected, first_bad, n_bad, host_threads, leg_used);
+    if (rc) return rc;
+    if (*n_bad > 0) return fail(STORMCK_EMISMATCH, "checksum mismatch");
+    return STORMCK_OK;
+}
+
 int stormck_fill_synthetic_device(void* d_dst, uint64_t stride, uint64_t n, uint64_t first, uint64_t seed,
                                   void* stream) {
     if (n == 0) return STORMCK_OK;

@@ -170,6 +170,8 @@ static void TestBatch() {
     }
     auto cs = ChecksumBatch(buf.data(), n, stride, stride);
     for (size_t i = 0; i < n; i += 37) EXPECT(cs[i] == Checksum(buf.data() + i * stride, stride));
+    EXPECT(ChecksumBatchGPU(buf.data(), n, stride, stride) == cs);  // the device leg alone
+    EXPECT(ChecksumBatch(buf.data(), n, stride, stride, nullptr, 1) == cs);
     auto ok = VerifyChecksumBatch(buf.data(), n, stride, stride, cs.data());
     EXPECT(ok.first_bad == n && ok.n_bad == 0);
     buf[123 * stride + 7] ^= 1;

@@ -7,6 +7,8 @@
 //   * the single-call leg stormck_xxh64 / stormck_checksum on every length 0..4100 at
 //     every start offset mod 8, against the oracle (out-of-bounds reads show up here);
 //   * argument validation of every entry point (EINVAL before any device work);
+//   * the batch host leg (stormck_checksum_host_leg / _verify_host_leg) from several
+//     caller threads at once, and the routed batch with a device;
 //   * f1 commit planning: validation, the threaded height walk-up (ForkJoin pool),
 //     cycle / range / alignment errors, on shuffled forests up to 300K records;
 //   * with a gfx950 device (GPU box): the same commits run to completion on a device
@@ -263,6 +265,47 @@ static void commit_host_leg(bool device) {
     for (auto& x : th) x.join();
 }
 
+// The batch host leg (no device needed): stormck_checksum_host_leg / _verify_host_leg on
+// exact-size heap copies (a read past a block shows up), per-block lengths 0..stride,
+// unaligned starts, 1 thread and the pool, from several caller threads at once; with a
+// device, the routed stormck_checksum_batch on both host-thread settings.
+static void batch_host_leg(bool device) {
+    auto one = [&](uint64_t n, uint64_t stride, uint64_t off, uint32_t threads, uint64_t seed) {
+        std::mt19937_64 rng(seed);
+        std::vector<uint8_t> buf(n * stride + off);
+        for (auto& c : buf) c = static_cast<uint8_t>(rng());
+        std::vector<uint32_t> lens(n);
+        for (auto& l : lens) l = static_cast<uint32_t>(rng() % (stride + 1));
+        if (n) lens[n - 1] = static_cast<uint32_t>(stride);  // the last block ends at the buffer's end
+        std::vector<uint8_t> exact(buf.begin() + off, buf.end());
+        std::vector<uint64_t> want(n), got(n, 0);
+        for (uint64_t i = 0; i < n; ++i) want[i] = oracle_xxh64(exact.data() + i * stride, lens[i]);
+        CHECK(stormck_checksum_host_leg(exact.data(), stride, lens.data(), 0, n, got.data(), threads) == STORMCK_OK &&
+              got == want);
+        uint64_t fb = 0, nb = 0;
+        auto bad = want;
+        if (n > 2) bad[n / 2] ^= 1;
+        const int rc = stormck_verify_host_leg(exact.data(), stride, lens.data(), 0, n, bad.data(), &fb, &nb, threads);
+        CHECK(n > 2 ? (rc == STORMCK_EMISMATCH && fb == n / 2 && nb == 1) : (rc == STORMCK_OK && nb == 0));
+        if (device) {
+            uint32_t leg = 0;
+            std::fill(got.begin(), got.end(), 0);
+            CHECK(stormck_checksum_batch(exact.data(), stride, lens.data(), 0, n, got.data(), threads, &leg) ==
+                      STORMCK_OK &&
+                  got == want && (n == 0 || leg == STORMCK_LEG_HOST || leg == STORMCK_LEG_DEVICE));
+        }
+    };
+    for (uint64_t n : {uint64_t{0}, uint64_t{1}, uint64_t{3}, uint64_t{4}, uint64_t{7}, uint64_t{1000}})
+        for (uint64_t off : {uint64_t{0}, uint64_t{5}})
+            for (uint32_t threads : {1u, 0u}) one(n, n > 100 ? 4096 : 200, off, threads, 31 + n + off);
+    std::vector<std::thread> th;
+    for (int t = 0; t < 4; ++t)
+        th.emplace_back([&, t] {
+            for (int it = 0; it < 3; ++it) one(700 + 131 * t, 8192, t & 1, it == 2 ? 1u : 0u, 60 + 10 * t + it);
+        });
+    for (auto& x : th) x.join();
+}
+
 static void host_pipeline_paths() {
     std::mt19937_64 rng(3);
     const uint64_t n = 12000, stride = 32768;  // 375 MiB: two 256 MiB pipeline chunks
@@ -397,6 +440,8 @@ int main() {
     std::printf("commit planning: done\n");
     commit_host_leg(device);
     std::printf("commit host leg: done\n");
+    batch_host_leg(device);
+    std::printf("batch host leg: done\n");
     if (device) host_pipeline_paths();
     if (device) concurrent_callers();
     if (device) std::printf("concurrent callers: done\n");

@@ -40,7 +40,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version():
     from storm_amd import _lib, ABI_VERSION
-    assert _lib.lib.stormck_abi_version() == ABI_VERSION == 3
+    assert _lib.lib.stormck_abi_version() == ABI_VERSION == 4
 
 
 def test_library_build_id_is_the_tree_sources_hash():
@@ -131,6 +131,18 @@ def test_argument_errors_precede_the_device_check():
                                                                  (ctypes.c_int * 1)(0), 1)),
         ("verify multi null", lambda: L.stormck_verify_host_multi(1 << 20, 32, None, 32, 4, None, None, None,
                                                                   (ctypes.c_int * 1)(0), 1)),
+        ("batch null base", lambda: L.stormck_checksum_batch(None, 32, None, 32, 4, ctypes.addressof(out), 0, None)),
+        ("batch null out", lambda: L.stormck_checksum_batch(1 << 20, 32, None, 32, 4, None, 0, None)),
+        ("batch overlap", lambda: L.stormck_checksum_batch(1 << 20, 16, None, 32, 4, ctypes.addressof(out), 0, None)),
+        ("verify batch null result", lambda: L.stormck_verify_batch(1 << 20, 32, None, 32, 4, ctypes.addressof(out),
+                                                                    None, None, 0, None)),
+        ("verify batch null expected", lambda: L.stormck_verify_batch(1 << 20, 32, None, 32, 4, None,
+                                                                      ctypes.byref(out), ctypes.byref(out), 0, None)),
+        ("host-leg batch null out", lambda: L.stormck_checksum_host_leg(1 << 20, 32, None, 32, 4, None, 1)),
+        ("host-leg batch overlap", lambda: L.stormck_checksum_host_leg(1 << 20, 16, None, 32, 4,
+                                                                       ctypes.addressof(out), 1)),
+        ("host-leg verify null result", lambda: L.stormck_verify_host_leg(1 << 20, 32, None, 32, 4,
+                                                                          ctypes.addressof(out), None, None, 1)),
         ("read-verify slot", lambda: L.stormck_read_verify_fd(0, (ctypes.c_uint64 * 1)(0), (ctypes.c_uint32 * 1)(100),
                                                               1, 32768, (ctypes.c_uint8 * 64)(), 64,
                                                               (ctypes.c_uint64 * 1)(0), 1, ctypes.byref(out),

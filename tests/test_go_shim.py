@@ -240,3 +240,25 @@ def test_commit_batch_takes_the_routed_commit():
         assert re.search(name + r"\s*=\s*uint32\(C\." + c + r"\)", text), name
     stormck = _go("commit_stormck.go")
     assert "_, err = blocks.CommitBatch(c.data, dirty, sb.Revision, &last, out)" in stormck
+
+
+def _go_func(text, name):
+    body = text[text.index("func " + name + "("):]
+    return body[:body.index("\n}\n")]
+
+
+def test_batches_take_the_routed_batch():
+    """ChecksumBatch / VerifyChecksumBatch hand host blocks to stormck_checksum_batch /
+    stormck_verify_batch, which pick the device or host leg by the measured cost model
+    ("Host-memory batches, routed"); ChecksumBatchGPU keeps the device leg alone
+    and ChecksumBatchDevices the multi-GPU one. The host-thread knob is exported."""
+    text = open(SHIM).read()
+    cb = _go_func(text, "ChecksumBatch")
+    assert "C.stormck_checksum_batch(bytesPtr(data)" in cb and "C.uint32_t(BatchHostThreads)" in cb
+    assert "stormck_checksum_host(" not in cb
+    vb = _go_func(text, "VerifyChecksumBatch")
+    assert "C.stormck_verify_batch(bytesPtr(data)" in vb and "C.uint32_t(BatchHostThreads)" in vb
+    assert "C.STORMCK_EMISMATCH" in vb
+    assert "C.stormck_checksum_host(bytesPtr(data)" in _go_func(text, "ChecksumBatchGPU")
+    assert "C.stormck_checksum_host_multi(" in _go_func(text, "ChecksumBatchDevices")
+    assert re.search(r"var BatchHostThreads uint32", text)

@@ -423,9 +423,9 @@ def test_verify_device_and_host(dev):
     # host path: corrupt one byte of block 123
     host = buf.cpu().numpy().copy()
     exp = _u64(good)
-    assert blocks.VerifyChecksumBatch(host, n, stride, exp, length=stride) == (n, 0)
+    assert blocks.VerifyChecksumBatchGPU(host, n, stride, exp, length=stride) == (n, 0)
     host[123, 5] ^= 0xFF
-    assert blocks.VerifyChecksumBatch(host, n, stride, exp, length=stride) == (123, 1)
+    assert blocks.VerifyChecksumBatchGPU(host, n, stride, exp, length=stride) == (123, 1)
 
 
 def test_host_batch_paths(dev):
@@ -435,14 +435,14 @@ def test_host_batch_paths(dev):
     n, stride = 20000, 32768  # 625 MiB: several 256 MiB pipeline chunks
     host = rng.integers(0, 256, size=(n, stride), dtype=np.uint8)
     want = o.checksum_batch(host, n, stride, stride, threads=8)
-    assert np.array_equal(blocks.ChecksumBatch(host, n, stride, length=stride), want)
+    assert np.array_equal(blocks.ChecksumBatchGPU(host, n, stride, length=stride), want)
     lens = rng.integers(0, stride + 1, size=n)
     want_l = o.checksum_batch(host, n, stride, lens=lens, threads=8)
-    assert np.array_equal(blocks.ChecksumBatch(host, n, stride, lens=lens), want_l)
+    assert np.array_equal(blocks.ChecksumBatchGPU(host, n, stride, lens=lens), want_l)
     # registered (pinned) memory is DMA'd directly
     _lib.check(_lib.lib.stormck_host_register(host.ctypes.data, host.nbytes))
     try:
-        assert np.array_equal(blocks.ChecksumBatch(host, n, stride, length=stride), want)
+        assert np.array_equal(blocks.ChecksumBatchGPU(host, n, stride, length=stride), want)
     finally:
         _lib.check(_lib.lib.stormck_host_unregister(host.ctypes.data))
 
@@ -921,8 +921,8 @@ def test_quad_paths_verify_and_gather_variants(dev):
     # host verify with per-block lengths
     bad = want.copy()
     bad[77] ^= 1
-    assert blocks.VerifyChecksumBatch(host, n, stride, want, lens=lens) == (n, 0)
-    assert blocks.VerifyChecksumBatch(host, n, stride, bad, lens=lens) == (77, 1)
+    assert blocks.VerifyChecksumBatchGPU(host, n, stride, want, lens=lens) == (n, 0)
+    assert blocks.VerifyChecksumBatchGPU(host, n, stride, bad, lens=lens) == (77, 1)
 
 
 def test_device_entry_points_are_graph_capturable(dev):

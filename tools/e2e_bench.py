@@ -2,7 +2,7 @@
 
 storm's blocks live in host memory (cache.data backed by pkg/memdev / pkg/filedev,
 /root/reference/cache/cache.go:36-40), so a drop-in call starts and ends there.
-Measures blocks.ChecksumBatch over a host buffer of synthetic 32 KiB blocks:
+Measures blocks.ChecksumBatchGPU (the device leg of ChecksumBatch) over a host buffer of synthetic 32 KiB blocks:
   * pageable memory (library stages through pinned buffers with parallel memcpy)
   * registered memory (stormck_host_register: DMA straight from the caller's pages)
 and, for reference, the raw pinned H2D copy rate. Results are checked bit-exact
@@ -66,14 +66,14 @@ def main():
         return best, out
 
     res = {"blocks": n, "block_bytes": BLOCK, "gib": round(n * BLOCK / 2**30, 3)}
-    blocks.ChecksumBatch(host[:64], 64, BLOCK, length=BLOCK)  # warm the context / staging
-    t, out = timed(lambda: blocks.ChecksumBatch(host, n, BLOCK, length=BLOCK))
+    blocks.ChecksumBatchGPU(host[:64], 64, BLOCK, length=BLOCK)  # warm the context / staging
+    t, out = timed(lambda: blocks.ChecksumBatchGPU(host, n, BLOCK, length=BLOCK))
     assert np.array_equal(out, want), "pageable host path mismatch"
     res["pageable_gib_s"] = round(n * BLOCK / t / 2**30, 2)
 
     _lib.check(_lib.lib.stormck_host_register(host.ctypes.data, host.nbytes))
     try:
-        t, out = timed(lambda: blocks.ChecksumBatch(host, n, BLOCK, length=BLOCK))
+        t, out = timed(lambda: blocks.ChecksumBatchGPU(host, n, BLOCK, length=BLOCK))
         assert np.array_equal(out, want), "registered host path mismatch"
         res["registered_gib_s"] = round(n * BLOCK / t / 2**30, 2)
         # raw H2D copy of the same registered bytes, 256 MiB chunks, for reference
