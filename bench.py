@@ -68,8 +68,10 @@ def parse():
                    help="c5 batch: BenchmarkKeyStore's commit (objectlist leaves) or BenchmarkStorm's (blob leaves "
                         "and a spacelist block)")
     p.add_argument("--gather-blocks", type=int, default=4 << 20, help="gather workload: blocks per step")
-    p.add_argument("--gather-order", default="shuffled", choices=["shuffled", "sequential"],
-                   help="gather workload: slot order (storm's cache slots are spread by addressingOffsets)")
+    p.add_argument("--gather-order", default="shuffled", choices=["shuffled", "sequential", "strided"],
+                   help="gather workload: slot order (storm's cache slots are spread by addressingOffsets); "
+                        "strided = no offsets, the blocks at base + i * 32 KiB with per-block lengths "
+                        "(stormck_checksum_device with lens: the same kernel without the gather, A/B)")
     p.add_argument("--gather-lens", type=int, default=0, help="gather workload: one length for every block (A/B)")
     p.add_argument("--workload", default="c3", choices=["c3", "commit", "keytags", "c5", "gather", "commit_e2e", "batch_e2e"],
                    help="c3 = BASELINE metric (default); commit = f1 level-synchronous Cache.Commit of a dirty "
@@ -614,7 +616,10 @@ def gather_workload(a):
     st = stream.cuda_stream
 
     def step():
-        engine.checksum_gather_device(arena_ptr, d_offs.data_ptr(), n, out.data_ptr(), 0, d_lens.data_ptr(), st)
+        if a.gather_order == "strided":
+            engine.checksum_device(arena_ptr, slot, n, out.data_ptr(), 0, d_lens.data_ptr(), st)
+        else:
+            engine.checksum_gather_device(arena_ptr, d_offs.data_ptr(), n, out.data_ptr(), 0, d_lens.data_ptr(), st)
 
     settle(step, a.settle)
     for _ in range(a.warmup):
@@ -633,7 +638,7 @@ def gather_workload(a):
     kms = sorted(e0.elapsed_time(e1) for e0, e1 in evs)
     avg_ms = sum(kms) / len(kms)
     hashed = int(lens.sum())
-    alg = hashed + n * (8 + 8 + 4)  # block bytes + checksum written + offset and length read
+    alg = hashed + n * (8 + (0 if a.gather_order == "strided" else 8) + 4)  # blocks + checksum + offset, length
     res = {"metric": "GiB/s gathered per-block-length checksum (storm's dirty-slot batch shape), device-resident",
            "value": round(hashed * a.steps / el / 2**30, 2), "unit": "GiB/s", "n_gpus": 1, "steps": a.steps,
            "warmup": a.warmup, "ms_per_step": round(el / a.steps * 1e3, 3), "higher_is_better": True,

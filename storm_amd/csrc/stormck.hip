@@ -2550,11 +2550,17 @@ int stormck_commit(void* arena, stormck_dirty_block* blocks, uint64_t n, uint64_
 // (AVX-512) until host memory bandwidth binds. stormck_checksum_batch routes each batch
 // to the leg the cost model below predicts is faster, as stormck_commit routes a commit.
 namespace {
-// The 16-thread host leg reads host memory at about this rate on the MI355X box's EPYC
-// 9575F (its 128K-leaf commit: 4.3 GB in 14.5 ms; the batch table in
-// §5 "Host-memory batches, routed"), below 16 x kHostCoreX4BytesPerUs.
-constexpr double kHostMemBytesPerUs = 280000.0;
-constexpr double kDevBatchCallUs = 16.0;  // stage, launch, copy back, sync of one small pipelined batch
+// Fitted to the batch table measured on MI355X with its EPYC 9575F host (DESIGN.md §5,
+// "Host-memory batches, routed", profiles/r04_batch_e2e/): 16 host threads streaming an
+// 8 GiB batch from DRAM hash 8.59 GB in 48.0 ms (179 GB/s), below 16 x
+// kHostCoreX4BytesPerUs; the device pipeline moves 8 GiB in 153-154 ms from pageable or
+// registered memory (55.7 GB/s), and a pageable batch first copies its first 256 MiB
+// chunk into pinned staging with nothing to overlap (16K blocks: 15.6 ms pageable against
+// 11.6 ms registered).
+constexpr double kHostMemBytesPerUs = 180000.0;
+constexpr double kPipeBytesPerUs = 55000.0;       // H2D of the pipelined device leg
+constexpr double kStageCopyBytesPerUs = 55000.0;  // pageable -> pinned staging copy (8 threads)
+constexpr double kDevBatchCallUs = 16.0;          // stage, launch, copy back, sync of one small batch
 
 struct BatchShape {
     uint64_t bytes = 0, longest = 0;
@@ -2585,9 +2591,12 @@ double batch_host_us(const BatchShape& s, unsigned nt) {
     return static_cast<double>(s.bytes) / std::min(core * pl, kHostMemBytesPerUs) + kHostLevelUs;
 }
 
-double batch_device_us(const BatchShape& s) {
+// The device pipeline: a call, one chain over the longest block, the bytes over the link,
+// and for pageable memory the first chunk's staging copy, which nothing overlaps.
+double batch_device_us(const BatchShape& s, bool pinned) {
+    const double fill = pinned ? 0.0 : static_cast<double>(std::min<uint64_t>(s.bytes, kChunkBytes)) / kStageCopyBytesPerUs;
     return kDevBatchCallUs + static_cast<double>(s.longest) / kDevChainBytesPerUs +
-           static_cast<double>(s.bytes) / kLinkBytesPerUs;
+           static_cast<double>(s.bytes) / kPipeBytesPerUs + fill;
 }
 
 // The host leg: blocks in pieces from a shared counter on `threads` pool threads (0 = the
@@ -2681,7 +2690,7 @@ int batch_routed(const void* base, uint64_t stride, const uint32_t* lens, uint32
     const unsigned nt = host_threads ? std::min<unsigned>(host_threads, ForkJoin::get().size()) : ForkJoin::get().size();
     // the device pipeline stages whole blocks through 256 MiB chunks
     const uint64_t step = n == 1 ? std::max<uint64_t>(s.longest, 8) : std::max<uint64_t>(stride, 8);
-    const bool device = step <= kChunkBytes && batch_device_us(s) < batch_host_us(s, nt);
+    const bool device = step <= kChunkBytes && batch_device_us(s, is_pinned(base)) < batch_host_us(s, nt);
     if (!device) {
         if (leg_used) *leg_used = STORMCK_LEG_HOST;
         return batch_host_leg(static_cast<const uint8_t*>(base), stride, lens, len, n, out, expected, first_bad, n_bad, nt);
