@@ -1192,27 +1192,30 @@ __global__ __launch_bounds__(64 * WAVES) void k_xxh64_glds_skew(const uint8_t* _
 // against 0.85-0.87 in slot order on the same arenas (profiles/r03d/, r03f/). Bucketing by
 // 32 MiB region alone (TLB locality) changed nothing (r03f); the blocks of a group must
 // be in address order. So: a counting sort by 32 MiB region of the offset (4,096
-// buckets, wrapping every 128 GiB): k_order_count (a histogram per part of the input,
-// in LDS), k_order_scan_rows + k_order_scan_buckets (exclusive scan of the part counts,
-// bucket-major), k_order_place (each part places its elements from its column of the
-// scanned counts, ranked with LDS atomics: no global atomics); then k_order_sort sorts
-// each bucket of up to kOrderSortMax blocks by offset in LDS (bitonic). Every checksum
-// is still written at its own index.
-constexpr uint32_t kOrderShift = 25, kOrderBuckets = 4096, kOrderParts = 128;
+// buckets, wrapping every 128 GiB): k_order_count (a histogram per part of the input in
+// LDS, added to the bucket totals), k_order_scan_buckets (their exclusive scan),
+// k_order_place (each part reserves a range of every bucket it uses with one global
+// atomic and places its elements there, ranked with LDS atomics); then k_order_sort
+// sorts each bucket of up to kOrderSortMax blocks by offset in LDS. Every checksum is
+// still written at its own index. Round 4 rebuilt the order this way (512 parts instead
+// of a 128-part count matrix, a counting pass instead of a bitonic network in the sort):
+// 0.31 ms per 4M-block gather before (profiles/r03b/gather_kernel_stats.csv).
+constexpr uint32_t kOrderShift = 25, kOrderBuckets = 4096, kOrderParts = 512;
 
 __device__ __forceinline__ uint32_t order_bucket(uint64_t off) {
     return static_cast<uint32_t>(off >> kOrderShift) & (kOrderBuckets - 1);
 }
 
-// The elements split into kOrderParts contiguous parts, one workgroup each. counts is a
-// bucket-major matrix: counts[b * kOrderParts + w] = elements of part w in bucket b.
+// The elements split into kOrderParts contiguous parts, one workgroup each.
 __device__ __forceinline__ void order_part(uint64_t n, uint32_t w, uint64_t* lo, uint64_t* hi) {
     *lo = n * w / kOrderParts;
     *hi = n * (w + 1) / kOrderParts;
 }
 
+// Bucket totals: each part counts its elements per bucket in LDS, then adds its nonzero
+// counts to totals[b] (zeroed by the caller): one global atomic per (part, bucket) used.
 __global__ __launch_bounds__(256) void k_order_count(const uint64_t* __restrict__ offs, uint64_t n,
-                                                     uint32_t* __restrict__ counts) {
+                                                     uint32_t* __restrict__ totals) {
     __shared__ uint32_t h[kOrderBuckets];
     for (uint32_t i = threadIdx.x; i < kOrderBuckets; i += 256) h[i] = 0;
     __syncthreads();
@@ -1220,30 +1223,15 @@ __global__ __launch_bounds__(256) void k_order_count(const uint64_t* __restrict_
     order_part(n, blockIdx.x, &lo, &hi);
     for (uint64_t i = lo + threadIdx.x; i < hi; i += 256) atomicAdd(&h[order_bucket(offs[i])], 1u);
     __syncthreads();
-    for (uint32_t i = threadIdx.x; i < kOrderBuckets; i += 256) counts[i * kOrderParts + blockIdx.x] = h[i];
+    for (uint32_t i = threadIdx.x; i < kOrderBuckets; i += 256)
+        if (h[i]) atomicAdd(&totals[i], h[i]);
 }
 
-// one wave per bucket: its row of the count matrix -> each part's offset inside the
-// bucket; the bucket's total goes to bounds[B + b]
-__global__ __launch_bounds__(256) void k_order_scan_rows(uint32_t* __restrict__ counts, uint32_t* __restrict__ bounds) {
-    static_assert(kOrderParts == 128, "two parts per lane");
-    const uint32_t lane = threadIdx.x & 63, b = blockIdx.x * 4 + (threadIdx.x >> 6);
-    uint32_t* row = counts + b * kOrderParts + lane * 2;
-    const uint32_t c0 = row[0], c1 = row[1];
-    uint32_t inc = c0 + c1;
-    for (uint32_t d = 1; d < 64; d <<= 1) {
-        const uint32_t up = __shfl_up(inc, d);
-        if (lane >= d) inc += up;
-    }
-    const uint32_t ex = inc - c0 - c1;
-    row[0] = ex;
-    row[1] = ex + c0;
-    if (lane == 63) bounds[kOrderBuckets + b] = inc;
-}
-
-// one workgroup of 1024 threads: bucket totals -> bounds[b] / bounds[B + b] = bucket b's
-// first / one-past-last position
-__global__ __launch_bounds__(1024) void k_order_scan_buckets(uint32_t* __restrict__ bounds) {
+// One workgroup of 1024 threads: bucket totals (bounds[B + b]) -> bounds[b] / bounds[B + b]
+// = bucket b's first / one-past-last position, and cursor[b] = its first position (the
+// next free place k_order_place reserves from).
+__global__ __launch_bounds__(1024) void k_order_scan_buckets(uint32_t* __restrict__ bounds,
+                                                             uint32_t* __restrict__ cursor) {
     constexpr uint32_t PER = kOrderBuckets / 1024;
     __shared__ uint32_t part[1024];
     uint32_t c[PER], sum = 0;
@@ -1260,20 +1248,29 @@ __global__ __launch_bounds__(1024) void k_order_scan_buckets(uint32_t* __restric
     for (uint32_t k = 0; k < PER; ++k) {
         const uint32_t b = threadIdx.x * PER + k;
         bounds[b] = run;
+        cursor[b] = run;
         run += c[k];
         bounds[kOrderBuckets + b] = run;
     }
 }
 
+// Each part counts its elements per bucket again (its 64 KiB of offsets are still in L2),
+// reserves a range of each bucket it uses with one global atomic, and places its elements
+// there (rank inside the part by LDS atomics). The order inside a bucket is the
+// reservations' arrival order; k_order_sort then orders each bucket by offset.
 __global__ __launch_bounds__(256) void k_order_place(const uint64_t* __restrict__ offs, uint64_t n,
-                                                     const uint32_t* __restrict__ counts,
-                                                     const uint32_t* __restrict__ bounds, uint32_t* __restrict__ order,
+                                                     uint32_t* __restrict__ cursor, uint32_t* __restrict__ order,
                                                      uint64_t* __restrict__ s_offs) {
     __shared__ uint32_t pos[kOrderBuckets];
-    for (uint32_t i = threadIdx.x; i < kOrderBuckets; i += 256) pos[i] = bounds[i] + counts[i * kOrderParts + blockIdx.x];
+    for (uint32_t i = threadIdx.x; i < kOrderBuckets; i += 256) pos[i] = 0;
     __syncthreads();
     uint64_t lo, hi;
     order_part(n, blockIdx.x, &lo, &hi);
+    for (uint64_t i = lo + threadIdx.x; i < hi; i += 256) atomicAdd(&pos[order_bucket(offs[i])], 1u);
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < kOrderBuckets; i += 256)
+        if (pos[i]) pos[i] = atomicAdd(&cursor[i], pos[i]);
+    __syncthreads();
     for (uint64_t i = lo + threadIdx.x; i < hi; i += 256) {
         const uint64_t o = offs[i];
         const uint32_t at = atomicAdd(&pos[order_bucket(o)], 1u);
@@ -1283,59 +1280,127 @@ __global__ __launch_bounds__(256) void k_order_place(const uint64_t* __restrict_
 }
 
 constexpr uint32_t kOrderSortMax = 2048;
+// k_order_sort's counting pass: 1,024 sub-buckets of 32 KiB per 32 MiB region (storm's
+// slots: one block each), runs of up to kOrderRunMax entries finished by insertion sort
+constexpr uint32_t kOrderSub = 1024, kOrderSubShift = kOrderShift - 10, kOrderRunMax = 16;
 
 // one workgroup per bucket: its entries order[start[b] .. end[b]) sorted by offset (larger
 // buckets stay in placement order)
-// Sort key: [offset inside the 32 MiB region] [the entry's index in the bucket], one
-// 64-bit compare-exchange per pair (bitonic, one pair per thread per pass); the index
-// finds the block's number and offset, kept in LDS. The bucket's offsets (placed beside
-// the indices by k_order_place) and lengths are written in the new order too (s_offs,
-// s_lens), so the hash kernel reads them sequentially; only the checksum store goes
-// through order. Grouping a region's blocks by
-// tile count first (fewer masked rows in a wave) measured worse: 0.78 against 0.85 of
-// 8 TB/s on the shuffled storm-length gather (profiles/r03k/), address order wins.
+// Sort key: [offset inside the 32 MiB region] [the entry's index in the bucket]. A counting
+// pass by 32 KiB sub-bucket orders the entries in a few barriers (a bitonic network over
+// 1,024 entries takes 55); the entries of one sub-bucket (one per 32 KiB slot in storm's
+// cache.data) are then put in key order by insertion, one thread per sub-bucket. A bucket
+// with a sub-bucket of more than kOrderRunMax entries (blocks packed below 2 KiB apart)
+// takes the bitonic network instead, one 64-bit compare-exchange per pair per pass. The
+// index finds the block's number and offset, kept in LDS. The bucket's offsets (placed
+// beside the indices by k_order_place) and lengths are written in the new order too
+// (s_offs, s_lens), so the hash kernel reads them sequentially; only the checksum store
+// goes through order. Grouping a region's blocks by tile count first (fewer masked rows
+// in a wave) measured worse: 0.78 against 0.85 of 8 TB/s on the shuffled storm-length
+// gather (profiles/r03k/), address order wins.
 __global__ __launch_bounds__(256) void k_order_sort(const uint32_t* __restrict__ lens, const uint32_t* __restrict__ bounds,
                                                     uint32_t* __restrict__ order, uint64_t* __restrict__ s_offs,
                                                     uint32_t* __restrict__ s_lens) {
     static_assert(kOrderSortMax <= 2048 && kOrderShift + 11 <= 64, "key fields");
+    static_assert(kOrderSub == 4 * 256, "four sub-buckets per thread");
     __shared__ uint64_t key[kOrderSortMax];
     __shared__ uint64_t off[kOrderSortMax];
     __shared__ uint32_t val[kOrderSortMax];
+    __shared__ uint32_t hist[kOrderSub];
+    __shared__ uint32_t first[kOrderSub];
+    __shared__ uint16_t at[kOrderSortMax];
+    __shared__ uint32_t wsum[4], longest;
+    const uint32_t tid = threadIdx.x;
     const uint32_t lo = bounds[blockIdx.x], cnt = bounds[kOrderBuckets + blockIdx.x] - lo;
     if (cnt > kOrderSortMax) {  // left in placement order
         if (lens)
-            for (uint32_t i = threadIdx.x; i < cnt; i += 256) s_lens[lo + i] = lens[order[lo + i]];
+            for (uint32_t i = tid; i < cnt; i += 256) s_lens[lo + i] = lens[order[lo + i]];
         return;
     }
-    uint32_t m = 2;
-    while (m < cnt) m <<= 1;
     constexpr uint64_t kRegion = (uint64_t{1} << kOrderShift) - 1;
-    for (uint32_t i = threadIdx.x; i < m; i += 256) {
-        uint64_t k = ~uint64_t{0};
-        if (i < cnt) {
-            const uint32_t v = order[lo + i];
-            const uint64_t o = s_offs[lo + i];
-            val[i] = v;
-            off[i] = o;
-            k = ((o & kRegion) << 11) | i;
-        }
-        key[i] = k;
+    for (uint32_t i = tid; i < kOrderSub; i += 256) hist[i] = 0;
+    if (tid == 0) longest = 0;
+    __syncthreads();
+    for (uint32_t i = tid; i < cnt; i += 256) {
+        const uint64_t o = s_offs[lo + i];
+        val[i] = order[lo + i];
+        off[i] = o;
+        key[i] = ((o & kRegion) << 11) | i;
+        atomicAdd(&hist[static_cast<uint32_t>((o & kRegion) >> kOrderSubShift)], 1u);
     }
     __syncthreads();  // (every thread's reads of s_offs and order are done before the writes below)
+    // exclusive scan of the sub-bucket counts, four per thread, and the longest run
+    uint32_t c[4], mine = 0, run = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        c[k] = hist[4 * tid + k];
+        mine += c[k];
+        run = max(run, c[k]);
+    }
+    const uint32_t lane = tid & 63, w = tid >> 6;
+    uint32_t inc = mine;
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+        const uint32_t up = static_cast<uint32_t>(__shfl_up(static_cast<int>(inc), d));
+        if (lane >= d) inc += up;
+    }
+    if (lane == 63) wsum[w] = inc;
+    atomicMax(&longest, run);
+    __syncthreads();
+    if (longest <= kOrderRunMax) {
+        uint32_t base = inc - mine;
+        for (uint32_t v = 0; v < w; ++v) base += wsum[v];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            first[4 * tid + k] = base;
+            hist[4 * tid + k] = base;  // the sub-bucket's next place
+            base += c[k];
+        }
+        __syncthreads();
+        for (uint32_t i = tid; i < cnt; i += 256)
+            at[atomicAdd(&hist[static_cast<uint32_t>((off[i] & kRegion) >> kOrderSubShift)], 1u)] =
+                static_cast<uint16_t>(i);
+        __syncthreads();
+        // each sub-bucket's entries [first, hist) in key order (insertion; at most kOrderRunMax)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t s0 = first[4 * tid + k], s1 = hist[4 * tid + k];
+            for (uint32_t a = s0 + 1; a < s1; ++a) {
+                const uint16_t e = at[a];
+                const uint64_t ke = key[e];
+                uint32_t b = a;
+                for (; b > s0 && key[at[b - 1]] > ke; --b) at[b] = at[b - 1];
+                at[b] = e;
+            }
+        }
+        __syncthreads();
+        for (uint32_t i = tid; i < cnt; i += 256) {
+            const uint32_t e = at[i];
+            const uint32_t v = val[e];
+            order[lo + i] = v;
+            s_offs[lo + i] = off[e];
+            if (lens) s_lens[lo + i] = lens[v];
+        }
+        return;
+    }
+    // bitonic network over the keys (padded to a power of two with the largest key)
+    uint32_t m = 2;
+    while (m < cnt) m <<= 1;
+    for (uint32_t i = cnt + tid; i < m; i += 256) key[i] = ~uint64_t{0};
+    __syncthreads();
     for (uint32_t k = 2; k <= m; k <<= 1) {
         for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-            for (uint32_t t = threadIdx.x; t < m / 2; t += 256) {
+            for (uint32_t t = tid; t < m / 2; t += 256) {
                 const uint32_t i = 2 * j * (t / j) + t % j, p = i + j;
-                const uint64_t a = key[i], c = key[p];
-                if ((a > c) == ((i & k) == 0)) {
-                    key[i] = c;
+                const uint64_t a = key[i], cc = key[p];
+                if ((a > cc) == ((i & k) == 0)) {
+                    key[i] = cc;
                     key[p] = a;
                 }
             }
             __syncthreads();
         }
     }
-    for (uint32_t i = threadIdx.x; i < cnt; i += 256) {
+    for (uint32_t i = tid; i < cnt; i += 256) {
         const uint32_t e = static_cast<uint32_t>(key[i]) & 2047;
         const uint32_t v = val[e];
         order[lo + i] = v;

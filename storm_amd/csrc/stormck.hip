@@ -601,18 +601,18 @@ int launch_checksum(const uint8_t* base, uint64_t stride, const uint32_t* lens, 
             hipMemPool_t pool = nullptr;
             const int prc = workspace_pool(&pool);
             if (prc) return prc;
-            const uint64_t words = (uint64_t{kOrderBuckets} * (kOrderParts + 2) + n + 1) & ~uint64_t{1};
+            const uint64_t words = (uint64_t{kOrderBuckets} * 3 + n + 1) & ~uint64_t{1};
             void* ws = nullptr;
             HIP_TRY(hipMallocFromPoolAsync(&ws, words * 4 + n * 8 + (lens ? n * 4 : 0), pool, st));
-            uint32_t* counts = static_cast<uint32_t*>(ws);  // [bucket][part], then positions
-            uint32_t* bounds = counts + kOrderBuckets * kOrderParts;
-            uint32_t* order = bounds + 2 * kOrderBuckets;
-            uint64_t* s_offs = reinterpret_cast<uint64_t*>(counts + words);
+            uint32_t* bounds = static_cast<uint32_t*>(ws);  // [first, end) per bucket (end: totals first)
+            uint32_t* cursor = bounds + 2 * kOrderBuckets;
+            uint32_t* order = cursor + kOrderBuckets;
+            uint64_t* s_offs = reinterpret_cast<uint64_t*>(bounds + words);
             uint32_t* s_lens = lens ? reinterpret_cast<uint32_t*>(s_offs + n) : nullptr;
-            hipLaunchKernelGGL(k_order_count, dim3(kOrderParts), dim3(256), 0, st, offs, n, counts);
-            hipLaunchKernelGGL(k_order_scan_rows, dim3(kOrderBuckets / 4), dim3(256), 0, st, counts, bounds);
-            hipLaunchKernelGGL(k_order_scan_buckets, dim3(1), dim3(1024), 0, st, bounds);
-            hipLaunchKernelGGL(k_order_place, dim3(kOrderParts), dim3(256), 0, st, offs, n, counts, bounds, order, s_offs);
+            HIP_TRY(hipMemsetAsync(bounds + kOrderBuckets, 0, kOrderBuckets * 4, st));
+            hipLaunchKernelGGL(k_order_count, dim3(kOrderParts), dim3(256), 0, st, offs, n, bounds + kOrderBuckets);
+            hipLaunchKernelGGL(k_order_scan_buckets, dim3(1), dim3(1024), 0, st, bounds, cursor);
+            hipLaunchKernelGGL(k_order_place, dim3(kOrderParts), dim3(256), 0, st, offs, n, cursor, order, s_offs);
             hipLaunchKernelGGL(k_order_sort, dim3(kOrderBuckets), dim3(256), 0, st, lens, bounds, order, s_offs, s_lens);
 #ifdef STORMCK_PROBES
             // rejected (round 4): each group's rows re-dealt by length rank, rotated per
