@@ -1409,6 +1409,14 @@ __global__ __launch_bounds__(256) void k_order_sort(const uint32_t* __restrict__
     }
 }
 
+// The checksums of a locality-ordered gather hashed into their sorted positions, then
+// moved to the caller's indices in one pass: out[order[k]] = s_out[k].
+__global__ __launch_bounds__(256) void k_order_scatter(const uint32_t* __restrict__ order,
+                                                       const uint64_t* __restrict__ s_out, uint64_t* __restrict__ out,
+                                                       uint64_t n) {
+    for (uint64_t k = blockIdx.x * 256ull + threadIdx.x; k < n; k += gridDim.x * 256ull) out[order[k]] = s_out[k];
+}
+
 // Rows of a group by length, rotated per workgroup step (round 4; probe build only: it
 // measured 0.794 against 0.848 of 8 TB/s for address order, profiles/r04_gather_rank/).
 // A wave streams as many

@@ -601,14 +601,23 @@ int launch_checksum(const uint8_t* base, uint64_t stride, const uint32_t* lens, 
             hipMemPool_t pool = nullptr;
             const int prc = workspace_pool(&pool);
             if (prc) return prc;
+            // probe knob STORMCK_GATHER_DEFER=1: hash into the sorted positions (coalesced
+            // stores), then one scatter pass to the caller's indices (A/B)
+            static const bool defer = [] {
+                const char* e = STORMCK_KNOB("STORMCK_GATHER_DEFER");
+                return e && e[0] == '1';
+            }();
             const uint64_t words = (uint64_t{kOrderBuckets} * 3 + n + 1) & ~uint64_t{1};
             void* ws = nullptr;
-            HIP_TRY(hipMallocFromPoolAsync(&ws, words * 4 + n * 8 + (lens ? n * 4 : 0), pool, st));
+            HIP_TRY(hipMallocFromPoolAsync(&ws, words * 4 + n * 8 + (lens ? n * 4 : 0) + (defer ? n * 8 + 8 : 0), pool, st));
             uint32_t* bounds = static_cast<uint32_t*>(ws);  // [first, end) per bucket (end: totals first)
             uint32_t* cursor = bounds + 2 * kOrderBuckets;
             uint32_t* order = cursor + kOrderBuckets;
             uint64_t* s_offs = reinterpret_cast<uint64_t*>(bounds + words);
             uint32_t* s_lens = lens ? reinterpret_cast<uint32_t*>(s_offs + n) : nullptr;
+            uint64_t* s_out = defer ? reinterpret_cast<uint64_t*>(  // 8-byte aligned after the lengths
+                                          (reinterpret_cast<uintptr_t>(s_offs + n) + (lens ? n * 4 : 0) + 7) & ~uintptr_t{7})
+                                    : nullptr;
             HIP_TRY(hipMemsetAsync(bounds + kOrderBuckets, 0, kOrderBuckets * 4, st));
             hipLaunchKernelGGL(k_order_count, dim3(kOrderParts), dim3(256), 0, st, offs, n, bounds + kOrderBuckets);
             hipLaunchKernelGGL(k_order_scan_buckets, dim3(1), dim3(1024), 0, st, bounds, cursor);
@@ -641,7 +650,21 @@ int launch_checksum(const uint8_t* base, uint64_t stride, const uint32_t* lens, 
             } else
 #undef STORMCK_ORDC
 #endif
-            if (persistent) {
+            if (defer) {
+#define STORMCK_ORDS(SK, LN)                                                                                     \
+    hipLaunchKernelGGL((k_xxh64_glds_var<kTileStripes, kAuxNT, false, kGldsWaves, SK, LN, true>), grid,            \
+                       dim3(kGldsThreads), 0, st, base, stride, lens, len, offs, n, s_out, expected, first_bad, n_bad, \
+                       nullptr)
+                if (persistent) {
+                    if (lens) STORMCK_ORDS(kSkewTiles, true);
+                    else STORMCK_ORDS(kSkewTiles, false);
+                } else {
+                    if (lens) STORMCK_ORDS(0, true);
+                    else STORMCK_ORDS(0, false);
+                }
+#undef STORMCK_ORDS
+                hipLaunchKernelGGL(k_order_scatter, dim3(2048), dim3(256), 0, st, order, s_out, out, n);
+            } else if (persistent) {
                 if (lens) STORMCK_ORD(kSkewTiles, true);
                 else STORMCK_ORD(kSkewTiles, false);
             } else {
