@@ -1201,15 +1201,20 @@ __global__ __launch_bounds__(64 * WAVES) void k_xxh64_glds_skew(const uint8_t* _
 // of a 128-part count matrix, a counting pass instead of a bitonic network in the sort):
 // 0.31 ms per 4M-block gather before (profiles/r03b/gather_kernel_stats.csv).
 constexpr uint32_t kOrderShift = 25, kOrderBuckets = 4096, kOrderParts = 512;
+// k_order_place's parts: fewer and longer than the count's, so that a part's elements of
+// one bucket land side by side (~8 per bucket at 4M blocks rather than ~2): its scattered
+// placement stores are most of its time (512 parts: 123 us per 4M blocks)
+constexpr uint32_t kOrderPlaceParts = 128;
 
 __device__ __forceinline__ uint32_t order_bucket(uint64_t off) {
     return static_cast<uint32_t>(off >> kOrderShift) & (kOrderBuckets - 1);
 }
 
-// The elements split into kOrderParts contiguous parts, one workgroup each.
+// The elements split into P contiguous parts, one workgroup each.
+template <uint32_t P = kOrderParts>
 __device__ __forceinline__ void order_part(uint64_t n, uint32_t w, uint64_t* lo, uint64_t* hi) {
-    *lo = n * w / kOrderParts;
-    *hi = n * (w + 1) / kOrderParts;
+    *lo = n * w / P;
+    *hi = n * (w + 1) / P;
 }
 
 // Bucket totals: each part counts its elements per bucket in LDS, then adds its nonzero
@@ -1254,7 +1259,7 @@ __global__ __launch_bounds__(1024) void k_order_scan_buckets(uint32_t* __restric
     }
 }
 
-// Each part counts its elements per bucket again (its 64 KiB of offsets are still in L2),
+// Each of kOrderPlaceParts parts counts its elements per bucket (its offsets then stay in L2),
 // reserves a range of each bucket it uses with one global atomic, and places its elements
 // there (rank inside the part by LDS atomics). The order inside a bucket is the
 // reservations' arrival order; k_order_sort then orders each bucket by offset.
@@ -1265,7 +1270,7 @@ __global__ __launch_bounds__(256) void k_order_place(const uint64_t* __restrict_
     for (uint32_t i = threadIdx.x; i < kOrderBuckets; i += 256) pos[i] = 0;
     __syncthreads();
     uint64_t lo, hi;
-    order_part(n, blockIdx.x, &lo, &hi);
+    order_part<kOrderPlaceParts>(n, blockIdx.x, &lo, &hi);
     for (uint64_t i = lo + threadIdx.x; i < hi; i += 256) atomicAdd(&pos[order_bucket(offs[i])], 1u);
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < kOrderBuckets; i += 256)

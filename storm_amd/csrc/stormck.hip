@@ -221,7 +221,11 @@ uint64_t cu_count() {
 // are pinned, device-mapped, coherent words, allocated with the device's table by
 // stormck_init or the first call that sets up the device (never inside a stream capture).
 // A table holds kFaultSlots streams; past that, the slot of the least recently launched
-// stream whose word is clear is reused.
+// stream whose word is clear is reused. That stream's last ring launch is then older than
+// the last launches of 1,023 other streams, while a ring kernel runs for tens of
+// microseconds, so in practice it has ended; a graph captured on it would still write the
+// old slot on a later replay, which is why captured launches need a stream of their own
+// among at most kFaultSlots live ones (include/stormck.h).
 constexpr uint32_t kFaultSlots = 1024;
 
 struct FaultTable {
@@ -621,7 +625,7 @@ int launch_checksum(const uint8_t* base, uint64_t stride, const uint32_t* lens, 
             HIP_TRY(hipMemsetAsync(bounds + kOrderBuckets, 0, kOrderBuckets * 4, st));
             hipLaunchKernelGGL(k_order_count, dim3(kOrderParts), dim3(256), 0, st, offs, n, bounds + kOrderBuckets);
             hipLaunchKernelGGL(k_order_scan_buckets, dim3(1), dim3(1024), 0, st, bounds, cursor);
-            hipLaunchKernelGGL(k_order_place, dim3(kOrderParts), dim3(256), 0, st, offs, n, cursor, order, s_offs);
+            hipLaunchKernelGGL(k_order_place, dim3(kOrderPlaceParts), dim3(256), 0, st, offs, n, cursor, order, s_offs);
             hipLaunchKernelGGL(k_order_sort, dim3(kOrderBuckets), dim3(256), 0, st, lens, bounds, order, s_offs, s_lens);
 #ifdef STORMCK_PROBES
             // rejected (round 4): each group's rows re-dealt by length rank, rotated per
