@@ -1201,10 +1201,11 @@ __global__ __launch_bounds__(64 * WAVES) void k_xxh64_glds_skew(const uint8_t* _
 // of a 128-part count matrix, a counting pass instead of a bitonic network in the sort):
 // 0.31 ms per 4M-block gather before (profiles/r03b/gather_kernel_stats.csv).
 constexpr uint32_t kOrderShift = 25, kOrderBuckets = 4096, kOrderParts = 512;
-// k_order_place's parts: fewer and longer than the count's, so that a part's elements of
-// one bucket land side by side (~8 per bucket at 4M blocks rather than ~2): its scattered
-// placement stores are most of its time (512 parts: 123 us per 4M blocks)
-constexpr uint32_t kOrderPlaceParts = 128;
+// k_order_place's parts. Fewer, longer parts put a part's elements of one bucket side by
+// side (~8 per bucket at 4M blocks rather than ~2), but 128 of them measured slower than
+// 512: 133.7 against 122-123 us per 4M blocks (profiles/r04_check3/), so the same as the
+// count's
+constexpr uint32_t kOrderPlaceParts = kOrderParts;
 
 __device__ __forceinline__ uint32_t order_bucket(uint64_t off) {
     return static_cast<uint32_t>(off >> kOrderShift) & (kOrderBuckets - 1);
