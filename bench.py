@@ -73,6 +73,10 @@ def parse():
                         "strided = no offsets, the blocks at base + i * 32 KiB with per-block lengths "
                         "(stormck_checksum_device with lens: the same kernel without the gather, A/B)")
     p.add_argument("--gather-lens", type=int, default=0, help="gather workload: one length for every block (A/B)")
+    p.add_argument("--gather-slot", type=int, default=BLOCK, help="gather workload: slot bytes (a multiple of 16)")
+    p.add_argument("--gather-lens-set", default="",
+                   help="gather workload: comma-separated lengths drawn per block instead of storm's leaf sizes "
+                        "(e.g. 256,536,728: the `-tags test` sizes, storm_test.go:131-138)")
     p.add_argument("--workload", default="c3", choices=["c3", "commit", "keytags", "c5", "gather", "commit_e2e", "batch_e2e"],
                    help="c3 = BASELINE metric (default); commit = f1 level-synchronous Cache.Commit of a dirty "
                         "forest; keytags = f4 xxhash.Sum64 of 48-byte keys")
@@ -601,10 +605,13 @@ def gather_workload(a):
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     engine.init(0)
-    n, slot = a.gather_blocks, BLOCK
+    n, slot = a.gather_blocks, a.gather_slot
     rng = np.random.default_rng(3)
     perm = rng.permutation(n).astype(np.uint64) if a.gather_order == "shuffled" else np.arange(n, dtype=np.uint64)
-    lens = np.array([31808, 30000, 32768, 28808], dtype=np.uint32)[rng.integers(0, 4, size=n)]
+    lset = [int(x) for x in a.gather_lens_set.split(",")] if a.gather_lens_set else [31808, 30000, 32768, 28808]
+    if slot % 16 or max(lset + [a.gather_lens]) > slot:
+        raise SystemExit("--gather-slot must be a multiple of 16 and hold every length")
+    lens = np.array(lset, dtype=np.uint32)[rng.integers(0, len(lset), size=n)]
     if a.gather_lens:
         lens[:] = a.gather_lens
     arena_ptr = engine.device_alloc(n * slot)
@@ -643,8 +650,8 @@ def gather_workload(a):
            "value": round(hashed * a.steps / el / 2**30, 2), "unit": "GiB/s", "n_gpus": 1, "steps": a.steps,
            "warmup": a.warmup, "ms_per_step": round(el / a.steps * 1e3, 3), "higher_is_better": True,
            "scaling": "weak", "vs_baseline": None, "dtype": "u64", "data": "synthetic",
-           "config": {"workload": f"gather: {n} blocks from {n} {a.gather_order} 32 KiB slots, lengths of "
-                                  + (f"{a.gather_lens} B" if a.gather_lens else "31808/30000/32768/28808 B")
+           "config": {"workload": f"gather: {n} blocks from {n} {a.gather_order} {slot}-byte slots, lengths of "
+                                  + (f"{a.gather_lens} B" if a.gather_lens else "/".join(map(str, lset)) + " B")
                                   + ", per-block lengths (stormck_checksum_gather_device)",
                       "blocks": n, "hashed_bytes": hashed,
                       "arena": {"va": "0x%x" % arena_ptr, "va_alignment": va_alignment(arena_ptr)}},
@@ -653,6 +660,7 @@ def gather_workload(a):
                         "kernel": "k_xxh64_glds_var<16,nt,8w,4KiB,lens,offs>", "avg_launch_ms": round(avg_ms, 4),
                         "launch_ms": {"n": len(kms), "min": round(kms[0], 4), "max": round(kms[-1], 4)},
                         "algorithmic_bytes_per_launch": alg}}
+    res["G_blocks_per_s"] = round(n / (avg_ms * 1e-3) / 1e9, 3)  # the rate that matters for small blocks
     # the same arena through the uniform-length path (k_xxh64_glds_skew: every block 32 KiB,
     # in slot order), 3 launches after the timed region: the rate this placement gives the
     # uniform kernel, beside which the gather's frac reads
