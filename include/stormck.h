@@ -123,7 +123,11 @@ int stormck_device_free(void* d_ptr);
 /* ---- hot path: batch checksums of device-resident blocks -------------------
  * Block i starts at d_base + i*stride and is (d_lens ? d_lens[i] : len) bytes
  * long. out[i] = XXH64(block i) = blocks.Checksum(block bytes). Any alignment is
- * accepted; 8-byte-aligned blocks take the fast path. n == 0 is a no-op. */
+ * accepted; 8-byte-aligned blocks take the fast path. n == 0 is a no-op.
+ * With d_lens, len may carry an upper bound of the lengths (0 = unknown), which the
+ * library plans the launch with: batches of short blocks (storm's `-tags test` sizes)
+ * take a different kernel than 32 KiB ones. Results never depend on it. The same holds
+ * for the gather and verify entry points below. */
 int stormck_checksum_device(const void* d_base, uint64_t stride, const uint32_t* d_lens, uint32_t len,
                             uint64_t n, uint64_t* d_out, void* stream);
 

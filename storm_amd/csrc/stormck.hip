@@ -427,6 +427,20 @@ int workspace_pool(hipMemPool_t* out) {
     return STORMCK_OK;
 }
 
+// Per-block-length and gathered batches whose longest block is at most this many bytes
+// stay on the register quad kernel: k_xxh64_glds_var streams 512-byte rows in lock step,
+// and short blocks leave most of a step's rows empty (storm's `-tags test` sizes 256 / 536
+// / 728 B: 3.7 against 6.4 G blocks/s strided, 2.8 against 6.2 shuffled, 1M blocks;
+// DESIGN.md §5 "Short blocks", profiles/r04_small_blocks/).
+constexpr uint64_t kVarMinLen = 4096;
+uint64_t var_min_len() {  // probe knob STORMCK_VAR_MIN_LEN: another threshold (A/B)
+    static const uint64_t v = [] {
+        const char* e = STORMCK_KNOB("STORMCK_VAR_MIN_LEN");
+        return e ? std::strtoull(e, nullptr, 10) : kVarMinLen;
+    }();
+    return v;
+}
+
 // Gathers of at least this many blocks visit them in a locality order (k_order_*); probe
 // knob STORMCK_GATHER_ORDER=0 turns it off (A/B).
 constexpr uint64_t kOrderMinBlocks = 1u << 20;
@@ -467,6 +481,10 @@ int launch_checksum(const uint8_t* base, uint64_t stride, const uint32_t* lens, 
                     uint64_t n, uint64_t* out, const uint64_t* expected, unsigned long long* first_bad,
                     unsigned long long* n_bad, hipStream_t st) {
     const bool verify = expected != nullptr;
+    // The longest block the dispatch plans for: len for uniform lengths; with per-block
+    // lengths (on the device) the caller's upper bound passed in len, 0 = unknown, planned
+    // as storm's 32 KiB. Results never depend on it, only the kernel choice does.
+    const uint64_t plan_len = lens ? (len ? len : uint64_t{32768}) : len;
     // Batch-size dispatch (profiles/r01_probe_small.txt, us per launch at 32 KiB):
     //  * n <= kWideBatch: one workgroup per block, whole block staged in one round trip
     //  * n <  kMidBatch: register quad kernel (64 blocks per workgroup spread the
@@ -575,7 +593,7 @@ int launch_checksum(const uint8_t* base, uint64_t stride, const uint32_t* lens, 
         return e ? std::strtoull(e, nullptr, 10) : 0;
     }();
     if (var_on && n >= (var_lo ? var_lo : std::max<uint64_t>(kMidBatch, 44 * cu_count())) && n > 16 * cu_count() &&
-        (lens || offs) &&
+        (lens || offs) && plan_len > var_min_len() &&
         (offs || ((reinterpret_cast<uintptr_t>(base) & 15) == 0 && (stride & 15) == 0))) {
         // below kBigBatch: 3- or 1-wave workgroups, whichever loads the busiest CU least;
         // up to kBigW, 3-wave workgroups where they cut the busiest CU's blocks by a
@@ -593,8 +611,8 @@ int launch_checksum(const uint8_t* base, uint64_t stride, const uint32_t* lens, 
         const uint64_t wgs = (n + per_wg - 1) / per_wg;
         if (wgs > 0x7fffffffULL) return fail(STORMCK_EINVAL, "batch too large for one launch");
         const uint64_t cus = cu_count();
-        // tile steps per workgroup: per-block lengths are on the device, assume 32 KiB
-        const uint64_t tiles = lens ? uint64_t{32768 / 32 / kTileStripes} : (uint64_t{len} / 32 + kTileStripes - 1) / kTileStripes;
+        // tile steps per workgroup, from the planning length
+        const uint64_t tiles = (plan_len / 32 + kTileStripes - 1) / kTileStripes;
         const bool persistent = big && cus > 0 && wgs >= cus && (wgs + cus - 1) / cus * tiles >= kSkewMinSteps;
         const dim3 grid(static_cast<unsigned>(persistent ? cus : wgs));
         // large gathers visit their blocks in a locality order (kernels.h k_order_*): a
@@ -1044,6 +1062,8 @@ int host_pipeline(const void* base, uint64_t stride, const uint32_t* lens, uint3
         for (uint64_t i = 0; i < n; ++i) maxlen = std::max<uint64_t>(maxlen, lens[i]);
     }
     if (n > 1 && stride < maxlen) return fail(STORMCK_EINVAL, "stride smaller than a block length (blocks overlap)");
+    // with per-block lengths, the longest one is the kernels' planning length (0: none)
+    const uint32_t plan = static_cast<uint32_t>(std::max<uint64_t>(maxlen, 1));
     const uint64_t step = n == 1 ? std::max<uint64_t>(maxlen, 8) : std::max<uint64_t>(stride, 8);
     if (step > kChunkBytes) return fail(STORMCK_EINVAL, "block stride exceeds the staging chunk (256 MiB)");
     const uint64_t per_chunk = std::max<uint64_t>(1, kChunkBytes / step);
@@ -1110,14 +1130,14 @@ int host_pipeline(const void* base, uint64_t stride, const uint32_t* lens, uint3
                 const uint64_t init[2] = {cnt, 0};
                 std::memcpy(s.h_result, init, 16);
                 HIP_TRY(hipMemcpyAsync(s.d_result, s.h_result, 16, hipMemcpyHostToDevice, s.stream));
-                rc = launch_checksum(s.d_data, stride, lens ? s.d_lens : nullptr, len, nullptr, cnt, nullptr,
+                rc = launch_checksum(s.d_data, stride, lens ? s.d_lens : nullptr, lens ? plan : len, nullptr, cnt, nullptr,
                                      s.d_expected, reinterpret_cast<unsigned long long*>(s.d_result),
                                      reinterpret_cast<unsigned long long*>(s.d_result + 1), s.stream);
                 if (rc) return rc;
                 HIP_TRY(hipMemcpyAsync(s.h_result, s.d_result, 16, hipMemcpyDeviceToHost, s.stream));
             } else {
-                rc = launch_checksum(s.d_data, stride, lens ? s.d_lens : nullptr, len, nullptr, cnt, s.d_out, nullptr,
-                                     nullptr, nullptr, s.stream);
+                rc = launch_checksum(s.d_data, stride, lens ? s.d_lens : nullptr, lens ? plan : len, nullptr, cnt, s.d_out,
+                                     nullptr, nullptr, nullptr, s.stream);
                 if (rc) return rc;
                 HIP_TRY(hipMemcpyAsync(s.h_out, s.d_out, cnt * 8, hipMemcpyDeviceToHost, s.stream));
             }
@@ -1985,12 +2005,15 @@ int stormck_commit_device(void* d_arena, stormck_dirty_block* blocks, uint64_t n
     std::atomic<int> bad{0};  // 1 parent range, 2 origin alignment, 3 cycle
     std::atomic<uint64_t> relocating_n{0}, upper_n{0}, upper_min{n};
     std::atomic<bool> misaligned{(reinterpret_cast<uintptr_t>(d_arena) & 15) != 0};
+    std::atomic<uint32_t> longest{0};  // the longest block: short-block forests skip the LDS-DMA levels
     par([&](unsigned, uint64_t lo, uint64_t hi) {
         uint64_t reloc = 0, up = 0, up_min = n;
+        uint32_t my_longest = 0;
         bool mis = false;
         for (uint64_t i = lo; i < hi && !bad.load(std::memory_order_relaxed); ++i) {
             const stormck_dirty_block& b = blocks[i];
             mis |= (b.data_offset & 15) != 0;
+            my_longest = std::max(my_longest, b.length);
             if (b.parent != STORMCK_NO_PARENT && (b.parent < 0 || static_cast<uint64_t>(b.parent) >= n)) {
                 bad.store(1);
                 break;
@@ -2031,6 +2054,9 @@ int stormck_commit_device(void* d_arena, stormck_dirty_block* blocks, uint64_t n
         while (up_min < m && !upper_min.compare_exchange_weak(m, up_min, std::memory_order_relaxed)) {
         }
         if (mis) misaligned.store(true, std::memory_order_relaxed);
+        uint32_t cur = longest.load(std::memory_order_relaxed);
+        while (my_longest > cur && !longest.compare_exchange_weak(cur, my_longest, std::memory_order_relaxed)) {
+        }
     });
     if (bad.load() == 1) return fail(STORMCK_EINVAL, "parent index out of range");
     if (bad.load() == 2) return fail(STORMCK_EINVAL, "origin_pointer must be 8-byte aligned (Go blocks.Pointer alignment)");
@@ -2039,7 +2065,9 @@ int stormck_commit_device(void* d_arena, stormck_dirty_block* blocks, uint64_t n
     const uint64_t nu = upper_n.load(), n0 = n - nu;
     if (n0 == 0) return fail(STORMCK_EINVAL, "parent links form a cycle");  // every block has a dirty child
     const bool prefix0 = nu == 0 || upper_min.load() == n0;
-    const bool aligned16 = !misaligned.load();
+    // the LDS-DMA level kernels need 16-byte aligned rows, and pay only when blocks are
+    // longer than a few of their 512-byte rows (as launch_checksum's kVarMinLen)
+    const bool glds_levels = !misaligned.load() && longest.load() > var_min_len();
     pt.mark("heights");
 
     // device resources before the records are touched: a failure here leaves them as given
@@ -2107,7 +2135,7 @@ int stormck_commit_device(void* d_arena, stormck_dirty_block* blocks, uint64_t n
     }();
     auto launch_level = [&](uint64_t lo, uint64_t cnt) -> int {
         auto busiest = [&](uint64_t w) { return (((cnt + 16 * w - 1) / (16 * w)) + ncu - 1) / ncu * 16 * w; };
-        if (commit_midw && aligned16 && ncu > 0 && cnt >= 39 * ncu &&
+        if (commit_midw && glds_levels && ncu > 0 && cnt >= 39 * ncu &&
             (cnt < kBigBatch || (cnt < kBigW && big_w_on() && 4 * busiest(3) <= 3 * busiest(8)))) {
             // mid-size levels: the LDS-DMA ring in 3- or 1-wave workgroups, whichever puts
             // fewer blocks on the busiest CU; from kBigBatch, 3-wave ones where they cut the
@@ -2118,7 +2146,7 @@ int stormck_commit_device(void* d_arena, stormck_dirty_block* blocks, uint64_t n
             else
                 hipLaunchKernelGGL((k_commit_level_glds<kTileStripes, kAuxNT, 3>), dim3(static_cast<unsigned>((cnt + 47) / 48)),
                                    dim3(192), 0, st, static_cast<uint8_t*>(d_arena), d_blocks, lo, cnt, d_cs);
-        } else if (aligned16 && cnt >= kStreamBatch) {
+        } else if (glds_levels && cnt >= kStreamBatch) {
             // LDS-DMA ring, 8 waves x 128 blocks per workgroup (as the uniform fast path)
             const uint64_t wgs = (cnt + kGldsBlocks - 1) / kGldsBlocks;
             if (wgs > 0x7fffffffULL) return fail(STORMCK_EINVAL, "level too large");

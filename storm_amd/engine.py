@@ -192,10 +192,11 @@ def checksum_tensor(blocks, length: Optional[int] = None, lens=None, out=None, c
     if lens is not None:
         if lens.dtype != torch.int32 or lens.device != blocks.device or lens.numel() != n:
             raise ValueError("lens must be an int32 tensor [n] on the blocks' device")
-        if int(lens.max()) > width:
+        longest = int(lens.max()) if n else 0
+        if longest > width:
             raise ValueError("a length exceeds the row width")
         d_lens = lens.data_ptr()
-        length = 0
+        length = max(longest, 1)  # with lens: the longest, which the library plans the launch with
     elif length is None:
         length = width
     elif length > width:
