@@ -175,3 +175,30 @@ def test_gather_locality_order_repeats(dev):
         want_by_slot[c0:c0 + m] = o.checksum_batch(host, m, slot, 0, lens=slot_len[c0:c0 + m], threads=16)
     bad = np.nonzero(_u64(out) != want_by_slot[pick])[0]
     assert bad.size == 0, f"{bad.size} of {n} blocks differ from the oracle, first {int(bad[0])}"
+
+
+@pytest.mark.timeout(300)
+def test_length_bound_picks_the_kernel_not_the_result(dev):
+    """With per-block lengths the caller may pass the longest length as `len`: batches of
+    short blocks (storm's `-tags test` sizes) then take the register quad kernel instead
+    of k_xxh64_glds_var (stormck.hip kVarMinLen). Every bound, none included, gives the
+    oracle's checksums, gathered and strided."""
+    from storm_amd import engine
+    n, slot = 300_000, 1024
+    rng = np.random.default_rng(17)
+    lens = rng.choice([256, 536, 728], size=n).astype(np.uint32)
+    host = rng.integers(0, 256, size=n * slot, dtype=np.uint8)
+    d = torch.from_numpy(host).to(dev)
+    d_lens = torch.from_numpy(lens.view(np.int32)).to(dev)
+    offs = (rng.permutation(n).astype(np.uint64) * np.uint64(slot))
+    d_offs = torch.from_numpy(offs.view(np.int64)).to(dev)
+    want_s = o.checksum_batch(host, n, slot, 0, lens=lens, threads=16)
+    want_g = o.checksum_gather(host, offs, lens=lens, threads=16)
+    out = torch.empty(n, dtype=torch.int64, device=dev)
+    for bound in (0, 728, 100, 1 << 20):  # none, exact, below the real longest, far above
+        engine.checksum_device(d.data_ptr(), slot, n, out.data_ptr(), bound, d_lens.data_ptr())
+        torch.cuda.synchronize()
+        assert np.array_equal(_u64(out), want_s), ("strided", bound)
+        engine.checksum_gather_device(d.data_ptr(), d_offs.data_ptr(), n, out.data_ptr(), bound, d_lens.data_ptr())
+        torch.cuda.synchronize()
+        assert np.array_equal(_u64(out), want_g), ("gather", bound)
