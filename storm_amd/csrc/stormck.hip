@@ -430,8 +430,10 @@ int workspace_pool(hipMemPool_t* out) {
 // Per-block-length and gathered batches whose longest block is at most this many bytes
 // stay on the register quad kernel: k_xxh64_glds_var streams 512-byte rows in lock step,
 // and short blocks leave most of a step's rows empty (storm's `-tags test` sizes 256 / 536
-// / 728 B: 3.7 against 6.4 G blocks/s strided, 2.8 against 6.2 shuffled, 1M blocks;
-// DESIGN.md §5 "Short blocks", profiles/r04_small_blocks/).
+// / 728 B: 3.7 against 6.4 G blocks/s strided, 2.8 against 6.2 shuffled, 1M blocks).
+// One length L per batch, strided, var / quad in G blocks/s: 1 KiB 4.29 / 5.73, 2 KiB
+// 2.82 / 2.99, 4 KiB 1.56 / 1.59, 8 KiB 0.85 / 0.76, 16 KiB 0.41 / 0.37 (DESIGN.md §5
+// "Short blocks", profiles/r04_small_blocks/, r04_small_crossover/).
 constexpr uint64_t kVarMinLen = 4096;
 uint64_t var_min_len() {  // probe knob STORMCK_VAR_MIN_LEN: another threshold (A/B)
     static const uint64_t v = [] {
