@@ -1264,6 +1264,9 @@ __global__ __launch_bounds__(1024) void k_order_scan_buckets(uint32_t* __restric
 // reserves a range of each bucket it uses with one global atomic, and places its elements
 // there (rank inside the part by LDS atomics). The order inside a bucket is the
 // reservations' arrival order; k_order_sort then orders each bucket by offset.
+// IDX: place the indices only; k_order_sort<true> then reads each block's offset through
+// its index (half the scattered placement stores, a gathered read in the sort instead).
+template <bool IDX = false>
 __global__ __launch_bounds__(256) void k_order_place(const uint64_t* __restrict__ offs, uint64_t n,
                                                      uint32_t* __restrict__ cursor, uint32_t* __restrict__ order,
                                                      uint64_t* __restrict__ s_offs) {
@@ -1281,7 +1284,7 @@ __global__ __launch_bounds__(256) void k_order_place(const uint64_t* __restrict_
         const uint64_t o = offs[i];
         const uint32_t at = atomicAdd(&pos[order_bucket(o)], 1u);
         order[at] = static_cast<uint32_t>(i);
-        s_offs[at] = o;  // with the index: k_order_sort reads both in bucket order
+        if constexpr (!IDX) s_offs[at] = o;  // with the index: k_order_sort reads both in bucket order
     }
 }
 
@@ -1304,9 +1307,10 @@ constexpr uint32_t kOrderSub = 1024, kOrderSubShift = kOrderShift - 10, kOrderRu
 // goes through order. Grouping a region's blocks by tile count first (fewer masked rows
 // in a wave) measured worse: 0.78 against 0.85 of 8 TB/s on the shuffled storm-length
 // gather (profiles/r03k/), address order wins.
+template <bool IDX = false>
 __global__ __launch_bounds__(256) void k_order_sort(const uint32_t* __restrict__ lens, const uint32_t* __restrict__ bounds,
                                                     uint32_t* __restrict__ order, uint64_t* __restrict__ s_offs,
-                                                    uint32_t* __restrict__ s_lens) {
+                                                    uint32_t* __restrict__ s_lens, const uint64_t* __restrict__ offs) {
     static_assert(kOrderSortMax <= 2048 && kOrderShift + 11 <= 64, "key fields");
     static_assert(kOrderSub == 4 * 256, "four sub-buckets per thread");
     __shared__ uint64_t key[kOrderSortMax];
@@ -1319,8 +1323,12 @@ __global__ __launch_bounds__(256) void k_order_sort(const uint32_t* __restrict__
     const uint32_t tid = threadIdx.x;
     const uint32_t lo = bounds[blockIdx.x], cnt = bounds[kOrderBuckets + blockIdx.x] - lo;
     if (cnt > kOrderSortMax) {  // left in placement order
-        if (lens)
-            for (uint32_t i = tid; i < cnt; i += 256) s_lens[lo + i] = lens[order[lo + i]];
+        if (lens || IDX)
+            for (uint32_t i = tid; i < cnt; i += 256) {
+                const uint32_t v = order[lo + i];
+                if (lens) s_lens[lo + i] = lens[v];
+                if constexpr (IDX) s_offs[lo + i] = offs[v];
+            }
         return;
     }
     constexpr uint64_t kRegion = (uint64_t{1} << kOrderShift) - 1;
@@ -1328,8 +1336,9 @@ __global__ __launch_bounds__(256) void k_order_sort(const uint32_t* __restrict__
     if (tid == 0) longest = 0;
     __syncthreads();
     for (uint32_t i = tid; i < cnt; i += 256) {
-        const uint64_t o = s_offs[lo + i];
-        val[i] = order[lo + i];
+        const uint32_t v = order[lo + i];
+        const uint64_t o = IDX ? offs[v] : s_offs[lo + i];
+        val[i] = v;
         off[i] = o;
         key[i] = ((o & kRegion) << 11) | i;
         atomicAdd(&hist[static_cast<uint32_t>((o & kRegion) >> kOrderSubShift)], 1u);
