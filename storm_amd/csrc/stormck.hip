@@ -645,7 +645,7 @@ int launch_checksum(const uint8_t* base, uint64_t stride, const uint32_t* lens, 
             HIP_TRY(hipMemsetAsync(bounds + kOrderBuckets, 0, kOrderBuckets * 4, st));
             hipLaunchKernelGGL(k_order_count, dim3(kOrderParts), dim3(256), 0, st, offs, n, bounds + kOrderBuckets);
             hipLaunchKernelGGL(k_order_scan_buckets, dim3(1), dim3(1024), 0, st, bounds, cursor);
-            // probe knob STORMCK_ORDER_IDX=1: place the indices only, the sort gathers the offsets (A/B)
+#ifdef STORMCK_PROBES  // probe knob STORMCK_ORDER_IDX=1: place the indices only, the sort gathers the offsets (A/B)
             static const bool order_idx = [] {
                 const char* e = STORMCK_KNOB("STORMCK_ORDER_IDX");
                 return e && e[0] == '1';
@@ -655,7 +655,9 @@ int launch_checksum(const uint8_t* base, uint64_t stride, const uint32_t* lens, 
                                    s_offs);
                 hipLaunchKernelGGL(k_order_sort<true>, dim3(kOrderBuckets), dim3(256), 0, st, lens, bounds, order, s_offs,
                                    s_lens, offs);
-            } else {
+            } else
+#endif
+            {
                 hipLaunchKernelGGL(k_order_place<false>, dim3(kOrderPlaceParts), dim3(256), 0, st, offs, n, cursor, order,
                                    s_offs);
                 hipLaunchKernelGGL(k_order_sort<false>, dim3(kOrderBuckets), dim3(256), 0, st, lens, bounds, order, s_offs,
