@@ -178,10 +178,26 @@ def cpu_baseline(seconds: float):
             break
     multi = reps_mt * n * BLOCK / el_mt / 2**30
     assert int(out[0]) == int(o.checksum_batch(buf[:BLOCK], 1, BLOCK, BLOCK)[0])
+    # the library's own host leg (stormck_checksum_host_leg: four blocks per thread with
+    # AVX-512, the leg routed host-memory batches take), the same sample on the same threads
+    from storm_amd import blocks
+    got = blocks.ChecksumBatchHost(buf, n, BLOCK, BLOCK, threads=threads)
+    assert np.array_equal(got, out)
+    reps_h, t0 = 0, time.perf_counter()
+    while True:
+        blocks.ChecksumBatchHost(buf, n, BLOCK, BLOCK, threads=threads)
+        reps_h += 1
+        el_h = time.perf_counter() - t0
+        if el_h >= max(1.0, seconds * 0.1):
+            break
+    leg = reps_h * n * BLOCK / el_h / 2**30
     return {"value": round(one, 3), "unit": "GiB/s", "cores": 1, "kind": "port",
             "sample": f"{n} x 32 KiB synthetic blocks (1 GiB) hashed {reps}x in {el:.1f} s by oracle/xxh64_oracle.c "
                       f"(-O3, 1 thread); Go reference unbuildable here (no Go toolchain)",
-            "all_threads": {"value": round(multi, 3), "threads": threads}, "host": host}
+            "all_threads": {"value": round(multi, 3), "threads": threads},
+            "library_host_leg": {"value": round(leg, 3), "threads": threads,
+                                 "what": "stormck_checksum_host_leg (AVX-512, 4 blocks per thread) on the same sample"},
+            "host": host}
 
 
 def cpu_commit_baseline(seconds: float):
