@@ -41,7 +41,8 @@ REV = 1
 C3_BLOCKS = 16 << 20  # BASELINE.json configs[2]
 C4_BLOCKS = 64 << 20  # BASELINE.json configs[3]
 SYNTH_SEED = 0x53544F524D  # synthetic block generator seed ("STORM")
-# --alloc: (stormck_device_alloc_placed mode, physical chunk bytes)
+# --alloc: (placement mode, physical chunk bytes); modes other than plain need the probe
+# build (STORMCK_LIBRARY=tools/libstormck_probes.so: stormck_device_alloc_placed)
 ALLOC_MODES = {"plain": (0, 0), "vmm": (1, 0), "vmm1g": (1, 1 << 30), "contig": (2, 0)}
 KERNEL = "k_xxh64_glds_skew<16,nt,8w,4KiB>"  # dominant kernel (storm_amd/csrc/kernels.h), as named in profiles/traffic.json
 
@@ -56,7 +57,8 @@ def parse():
     p.add_argument("--total-blocks", type=int, default=0, help="blocks over all GPUs per step (strong scaling)")
     p.add_argument("--arena", type=int, default=4 << 20, help="resident arena (blocks)")
     p.add_argument("--alloc", default="plain", choices=sorted(ALLOC_MODES),
-                   help="arena placement (stormck_device_alloc_placed): plain = hipMalloc; vmm = a 1 GiB-aligned "
+                   help="arena placement: plain = hipMalloc (stormck_device_alloc); with the probe build "
+                        "(STORMCK_LIBRARY=tools/libstormck_probes.so) also vmm = a 1 GiB-aligned "
                         "VMM reservation backed by one physical allocation; vmm1g = backed by 1 GiB allocations; "
                         "contig = hipDeviceMallocContiguous")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget (rank 0, N=1)")
@@ -394,7 +396,11 @@ def commit_e2e_workload(a):
       host_1       stormck_commit_host on 1 thread (storm's serial loop: one XXH64 per
                    block, children first),
       host_all     stormck_commit_host on every usable thread,
-      routed       stormck_commit (the library's choice between the two),
+      split        stormck_commit_split, balanced: the leaves on the pool (from the front)
+                   and the device in place (from the back) at once, upper heights on the
+                   host (split_dev_share = the leaves the device hashed / all leaves),
+      split_1      the same with one host thread,
+      routed       stormck_commit (the library's choice of the three),
       routed_1     the same with one host thread allowed (host cores kept for storm),
     and, for reference, dev_hbm: the same forest with cache.data in HBM (device-resident,
     the north-star configuration). Forests: storm's c5 commits (BenchmarkKeyStore's
@@ -407,7 +413,7 @@ def commit_e2e_workload(a):
     import ctypes
     import numpy as np
     import torch
-    from storm_amd import _lib
+    from storm_amd import _lib, blocks
     from storm_amd import commit as sc
     from storm_amd import engine
 
@@ -455,6 +461,11 @@ def commit_e2e_workload(a):
                 rc = L.stormck_commit_host(arena.ctypes.data, bp, len(b), REV, ctypes.byref(la), op, 1)
             elif leg == "host_all":
                 rc = L.stormck_commit_host(arena.ctypes.data, bp, len(b), REV, ctypes.byref(la), op, threads)
+            elif leg in ("split", "split_1"):
+                done = ctypes.c_uint64(0)
+                rc = L.stormck_commit_split(arena.ctypes.data, bp, len(b), REV, ctypes.byref(la), op, None, 0,
+                                            1 if leg == "split_1" else 0, _lib.SPLIT_BALANCED, ctypes.byref(done))
+                shares.setdefault(leg, []).append(done.value / nl)
             else:  # routed: the library's pool (0) or one host thread ("routed_1")
                 used = ctypes.c_uint32(9)
                 rc = L.stormck_commit(arena.ctypes.data, bp, len(b), REV, ctypes.byref(la), op, None,
@@ -465,7 +476,8 @@ def commit_e2e_workload(a):
             return dt, out
 
         row = {"forest": name, "blocks": int(len(b0)), "leaves": nl, "hashed_bytes": bytes_hashed}
-        for leg in ("dev_inplace", "dev_hbm", "host_1", "host_all", "routed", "routed_1"):
+        shares = {}
+        for leg in ("dev_inplace", "dev_hbm", "host_1", "host_all", "split", "split_1", "routed", "routed_1"):
             n_reps = reps if not (leg == "host_1" and bytes_hashed > (1 << 30)) else 3
             for _ in range(2):
                 run(leg)
@@ -479,9 +491,17 @@ def commit_e2e_workload(a):
             row[leg + "_GiBps"] = round(bytes_hashed / med / 2**30, 2)
             outs[leg] = out
         for k in ("routed_leg", "routed_1_leg"):
-            row[k] = {1: "host", 2: "device"}.get(outs.get(k), outs.get(k))
+            row[k] = _lib.LEG_NAMES.get(outs.get(k), outs.get(k))
+        for k, v in shares.items():
+            row[k + "_dev_share"] = round(sum(v) / len(v), 3)
+        row["routed_over_best"] = round(row["routed_us"] / min(row[k + "_us"] for k in ("host_all", "dev_inplace",
+                                                                                          "split")), 3)
+        row["routed_1_over_best"] = round(row["routed_1_us"] / min(row[k + "_us"] for k in ("host_1", "dev_inplace",
+                                                                                              "split_1")), 3)
+        row["split_gain"] = round(min(row["host_all_us"], row["dev_inplace_us"]) / row["split_us"], 3)
+        row["rates"] = {k: round(v, 1) for k, v in blocks.RouteRates().items()}
         row["agree"] = all(np.array_equal(outs["host_1"], outs[k]) for k in
-                           ("dev_inplace", "dev_hbm", "host_all", "routed", "routed_1"))
+                           ("dev_inplace", "dev_hbm", "host_all", "split", "split_1", "routed", "routed_1"))
         rows.append(row)
         print(json.dumps(row), flush=True)
         del hbm
@@ -499,25 +519,40 @@ def commit_e2e_workload(a):
 
 def batch_e2e_workload(a):
     """Host-memory batches end to end (the Go shim's ChecksumBatch / VerifyChecksumBatch),
-    by leg:
-      dev          stormck_checksum_host on pageable memory (staged through pinned buffers,
-                   H2D / kernel / D2H pipelined),
-      dev_reg      the same on memory registered with stormck_host_register (DMA in place),
+    by leg, on pageable memory first:
+      dev          stormck_checksum_host (staged through pinned buffers, H2D / kernel / D2H
+                   pipelined),
       host_1       stormck_checksum_host_leg on 1 thread (storm's serial xxhash.Sum64 loop
                    costs about twice this: one scalar chain per block),
       host_all     stormck_checksum_host_leg on every usable thread,
-      routed       stormck_checksum_batch (the library's choice, DESIGN §5), pool threads,
-      routed_1     the same with one host thread allowed (host cores kept for storm).
-    Batches: storm's c5 commit batch (1,200 objectlist leaves + a pointer block + the
-    singularity, keystore/benchmark_test.go:58-62), the c1 batch (1K x 32 KiB), 3 blocks,
-    a `-tags test` batch (100 blocks of 536 / 728 B, storm_test.go:131-138), 16K and 256K
-    blocks of 32 KiB (512 MiB, 8 GiB). Every leg's checksums must agree. One line per
-    batch with the table (median us per call over --steps reps)."""
+      routed       stormck_checksum_batch (the library's choice, DESIGN §4), pool threads,
+      routed_1     the same with one host thread allowed (host cores kept for storm);
+    then on the same memory registered with stormck_host_register (as the Go binding's
+    cache.data):
+      dev_reg      the device pipeline, DMA in place,
+      split        stormck_checksum_split, balanced: the pool from the front and the device
+                   from the back at once (split_dev_share = the device's blocks / n),
+      split_1      the same with one host thread,
+      routed_reg / routed_reg_1   the routed call on registered memory (it may split),
+      routed_x2    two callers at once, each routed on its own half of the batch (wall
+                   time of both; ADVICE r04: a caller that finds the pool busy plans on its
+                   own thread).
+    The routed calls use the rates the library measured so far in this process (every leg
+    above updates them): `rates` is the model after the row. Batches: storm's c5 commit
+    batch (1,200 objectlist leaves + a pointer block + the singularity,
+    keystore/benchmark_test.go:58-62), the c1 batch (1K x 32 KiB), 3 blocks, a `-tags test`
+    batch (100 blocks of 536 / 728 B, storm_test.go:131-138), 16K and 256K blocks of 32 KiB
+    (512 MiB, 8 GiB). Every leg's checksums must agree. One line per batch with the table
+    (median us per call over --steps reps); routed_over_best = routed / the best of
+    host_all, dev, dev_reg, split on the same memory kind (1 thread: host_1, dev, split_1)."""
     import ctypes
     import numpy as np
     import torch
     from storm_amd import _lib
     from storm_amd import engine
+
+    import threading
+    from storm_amd import blocks
 
     torch.cuda.set_device(0)
     engine.init(0)
@@ -558,19 +593,46 @@ def batch_e2e_workload(a):
                 rc = L.stormck_checksum_host_leg(buf.ctypes.data, stride, lp, ln, n, op, 1)
             elif leg == "host_all":
                 rc = L.stormck_checksum_host_leg(buf.ctypes.data, stride, lp, ln, n, op, threads)
+            elif leg in ("split", "split_1"):
+                done = ctypes.c_uint64(0)
+                rc = L.stormck_checksum_split(buf.ctypes.data, stride, lp, ln, n, op, None, 0,
+                                              1 if leg == "split_1" else 0, _lib.SPLIT_BALANCED, ctypes.byref(done))
+                shares.setdefault(leg, []).append(done.value / n)
+            elif leg == "routed_x2":
+                h = n // 2
+                outs2, rcs = [out[:h], out[h:]], [0, 0]
+
+                def half(k):
+                    lo = 0 if k == 0 else h
+                    used = ctypes.c_uint32(9)
+                    rcs[k] = L.stormck_checksum_batch(buf.ctypes.data + lo * stride, stride,
+                                                      (la[lo:].ctypes.data if la is not None else None), ln,
+                                                      (h if k == 0 else n - h), outs2[k].ctypes.data, 0,
+                                                      ctypes.byref(used))
+                    legs.setdefault("routed_x2", set()).add(_lib.LEG_NAMES.get(int(used.value), int(used.value)))
+                ths = [threading.Thread(target=half, args=(k,)) for k in range(2)]
+                for t in ths:
+                    t.start()
+                for t in ths:
+                    t.join()
+                rc = rcs[0] or rcs[1]
             else:
                 used = ctypes.c_uint32(9)
-                rc = L.stormck_checksum_batch(buf.ctypes.data, stride, lp, ln, n, op, 1 if leg == "routed_1" else 0,
-                                              ctypes.byref(used))
-                legs[leg] = {1: "host", 2: "device"}.get(int(used.value), int(used.value))
+                rc = L.stormck_checksum_batch(buf.ctypes.data, stride, lp, ln, n, op,
+                                              1 if leg.endswith("_1") else 0, ctypes.byref(used))
+                legs[leg] = _lib.LEG_NAMES.get(int(used.value), int(used.value))
             dt = time.perf_counter() - t0
             _lib.check(rc)
             return dt, out
 
         row = {"batch": name, "blocks": n, "hashed_bytes": hashed}
-        for leg in ("dev", "host_1", "host_all", "routed", "routed_1", "dev_reg"):
+        shares = {}
+        for leg in ("dev", "host_1", "host_all", "routed", "routed_1", "dev_reg", "split", "split_1", "routed_reg",
+                    "routed_reg_1", "routed_x2"):
             if leg == "dev_reg":
                 _lib.check(L.stormck_host_register(buf.ctypes.data, buf.nbytes))
+            if leg == "routed_x2" and n < 1024:
+                continue
             for _ in range(2):
                 run(leg)
             ts = []
@@ -583,7 +645,20 @@ def batch_e2e_workload(a):
             row[leg + "_GiBps"] = round(hashed / med / 2**30, 2)
             outs[leg] = out
         _lib.check(L.stormck_host_unregister(buf.ctypes.data))
-        row["routed_leg"], row["routed_1_leg"] = legs.get("routed"), legs.get("routed_1")
+        for k in ("routed", "routed_1", "routed_reg", "routed_reg_1"):
+            row[k + "_leg"] = legs.get(k)
+        row["routed_x2_legs"] = sorted(legs.get("routed_x2", []))
+        for k, v in shares.items():
+            row[k + "_dev_share"] = round(sum(v) / len(v), 3)
+
+        def best(*ks):
+            return min(row[k + "_us"] for k in ks)
+        row["routed_over_best"] = round(row["routed_us"] / best("host_all", "dev"), 3)
+        row["routed_1_over_best"] = round(row["routed_1_us"] / best("host_1", "dev"), 3)
+        row["routed_reg_over_best"] = round(row["routed_reg_us"] / best("host_all", "dev_reg", "split"), 3)
+        row["routed_reg_1_over_best"] = round(row["routed_reg_1_us"] / best("host_1", "dev_reg", "split_1"), 3)
+        row["split_gain"] = round(best("host_all", "dev_reg") / row["split_us"], 3)
+        row["rates"] = {k: round(v, 1) for k, v in blocks.RouteRates().items()}
         row["agree"] = all(np.array_equal(outs["host_1"], outs[k]) for k in outs)
         rows.append(row)
         print(json.dumps(row), flush=True)
@@ -591,7 +666,8 @@ def batch_e2e_workload(a):
     res = {"metric": "us per host-memory batch checksum (ChecksumBatch E2E), by leg",
            "value": rows[0]["routed_us"], "unit": "us", "n_gpus": 1, "steps": reps, "warmup": 2,
            "higher_is_better": False, "scaling": "weak", "vs_baseline": None, "dtype": "u64", "data": "synthetic",
-           "config": {"workload": "host-memory batches, pageable unless dev_reg; value = routed c5_keystore",
+           "config": {"workload": "host-memory batches, pageable, then registered (dev_reg, split*, routed_reg*); "
+                                  "value = routed c5_keystore",
                       "host_threads": threads, "host": host_cpu_info()},
            "table": rows}
     print(json.dumps(res), flush=True)
@@ -1080,7 +1156,9 @@ def block_checksum_workload(a) -> int:
                                  "alloc": {"plain": "hipMalloc", "vmm": "VMM reserve (1 GiB aligned) + one hipMemCreate",
                                            "vmm1g": "VMM reserve (1 GiB aligned) + 1 GiB hipMemCreate chunks",
                                            "contig": "hipExtMallocWithFlags(hipDeviceMallocContiguous)"}[a.alloc]
-                                          + " (stormck_device_alloc_placed), the process's first device allocation"
+                                          + (" (stormck_device_alloc)" if a.alloc == "plain" else
+                                             " (stormck_device_alloc_placed, probe build)")
+                                          + ", the process's first device allocation"
                                           + (" after the process group's" if distributed else ""),
                                  "mode": a.alloc, "mapped_chunk": mapped_chunk},
                        "timed": "K steps between barrier + synchronize, minus the on-device regeneration of "

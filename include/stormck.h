@@ -19,16 +19,16 @@
  * "_host" entry points take host memory and return when the results are in host
  * memory (H2D -> kernel -> D2H, pipelined).
  *
- * There is no CPU fallback: without a usable gfx950 device every batched, device
- * and Merkle entry point returns STORMCK_ENODEV. Host computation is a measured leg,
+ * There is no CPU fallback: without a usable gfx950 device every batched, device,
+ * routed and Merkle entry point returns STORMCK_ENODEV. Host computation is a measured leg,
  * never a substitute for a missing device:
  *  - the latency leg of a SINGLE call (stormck_xxh64 / stormck_checksum): one buffer is
  *    four serial XXH64 chains, which one host core walks faster than the GPU at every
- *    length (DESIGN.md §5), so single calls stay on the host by design (SURVEY.md §8b);
+ *    length (DESIGN.md §4), so single calls stay on the host by design (SURVEY.md §8b);
  *  - the host legs of data that lives in HOST memory (stormck_commit_host,
  *    stormck_checksum_host_leg), which the routed entry points (stormck_commit,
- *    stormck_checksum_batch) pick when the cost model, fitted to end-to-end tables measured
- *    on MI355X, predicts they beat the PCIe-bound device leg.
+ *    stormck_checksum_batch) run alone, or beside the devices (the split leg), when the
+ *    library's cost model predicts that is faster than the PCIe-bound device leg.
  */
 #ifndef STORMCK_H
 #define STORMCK_H
@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define STORMCK_ABI_VERSION 4
+#define STORMCK_ABI_VERSION 5
 
 #define STORMCK_OK 0
 #define STORMCK_EINVAL (-1)  /* bad argument (null pointer, n/len/stride out of range, ...) */
@@ -99,25 +99,15 @@ void stormck_shutdown(void);
  * Up to 1024 streams per device have a slot of their own at once; past that the least
  * recently launched stream with no pending fault gives its slot up. */
 int stormck_device_status(void* stream);
-/* Device memory for a block arena (storm's cache.data mirrored in HBM) on the calling
- * thread's current device, outside any caching allocator, so an arena taken first in a
- * process is placed the same way whatever else the process allocates.
- * stormck_device_alloc = stormck_device_alloc_placed(bytes, STORMCK_ALLOC_PLAIN, 0, ...).
- * Placement modes ("Arena placement"):
- *   STORMCK_ALLOC_PLAIN       hipMalloc;
- *   STORMCK_ALLOC_VMM         a 1 GiB-aligned VA reservation (hipMemAddressReserve) mapped
- *                             to physical allocations (hipMemCreate) of chunk_bytes each
- *                             (0: one allocation for the whole arena), rounded up to the
- *                             device's allocation granularity; *mapped_chunk (optional)
- *                             receives the chunk size used;
- *   STORMCK_ALLOC_CONTIGUOUS  hipExtMallocWithFlags(hipDeviceMallocContiguous).
- * stormck_device_free releases an arena of any mode. */
-#define STORMCK_ALLOC_PLAIN 0u
-#define STORMCK_ALLOC_VMM 1u
-#define STORMCK_ALLOC_CONTIGUOUS 2u
+/* Release `stream`'s fault slot on the calling thread's current device; call it before
+ * destroying a stream that ring kernels were launched on. It synchronises the stream, and
+ * returns STORMCK_EHIP if a fault was still pending there (which is then cleared), so a
+ * stream created later with the same handle never inherits it. */
+int stormck_stream_forget(void* stream);
+/* Device memory for a block arena (storm's cache.data mirrored in HBM): hipMalloc on the
+ * calling thread's current device, outside any caching allocator, so an arena taken first
+ * in a process is placed the same way whatever else the process allocates. */
 int stormck_device_alloc(uint64_t bytes, void** d_ptr);
-int stormck_device_alloc_placed(uint64_t bytes, uint32_t mode, uint64_t chunk_bytes, void** d_ptr,
-                                uint64_t* mapped_chunk);
 int stormck_device_free(void* d_ptr);
 
 /* ---- hot path: batch checksums of device-resident blocks -------------------
@@ -168,15 +158,18 @@ int stormck_verify_host_multi(const void* base, uint64_t stride, const uint32_t*
                               const uint64_t* expected, uint64_t* first_bad, uint64_t* n_bad, const int* devices,
                               int n_devices);
 /* A host-memory batch routed by cost (the Go shim's ChecksumBatch / VerifyChecksumBatch).
- * Over PCIe the device leg (stormck_checksum_host / stormck_verify_host) moves about
- * 52 GiB/s end to end, while host threads hash the same bytes four blocks at a time
- * (AVX-512) until host memory bandwidth binds: stormck_checksum_batch runs each batch on
- * the leg the library's measured cost model predicts is faster ("Host-memory
- * batches, routed"), as stormck_commit does for a commit. host_threads: threads the host
- * leg may use (0 = the library pool, at most 16; 1 = keep the other cores for the caller).
- * *leg_used (optional) = STORMCK_LEG_HOST / STORMCK_LEG_DEVICE. Same arguments, results
- * and errors as the _host calls; device memory is STORMCK_EINVAL (use _device). Needs a
- * gfx950 device like every batched entry point (STORMCK_ENODEV without one).
+ * Over PCIe a device moves about 52 GiB/s end to end, while host threads hash the same
+ * bytes four blocks at a time (AVX-512) until host memory binds: stormck_checksum_batch runs
+ * each batch on the leg the library's cost model predicts is fastest (the routing section
+ * below): the host leg, the device leg (stormck_checksum_host, or _host_multi over the route
+ * devices), or, for pinned or registered memory, the split leg (both at once).
+ * host_threads: threads the host part may use (0 = the library pool, at most 16; 1 = keep
+ * the other cores for the caller; a call that finds the pool held by another call plans
+ * with its own thread only). *leg_used (optional) = STORMCK_LEG_HOST / _DEVICE / _SPLIT.
+ * Same arguments, results and errors as the _host calls; device memory, or memory the host
+ * cannot read, is STORMCK_EINVAL (use _device). Needs a gfx950 device like every batched
+ * entry point: STORMCK_ENODEV without one, even when the model would pick the host leg
+ * (a stormck build needs its GPU).
  * stormck_checksum_host_leg / stormck_verify_host_leg: the host leg alone, on `threads`
  * pool threads (0 = the pool); needs no device. */
 int stormck_checksum_batch(const void* base, uint64_t stride, const uint32_t* lens, uint32_t len, uint64_t n,
@@ -327,17 +320,88 @@ int stormck_commit_host(void* arena, stormck_dirty_block* blocks, uint64_t n, ui
 /* Cache.Commit's data phase as storm's cache calls it (the Go binding's CommitBatch):
  * `arena` is cache.data. An HBM arena (stormck_device_alloc) is committed by
  * stormck_commit_device. A host arena registered with stormck_host_register is committed
- * by whichever leg the library's measured cost model predicts is
- * faster for this forest: the device leg in place over the link, or the host leg on
- * host_threads threads (0 = the pool). An unregistered host arena is out of the device's
- * reach and takes the host leg. *leg_used (optional) = STORMCK_LEG_HOST / _DEVICE.
- * Needs a gfx950 device like every batched entry point (STORMCK_ENODEV without one). */
+ * on the leg the library's cost model (routing section below) predicts is fastest: the
+ * device leg in place over the link, the host leg on host_threads threads (0 = the pool),
+ * or the split (stormck_commit_split: the leaves on both at once). An unregistered host
+ * arena is out of the devices' reach and takes the host leg. Before a host or split leg
+ * reads a registered arena, `stream` is synchronised (device writes queued on it land
+ * first). *leg_used (optional) = STORMCK_LEG_HOST / _DEVICE / _SPLIT. Needs a gfx950 device
+ * like every batched entry point (STORMCK_ENODEV without one). */
 #define STORMCK_LEG_NONE 0u
 #define STORMCK_LEG_HOST 1u
 #define STORMCK_LEG_DEVICE 2u
+#define STORMCK_LEG_SPLIT 3u
 int stormck_commit(void* arena, stormck_dirty_block* blocks, uint64_t n, uint64_t revision,
                    uint64_t* last_allocated_block, uint64_t* out_checksums, void* stream, uint32_t host_threads,
                    uint32_t* leg_used);
+
+/* ---- routing of host-memory work: the split leg and the measured rates -----------
+ * Host-memory work (stormck_checksum_batch / _verify_batch, stormck_commit) runs on one of
+ * three legs:
+ *   STORMCK_LEG_HOST    the library's host threads alone;
+ *   STORMCK_LEG_DEVICE  the device(s) alone, over PCIe;
+ *   STORMCK_LEG_SPLIT   both at once on disjoint blocks of the one call: the host threads
+ *                       take blocks from the front, each device takes chunks from the back,
+ *                       each chunk sized from the rates so that the device finishes when the
+ *                       host does, until they meet. The devices DMA (batch) or read in place
+ *                       (commit) pinned or registered memory, with no host copy.
+ * The choice is the smallest time a cost model predicts. Its rates (bytes per microsecond)
+ * start at priors measured on an MI355X box and are measured again by the calls themselves:
+ * every host, device or split leg large enough to time updates its rate (EWMA). */
+typedef struct stormck_route_rates {
+    double host_thread;    /* one host thread (four blocks at once where the CPU has AVX-512) */
+    double host_memory;    /* the host pool's cap (host memory bandwidth, shared cores) */
+    double link_pinned;    /* one device's pipeline from pinned or registered host memory */
+    double link_pageable;  /* one device's pipeline from pageable memory (through pinned staging) */
+    double link_inplace;   /* one device's kernels reading registered host memory in place */
+    uint64_t observations; /* calls that updated the rates since the priors or the last set */
+} stormck_route_rates;
+int stormck_route_get_rates(stormck_route_rates* rates);
+/* Replace the rates (rates == NULL: back to the priors). flags: STORMCK_RATES_FREEZE stops
+ * the calls from updating them (tests, A/B); STORMCK_RATES_LEARN lets them. */
+#define STORMCK_RATES_LEARN 0u
+#define STORMCK_RATES_FREEZE 1u
+int stormck_route_set_rates(const stormck_route_rates* rates, uint32_t flags);
+/* The devices the routed entry points may use, process-wide (storm is one process; each
+ * device brings its own PCIe link). n_devices == 0: the calling thread's current device
+ * (the default). Listing a device twice lists it once. */
+int stormck_route_devices(const int* devices, int n_devices);
+/* The decision alone, from the model: no device and no data needed. memory:
+ * STORMCK_MEM_PAGEABLE or STORMCK_MEM_PINNED (page-locked; for a commit, registered);
+ * n_devices: devices the call could use (0: host leg only). *leg = the leg the routed call
+ * would take (STORMCK_LEG_NONE for n == 0); predicted_us (optional, 3 doubles): host,
+ * device and split time, INFINITY where the leg cannot run or the split gains nothing. */
+#define STORMCK_MEM_PAGEABLE 0u
+#define STORMCK_MEM_PINNED 1u
+int stormck_route_plan_batch(uint64_t stride, const uint32_t* lens, uint32_t len, uint64_t n, uint32_t memory,
+                             uint32_t host_threads, uint32_t n_devices, uint32_t* leg, double* predicted_us);
+int stormck_route_plan_commit(const stormck_dirty_block* blocks, uint64_t n, uint32_t memory, uint32_t host_threads,
+                              uint32_t n_devices, uint32_t* leg, double* predicted_us);
+/* The split leg alone. base: pinned or registered host memory (pageable is STORMCK_EINVAL:
+ * the devices would need host threads to copy it, which hash faster than they copy).
+ * devices / n_devices: the devices that take part (NULL / 0: the route devices);
+ * host_threads: 0 = the pool. device_blocks: STORMCK_SPLIT_BALANCED to size the devices'
+ * chunks from the rates as they run; otherwise exactly the last device_blocks blocks go to
+ * the devices and the others to the host threads (tests, A/B). *device_done (optional):
+ * blocks the devices hashed. Results and errors as stormck_checksum_host / _verify_host
+ * (first_bad is the lowest mismatching index over both sides, n_bad their sum). */
+#define STORMCK_SPLIT_BALANCED UINT64_MAX
+int stormck_checksum_split(const void* base, uint64_t stride, const uint32_t* lens, uint32_t len, uint64_t n,
+                           uint64_t* out, const int* devices, int n_devices, uint32_t host_threads,
+                           uint64_t device_blocks, uint64_t* device_done);
+int stormck_verify_split(const void* base, uint64_t stride, const uint32_t* lens, uint32_t len, uint64_t n,
+                         const uint64_t* expected, uint64_t* first_bad, uint64_t* n_bad, const int* devices,
+                         int n_devices, uint32_t host_threads, uint64_t device_blocks, uint64_t* device_done);
+/* A commit with its leaves (height 0) split: the same rules, order, relocation, stores,
+ * outputs and errors as stormck_commit_host, with `arena` registered host memory; the
+ * devices hash leaves from the back of the leaf height in place and the host threads store
+ * every Pointer (cache/trace.go:274-320); the upper heights (a few pointer blocks) run on
+ * the host threads. device_leaves: STORMCK_SPLIT_BALANCED or the exact number of leaves, the
+ * last ones of the commit order, the devices hash; *device_done (optional): leaves they
+ * hashed. */
+int stormck_commit_split(void* arena, stormck_dirty_block* blocks, uint64_t n, uint64_t revision,
+                         uint64_t* last_allocated_block, uint64_t* out_checksums, const int* devices, int n_devices,
+                         uint32_t host_threads, uint64_t device_leaves, uint64_t* device_done);
 
 /* ---- synthetic data (benchmarks / tests) -----------------------------------
  * Word w of block i = splitmix64(seed ^ (((first + i) << 20) + w)), w < stride/8,

@@ -23,10 +23,17 @@ ENODEV = -3
 ENOMEM = -4
 EMISMATCH = -5
 
-ALLOC_PLAIN = 0       # STORMCK_ALLOC_* (include/stormck.h): arena placement modes
+# arena placement modes of stormck_device_alloc_placed: the probe build only (measured and
+# rejected in round 4; the product allocates with hipMalloc, stormck_device_alloc)
+ALLOC_PLAIN = 0
 ALLOC_VMM = 1
 ALLOC_CONTIGUOUS = 2
-LEG_NONE, LEG_HOST, LEG_DEVICE = 0, 1, 2  # STORMCK_LEG_* (stormck_commit, stormck_checksum_batch)
+# STORMCK_LEG_* (stormck_commit, stormck_checksum_batch, the route plan)
+LEG_NONE, LEG_HOST, LEG_DEVICE, LEG_SPLIT = 0, 1, 2, 3
+LEG_NAMES = {LEG_NONE: "none", LEG_HOST: "host", LEG_DEVICE: "device", LEG_SPLIT: "split"}
+MEM_PAGEABLE, MEM_PINNED = 0, 1  # STORMCK_MEM_*
+RATES_LEARN, RATES_FREEZE = 0, 1  # STORMCK_RATES_*
+SPLIT_BALANCED = (1 << 64) - 1    # STORMCK_SPLIT_BALANCED
 
 
 class StormckError(RuntimeError):
@@ -39,6 +46,17 @@ class StormckError(RuntimeError):
 
 class NoDeviceError(StormckError):
     pass
+
+
+class RouteRates(ctypes.Structure):
+    """stormck_route_rates: the routing model's rates, bytes per microsecond."""
+
+    _fields_ = [("host_thread", ctypes.c_double), ("host_memory", ctypes.c_double),
+                ("link_pinned", ctypes.c_double), ("link_pageable", ctypes.c_double),
+                ("link_inplace", ctypes.c_double), ("observations", c_uint64)]
+
+    def as_dict(self) -> dict:
+        return {f: getattr(self, f) for f, _ in self._fields_}
 
 
 class PointerStruct(ctypes.Structure):
@@ -57,7 +75,7 @@ SIGNATURES = {
     "stormck_shutdown": (None, []),
     "stormck_device_status": (c_int, [c_void_p]),
     "stormck_device_alloc": (c_int, [c_uint64, POINTER(c_void_p)]),
-    "stormck_device_alloc_placed": (c_int, [c_uint64, c_uint32, c_uint64, POINTER(c_void_p), POINTER(c_uint64)]),
+    "stormck_stream_forget": (c_int, [c_void_p]),
     "stormck_device_free": (c_int, [c_void_p]),
     "stormck_checksum_device": (c_int, [c_void_p, c_uint64, c_void_p, c_uint32, c_uint64, c_void_p, c_void_p]),
     "stormck_checksum_gather_device": (c_int, [c_void_p, c_void_p, c_void_p, c_uint32, c_uint64, c_void_p, c_void_p]),
@@ -96,7 +114,27 @@ SIGNATURES = {
     "stormck_commit_host": (c_int, [c_void_p, c_void_p, c_uint64, c_uint64, POINTER(c_uint64), c_void_p, c_uint32]),
     "stormck_commit": (
         c_int, [c_void_p, c_void_p, c_uint64, c_uint64, POINTER(c_uint64), c_void_p, c_void_p, c_uint32, POINTER(c_uint32)]),
+    "stormck_route_get_rates": (c_int, [POINTER(RouteRates)]),
+    "stormck_route_set_rates": (c_int, [POINTER(RouteRates), c_uint32]),
+    "stormck_route_devices": (c_int, [c_void_p, c_int]),
+    "stormck_route_plan_batch": (
+        c_int, [c_uint64, c_void_p, c_uint32, c_uint64, c_uint32, c_uint32, c_uint32, POINTER(c_uint32), c_void_p]),
+    "stormck_route_plan_commit": (c_int, [c_void_p, c_uint64, c_uint32, c_uint32, c_uint32, POINTER(c_uint32), c_void_p]),
+    "stormck_checksum_split": (
+        c_int, [c_void_p, c_uint64, c_void_p, c_uint32, c_uint64, c_void_p, c_void_p, c_int, c_uint32, c_uint64,
+                POINTER(c_uint64)]),
+    "stormck_verify_split": (
+        c_int, [c_void_p, c_uint64, c_void_p, c_uint32, c_uint64, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
+                c_uint32, c_uint64, POINTER(c_uint64)]),
+    "stormck_commit_split": (
+        c_int, [c_void_p, c_void_p, c_uint64, c_uint64, POINTER(c_uint64), c_void_p, c_void_p, c_int, c_uint32,
+                c_uint64, POINTER(c_uint64)]),
     "stormck_fill_synthetic_device": (c_int, [c_void_p, c_uint64, c_uint64, c_uint64, c_uint64, c_void_p]),
+}
+
+# Exported by the probe build only (storm_amd/build.py build_probes_lib), bound when present.
+PROBE_SIGNATURES = {
+    "stormck_device_alloc_placed": (c_int, [c_uint64, c_uint32, c_uint64, POINTER(c_void_p), POINTER(c_uint64)]),
 }
 
 
@@ -117,6 +155,11 @@ def _load() -> ctypes.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    for name, (res, args) in PROBE_SIGNATURES.items():
+        if hasattr(lib, name):
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
     return lib
 
 

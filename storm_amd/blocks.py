@@ -260,6 +260,80 @@ def VerifyChecksumBatchHost(buf, n: int, stride: int, expected: Sequence[int], l
     return _verify_rc(rc, fb, nb)
 
 
+def ChecksumBatchSplit(buf, n: int, stride: int, length: Optional[int] = None,
+                       lens: Optional[Sequence[int]] = None, devices: Optional[Sequence[int]] = None,
+                       host_threads: int = 0, device_blocks: Optional[int] = None) -> Tuple[np.ndarray, int]:
+    """The split leg of ChecksumBatch (stormck_checksum_split): host threads hash from the
+    front, the devices (``devices``, default the route devices) from the back, at once.
+    ``buf`` must be pinned or registered (RegisterHostMemory). ``device_blocks``: None =
+    balanced by the library's rates; else exactly the last ``device_blocks`` blocks go to
+    the devices. Returns (checksums, blocks the devices hashed)."""
+    a, la, ln, lp = _batch_args(buf, n, stride, length, lens)
+    out = np.zeros(n, dtype=np.uint64)
+    if n == 0:
+        return out, 0
+    d = _devices_arg(devices)
+    done = ctypes.c_uint64(0)
+    _lib.check(_lib.lib.stormck_checksum_split(a.ctypes.data, stride, lp, ln, n, out.ctypes.data, d,
+                                               len(d) if d is not None else 0, host_threads,
+                                               _lib.SPLIT_BALANCED if device_blocks is None else device_blocks,
+                                               ctypes.byref(done)))
+    return out, done.value
+
+
+def VerifyChecksumBatchSplit(buf, n: int, stride: int, expected: Sequence[int], length: Optional[int] = None,
+                             lens: Optional[Sequence[int]] = None, devices: Optional[Sequence[int]] = None,
+                             host_threads: int = 0, device_blocks: Optional[int] = None) -> Tuple[int, int, int]:
+    """The split leg of VerifyChecksumBatch: (first_bad, n_bad, blocks the devices hashed)."""
+    a, la, ln, lp = _batch_args(buf, n, stride, length, lens)
+    exp = _expected_arg(n, expected)
+    if n == 0:
+        return 0, 0, 0
+    d = _devices_arg(devices)
+    fb, nb, done = ctypes.c_uint64(0), ctypes.c_uint64(0), ctypes.c_uint64(0)
+    rc = _lib.lib.stormck_verify_split(a.ctypes.data, stride, lp, ln, n, exp.ctypes.data, ctypes.byref(fb),
+                                       ctypes.byref(nb), d, len(d) if d is not None else 0, host_threads,
+                                       _lib.SPLIT_BALANCED if device_blocks is None else device_blocks,
+                                       ctypes.byref(done))
+    return _verify_rc(rc, fb, nb) + (done.value,)
+
+
+def RouteDevices(devices: Optional[Sequence[int]] = None) -> None:
+    """The devices the routed calls may use (stormck_route_devices); None: the calling
+    thread's current device."""
+    d = _devices_arg(devices) if devices else None
+    _lib.check(_lib.lib.stormck_route_devices(d, len(d) if d is not None else 0))
+
+
+def RouteRates() -> dict:
+    """The routing model's current rates (bytes/us) and how many calls refined them."""
+    r = _lib.RouteRates()
+    _lib.check(_lib.lib.stormck_route_get_rates(ctypes.byref(r)))
+    return r.as_dict()
+
+
+def SetRouteRates(rates: Optional[dict] = None, freeze: bool = False) -> None:
+    """Replace the routing rates (None: back to the priors); ``freeze`` stops the calls
+    from updating them."""
+    r = None
+    if rates is not None:
+        r = _lib.RouteRates(**{k: v for k, v in rates.items() if k != "observations"})
+    _lib.check(_lib.lib.stormck_route_set_rates(ctypes.byref(r) if r is not None else None,
+                                                _lib.RATES_FREEZE if freeze else _lib.RATES_LEARN))
+
+
+def PlanBatch(n: int, stride: int, length: Optional[int] = None, lens: Optional[Sequence[int]] = None,
+              pinned: bool = False, host_threads: int = 0, n_devices: int = 1) -> Tuple[int, Tuple[float, ...]]:
+    """The routed batch's decision alone (stormck_route_plan_batch; no device needed):
+    (leg, (host_us, device_us, split_us))."""
+    la, ln = _lens_arg(n, length, lens)
+    leg, us = ctypes.c_uint32(0), (ctypes.c_double * 3)()
+    _lib.check(_lib.lib.stormck_route_plan_batch(stride, la.ctypes.data if la is not None else None, ln, n,
+                                                 _lib.MEM_PINNED if pinned else _lib.MEM_PAGEABLE, host_threads,
+                                                 n_devices, ctypes.byref(leg), us))
+    return leg.value, tuple(us)
+
+
 READ_FULL_BLOCK = 1  # STORMCK_READ_FULL_BLOCK
 
 

@@ -88,6 +88,41 @@ def commit(arena_ptr: int, blocks: np.ndarray, revision: int, last_allocated: in
     return out, la.value, leg.value
 
 
+def commit_split(arena: np.ndarray, blocks: np.ndarray, revision: int, last_allocated: int, devices=None,
+                 host_threads: int = 0, device_leaves: Optional[int] = None,
+                 out: Optional[np.ndarray] = None) -> Tuple[np.ndarray, int, int]:
+    """The split commit (stormck_commit_split) on a registered host arena: the leaves
+    hashed by host threads from the front and the devices from the back at once, in place.
+    ``device_leaves``: None = balanced by the library's rates; else exactly the last
+    ``device_leaves`` leaves of the commit order go to the devices. Returns (checksums, new
+    last_allocated_block, leaves the devices hashed)."""
+    _check_blocks(blocks)
+    if arena.dtype != np.uint8 or not arena.flags["C_CONTIGUOUS"]:
+        raise ValueError("arena must be a contiguous uint8 array")
+    n = blocks.shape[0]
+    out = _out(out, n)
+    la, done = ctypes.c_uint64(last_allocated), ctypes.c_uint64(0)
+    d = (ctypes.c_int * len(devices))(*[int(x) for x in devices]) if devices else None
+    _lib.check(_lib.lib.stormck_commit_split(arena.ctypes.data, blocks.ctypes.data if n else None, n, revision,
+                                             ctypes.byref(la), out.ctypes.data if n else None, d,
+                                             len(devices) if devices else 0, host_threads,
+                                             _lib.SPLIT_BALANCED if device_leaves is None else device_leaves,
+                                             ctypes.byref(done)))
+    return out, la.value, done.value
+
+
+def plan_commit(blocks: np.ndarray, registered: bool = True, host_threads: int = 0, n_devices: int = 1):
+    """The routed commit's decision alone (stormck_route_plan_commit; no device needed):
+    (leg, (host_us, device_us, split_us))."""
+    _check_blocks(blocks)
+    n = blocks.shape[0]
+    leg, us = ctypes.c_uint32(0), (ctypes.c_double * 3)()
+    _lib.check(_lib.lib.stormck_route_plan_commit(blocks.ctypes.data if n else None, n,
+                                                  _lib.MEM_PINNED if registered else _lib.MEM_PAGEABLE,
+                                                  host_threads, n_devices, ctypes.byref(leg), us))
+    return leg.value, tuple(us)
+
+
 def _check_blocks(blocks: np.ndarray) -> None:
     if blocks.dtype != DIRTY_DTYPE or not blocks.flags["C_CONTIGUOUS"]:
         raise ValueError("blocks must be a contiguous DIRTY_DTYPE array")

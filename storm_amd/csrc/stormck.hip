@@ -49,6 +49,13 @@ class ForkJoin {
         return *instance_;
     }
     unsigned size() const { return nw_ + 1; }
+    // Whether another caller's job holds the pool right now (advisory: a routed call that
+    // finds it busy plans its host work for its own thread, which run() never queues).
+    bool busy() {
+        if (!run_mu_.try_lock()) return true;
+        run_mu_.unlock();
+        return false;
+    }
     // fn(t) for t in [0, parts); parts is clamped to size(); the caller runs t = 0
     template <class F>
     void run(unsigned parts, F&& fn) {
@@ -950,6 +957,7 @@ struct Stage {
     uint8_t* pinned = nullptr;      // staging for pageable sources
     uint8_t* d_data = nullptr;
     uint32_t* d_lens = nullptr;
+    uint64_t* d_offs = nullptr;     // split leg: block offsets of an in-place gather
     uint64_t* d_out = nullptr;
     uint64_t* h_out = nullptr;      // pinned
     uint64_t* d_expected = nullptr;
@@ -1001,6 +1009,7 @@ int ensure_ready(DeviceCtx* c) {
         HIP_TRY(hipMalloc(&s.d_data, kChunkBytes));
         const uint64_t maxb = kChunkBytes / 8;  // smallest admissible stride is 8 bytes per block
         HIP_TRY(hipMalloc(&s.d_lens, maxb * 4));
+        HIP_TRY(hipMalloc(&s.d_offs, maxb * 8));
         HIP_TRY(hipMalloc(&s.d_out, maxb * 8));
         HIP_TRY(hipMalloc(&s.d_expected, maxb * 8));
         HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&s.h_out), maxb * 8, hipHostMallocDefault));
@@ -1020,6 +1029,7 @@ void release_ctx(DeviceCtx* c) {
         if (s.stream) (void)hipStreamSynchronize(s.stream);
         (void)hipFree(s.d_data);
         (void)hipFree(s.d_lens);
+        (void)hipFree(s.d_offs);
         (void)hipFree(s.d_out);
         (void)hipFree(s.d_expected);
         (void)hipFree(s.d_result);
@@ -1039,13 +1049,58 @@ void release_ctx(DeviceCtx* c) {
     (void)hipSetDevice(prev);
 }
 
-bool is_pinned(const void* p) {
-    hipPointerAttribute_t a;
-    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
-        (void)hipGetLastError();
-        return false;
+// Whether this process can read the first and the last byte of [p, p + bytes): a write of
+// each byte into a pipe fails with EFAULT instead of faulting when the address is not
+// readable (e.g. a device address the CPU mapping leaves inaccessible).
+bool host_readable(const void* p, uint64_t bytes) {
+    static std::mutex mu;
+    static int fds[2] = {-1, -1};
+    std::lock_guard<std::mutex> g(mu);
+    if (fds[0] < 0 && pipe2(fds, O_NONBLOCK | O_CLOEXEC) != 0) return true;  // cannot tell: as before
+    const uint8_t* b = static_cast<const uint8_t*>(p);
+    for (const uint8_t* q : {b, b + (bytes ? bytes - 1 : 0)}) {
+        if (write(fds[1], q, 1) != 1) return errno != EFAULT;
+        uint8_t sink = 0;
+        (void)!read(fds[0], &sink, 1);
     }
-    return a.type == hipMemoryTypeHost || a.type == hipMemoryTypeManaged;
+    return true;
+}
+
+// Where a host-path argument lives. hipPointerGetAttributes names HIP's own allocations and
+// registrations; plain host memory is unknown to it (an error, or hipMemoryTypeUnregistered),
+// and so is device memory HIP did not map itself. An address it does not name is taken as
+// host memory only when the process can read it, so such device memory is an argument
+// error rather than a fault on a host thread.
+enum class Mem {
+    kPageable,    // ordinary host memory: host threads read it; the devices through staging
+    kPinned,      // page-locked host memory: DMA-able
+    kMapped,      // page-locked and mapped (stormck_host_register, hipHostMalloc): also read in place
+    kDevice,      // HBM: the _device entry points
+    kUnreadable,  // unknown to HIP and not readable by the host
+};
+#ifdef STORMCK_PROBES
+bool in_vmm_arena(const void* p);
+#endif
+
+Mem classify(const void* p, uint64_t bytes) {
+#ifdef STORMCK_PROBES
+    if (in_vmm_arena(p)) return Mem::kDevice;
+#endif
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) == hipSuccess) {
+        if (a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeArray) return Mem::kDevice;
+        if (a.type == hipMemoryTypeHost || a.type == hipMemoryTypeManaged)
+            return a.devicePointer ? Mem::kMapped : Mem::kPinned;
+    } else {
+        (void)hipGetLastError();
+    }
+    return host_readable(p, bytes) ? Mem::kPageable : Mem::kUnreadable;
+}
+
+// The error of a host-path argument that host threads must not read.
+int not_host_memory(Mem m) {
+    return m == Mem::kDevice ? fail(STORMCK_EINVAL, "base is device memory: use the _device entry points")
+                             : fail(STORMCK_EINVAL, "base is not readable host memory");
 }
 
 // Parallel memcpy into pinned staging (pageable sources): a single thread cannot
@@ -1093,13 +1148,9 @@ int host_pipeline(const void* base, uint64_t stride, const uint32_t* lens, uint3
     rc = ensure_ready(c);
     if (rc) return rc;
 
-    {
-        hipPointerAttribute_t a;
-        if (hipPointerGetAttributes(&a, base) == hipSuccess && a.type == hipMemoryTypeDevice)
-            return fail(STORMCK_EINVAL, "base is device memory: use the _device entry points");
-        (void)hipGetLastError();
-    }
-    const bool direct = is_pinned(base);
+    const Mem mem = classify(base, (n - 1) * stride + (lens ? lens[n - 1] : len));
+    if (mem == Mem::kDevice || mem == Mem::kUnreadable) return not_host_memory(mem);
+    const bool direct = mem != Mem::kPageable;
     const uint8_t* src = static_cast<const uint8_t*>(base);
     uint64_t fb = n, nb = 0;
 
@@ -1279,8 +1330,10 @@ int host_pipeline_multi(const void* base, uint64_t stride, const uint32_t* lens,
     return STORMCK_OK;
 }
 
-// Arenas from stormck_device_alloc_placed(STORMCK_ALLOC_VMM): their physical chunks, so
-// that stormck_device_free can unmap and release them.
+#ifdef STORMCK_PROBES
+// Probe build only: arenas from stormck_device_alloc_placed(VMM) (DESIGN_LOG.md, "Arena
+// placement": no better than hipMalloc, and 2 MiB chunks once read wrong before access was
+// set per chunk), with their physical chunks so stormck_device_free can release them.
 constexpr uint64_t kVmmAlign = 1ULL << 30;
 struct VmmArena {
     uint64_t size = 0, chunk = 0;
@@ -1288,6 +1341,17 @@ struct VmmArena {
 };
 std::mutex g_arena_mu;
 std::vector<std::pair<void*, VmmArena>> g_vmm;
+
+bool in_vmm_arena(const void* p) {
+    const uintptr_t x = reinterpret_cast<uintptr_t>(p);
+    std::lock_guard<std::mutex> g(g_arena_mu);
+    for (const auto& e : g_vmm) {
+        const uintptr_t b = reinterpret_cast<uintptr_t>(e.first);
+        if (x >= b && x < b + e.second.size) return true;
+    }
+    return false;
+}
+#endif
 
 }  // namespace
 
@@ -1347,23 +1411,33 @@ int stormck_device_status(void* stream) {
 }
 
 int stormck_device_alloc(uint64_t bytes, void** d_ptr) {
-    return stormck_device_alloc_placed(bytes, STORMCK_ALLOC_PLAIN, 0, d_ptr, nullptr);
+    if (!d_ptr) return fail(STORMCK_EINVAL, "d_ptr is null");
+    *d_ptr = nullptr;
+    if (bytes == 0) return fail(STORMCK_EINVAL, "bytes is 0");
+    int rc = device_check();
+    if (rc) return rc;
+    HIP_TRY(hipMalloc(d_ptr, bytes));
+    return STORMCK_OK;
 }
 
+#ifdef STORMCK_PROBES
+// Probe build only (not in include/stormck.h): the arena placement modes measured and
+// rejected in round 4 (mode 0 hipMalloc, 1 VMM reservation + hipMemCreate chunks,
+// 2 hipDeviceMallocContiguous).
 int stormck_device_alloc_placed(uint64_t bytes, uint32_t mode, uint64_t chunk_bytes, void** d_ptr,
                                 uint64_t* mapped_chunk) {
     if (!d_ptr) return fail(STORMCK_EINVAL, "d_ptr is null");
     *d_ptr = nullptr;
     if (mapped_chunk) *mapped_chunk = 0;
     if (bytes == 0) return fail(STORMCK_EINVAL, "bytes is 0");
-    if (mode > STORMCK_ALLOC_CONTIGUOUS) return fail(STORMCK_EINVAL, "unknown allocation mode");
+    if (mode > 2) return fail(STORMCK_EINVAL, "unknown allocation mode");
     int rc = device_check();
     if (rc) return rc;
-    if (mode == STORMCK_ALLOC_PLAIN) {
+    if (mode == 0) {
         HIP_TRY(hipMalloc(d_ptr, bytes));
         return STORMCK_OK;
     }
-    if (mode == STORMCK_ALLOC_CONTIGUOUS) {
+    if (mode == 2) {
         HIP_TRY(hipExtMallocWithFlags(d_ptr, bytes, hipDeviceMallocContiguous));
         return STORMCK_OK;
     }
@@ -1423,11 +1497,16 @@ int stormck_device_alloc_placed(uint64_t bytes, uint32_t mode, uint64_t chunk_by
     if (mapped_chunk) *mapped_chunk = chunk;
     return STORMCK_OK;
 }
+#endif
 
 int stormck_device_free(void* d_ptr) {
     if (!d_ptr) return STORMCK_OK;
     int rc = device_check();
     if (rc) return rc;
+#ifndef STORMCK_PROBES
+    HIP_TRY(hipFree(d_ptr));
+    return STORMCK_OK;
+#else
     VmmArena a;
     bool vmm = false;
     {
@@ -1451,6 +1530,35 @@ int stormck_device_free(void* d_ptr) {
     }
     HIP_TRY(hipMemAddressFree(d_ptr, a.size));
     return STORMCK_OK;
+#endif
+}
+
+int stormck_stream_forget(void* stream) {
+    int rc = device_check();
+    if (rc) return rc;
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev));
+    if (dev < 0 || dev >= 64) return fail(STORMCK_EINVAL, "device index beyond 64");
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    HIP_TRY(hipStreamSynchronize(st));  // no ring kernel of this stream may write the slot later
+    FaultTable& t = g_faults[dev];
+    uint32_t code = 0;
+    {
+        std::lock_guard<std::mutex> g(t.mu);
+        const int s = t.find(st);
+        if (s < 0 || !t.words) return STORMCK_OK;
+        code = __atomic_exchange_n(t.words + s, 0u, __ATOMIC_ACQ_REL);
+        t.owner[s] = nullptr;
+        t.last_launch[s] = 0;  // free for the next stream
+        for (size_t k = 0; k < t.index.size(); ++k)
+            if (t.index[k].second == static_cast<uint32_t>(s)) {
+                t.index[k] = t.index.back();
+                t.index.pop_back();
+                break;
+            }
+    }
+    if (code == 0) return STORMCK_OK;
+    return fail(STORMCK_EHIP, "device " + std::to_string(dev) + ": " + fault_text(code));
 }
 
 void stormck_shutdown(void) {
@@ -2395,138 +2503,664 @@ int stormck_commit_device(void* d_arena, stormck_dirty_block* blocks, uint64_t n
     return rc;
 }
 
-// ---- f1, host leg --------------------------------------------------------------
+}  // extern "C" (the routing engine below is internal C++)
+
+// ---- routing of host-memory work: host, device and split legs ------------------------
+// Work that lives in host memory (storm's cache.data: the Go shim's ChecksumBatch,
+// VerifyChecksumBatch and CommitBatch) runs on one of three legs:
+//   host    the library's pool threads hash the blocks, four at a time with AVX-512;
+//   device  the device(s) hash them over PCIe (the host pipeline; kernels reading the
+//           registered arena in place for a commit);
+//   split   both at once, on disjoint blocks of the one call: the host threads take pieces
+//           from the front, each device takes chunks from the back, each chunk sized so
+//           that the device finishes when everyone else does (SplitQueue), until they meet.
+// One engine runs the host and split legs (split_run; the host leg is a split without
+// devices). The routed entry points take the leg with the smallest predicted time, from
+// rates that start at priors measured on MI355X and that every call large
+// enough to time measures again (RouteModel).
 namespace {
-// A height is split over threads only in pieces of at least this many bytes (~10 us of
+
+// A host pass is split over threads only in pieces of at least this many bytes (~10 us of
 // hashing on one core, about what the pool's fork/join costs).
 constexpr uint64_t kHostMinBytesPerThread = 256 * 1024;
-}  // namespace
+constexpr double kHostLevelUs = 10.0;             // fork/join of a parallel pass
+constexpr double kDevCallUs = 10.0;               // device commit: a call
+constexpr double kDevLevelUs = 6.0;               // device commit: a launch per height
+constexpr double kDevChainBytesPerUs = 1600.0;    // one 4-lane XXH64 chain on gfx950 (32 KiB in ~20 us)
+constexpr double kDevBatchCallUs = 16.0;          // stage, launch, copy back and sync one small batch
+constexpr double kStageCopyBytesPerUs = 55000.0;  // pageable -> pinned staging copy (8 threads)
+constexpr double kSplitStartUs = 30.0;            // a device worker wakes and starts its first chunk
+constexpr double kSplitChunkUs = 8.0;             // a chunk issued behind one in flight: launch, copy back
+constexpr double kSplitMinClaimBytes = 1 << 20;   // a smaller device claim costs about what it saves
+constexpr double kSplitGain = 0.95;               // the split is taken only when predicted 5% faster
 
-// The same commit on host threads: what storm's own loop costs (commitData hashes one
-// block at a time on its goroutine, cache/cache.go:87-137), with the blocks of one height
-// spread over `threads` pool threads. The level-synchronous device commit pays a launch
-// and a chain per height (~20 us) and, on storm's host-resident cache.data, the PCIe
-// link for every byte; small forests are cheaper here (stormck_commit routes by the
-// measured crossover, DESIGN.md §11 f1 "End to end from host memory").
-int stormck_commit_host(void* arena, stormck_dirty_block* blocks, uint64_t n, uint64_t revision,
-                        uint64_t* last_allocated_block, uint64_t* out_checksums, uint32_t threads) {
-    if (n == 0) return STORMCK_OK;
-    if (!arena || !blocks || !last_allocated_block || !out_checksums) return fail(STORMCK_EINVAL, "null argument");
-    if (n > 0xffffffffULL) return fail(STORMCK_EINVAL, "more than 2^32 dirty blocks");
-    // validation and heights, with stormck_commit_device's rules and messages
-    std::vector<uint32_t> height(n, 0);
-    for (uint64_t i = 0; i < n; ++i) {
-        const stormck_dirty_block& b = blocks[i];
-        if (b.parent != STORMCK_NO_PARENT && (b.parent < 0 || static_cast<uint64_t>(b.parent) >= n))
-            return fail(STORMCK_EINVAL, "parent index out of range");
-        if (b.origin_pointer != STORMCK_NO_ORIGIN && (b.origin_pointer & 7) != 0)
-            return fail(STORMCK_EINVAL, "origin_pointer must be 8-byte aligned (Go blocks.Pointer alignment)");
+// Priors, bytes/us: the rates measured on an MI355X box with its EPYC 9575F host
+// (profiles/r04_batch_e2e/, r04_commit_e2e/).
+constexpr double kPriorHostThreadX4 = 48000.0;  // one thread hashing four blocks at once (AVX-512)
+constexpr double kPriorHostThread = 24000.0;    // one thread, scalar XXH64 (no AVX-512)
+constexpr double kPriorHostMemory = 180000.0;   // the pool: host memory bound (the slower box, 179 GB/s)
+constexpr double kPriorLinkPinned = 55000.0;    // the device pipeline from pinned / registered memory
+constexpr double kPriorLinkPageable = 55000.0;  // the same through pinned staging, copy overlapped
+constexpr double kPriorLinkInplace = 50000.0;   // kernels reading registered memory in place (49-52 GB/s)
+constexpr double kLearnWeight = 0.25;           // EWMA weight of one call's observed rate
+constexpr uint64_t kLearnMinHostBytes = 8ULL << 20;   // below: fork/join noise
+constexpr uint64_t kLearnMinLinkBytes = 64ULL << 20;  // below: launch and sync noise
+
+enum class Link { kPinned, kPageable, kInplace };
+
+class RouteModel {
+  public:
+    static RouteModel& get() {
+        static RouteModel m;
+        return m;
     }
-    uint32_t max_h = 0;
-    for (uint64_t i = 0; i < n; ++i) {
-        uint64_t cur = i;
-        uint32_t hh = 0;
-        while (blocks[cur].parent != STORMCK_NO_PARENT) {
-            cur = static_cast<uint64_t>(blocks[cur].parent);
-            if (++hh > n) return fail(STORMCK_EINVAL, "parent links form a cycle");
-            if (height[cur] >= hh) break;  // an earlier walk carries it upward
-            height[cur] = hh;
-            max_h = std::max(max_h, hh);
+    stormck_route_rates now() {
+        std::lock_guard<std::mutex> g(mu_);
+        return r_;
+    }
+    void set(const stormck_route_rates* r, bool freeze) {
+        std::lock_guard<std::mutex> g(mu_);
+        r_ = r ? *r : priors();
+        r_.observations = 0;
+        frozen_ = freeze;
+    }
+    // A host pass: `bytes` hashed on `threads` threads in `us`. One thread measures the
+    // per-thread rate; a pool pass either the threads (it ran at their rate) or the cap
+    // that host memory and shared cores put on them (it ran below it).
+    void learn_host(uint64_t bytes, unsigned threads, double us) {
+        if (bytes < kLearnMinHostBytes || us <= 0) return;
+        const double rate = static_cast<double>(bytes) / us;
+        std::lock_guard<std::mutex> g(mu_);
+        if (frozen_) return;
+        if (threads <= 1) {
+            r_.host_thread = ewma(r_.host_thread, rate);
+        } else if (rate >= 0.8 * threads * r_.host_thread) {
+            r_.host_thread = ewma(r_.host_thread, rate / threads);
+            r_.host_memory = std::max(r_.host_memory, rate);
+        } else {
+            r_.host_memory = ewma(r_.host_memory, rate);
         }
+        ++r_.observations;
     }
-    // commit order: by height, index order within a height (stormck_commit_device's)
-    std::vector<uint64_t> start(static_cast<size_t>(max_h) + 2, 0);
-    for (uint64_t i = 0; i < n; ++i) start[height[i] + 1]++;
-    if (start[1] == 0) return fail(STORMCK_EINVAL, "parent links form a cycle");
-    for (uint32_t l = 0; l <= max_h; ++l) start[l + 1] += start[l];
-    std::vector<uint32_t> order(n);
+    // One device's transfer: `bytes` in `us` beyond the call's fixed latency.
+    void learn_link(Link k, uint64_t bytes, double us) {
+        if (bytes < kLearnMinLinkBytes || us <= 0) return;
+        const double rate = static_cast<double>(bytes) / us;
+        std::lock_guard<std::mutex> g(mu_);
+        if (frozen_) return;
+        double& r = k == Link::kPinned ? r_.link_pinned : (k == Link::kPageable ? r_.link_pageable : r_.link_inplace);
+        r = ewma(r, rate);
+        ++r_.observations;
+    }
+
+  private:
+    RouteModel() : r_(priors()) {}
+    static stormck_route_rates priors() {
+        stormck_route_rates r;
+        std::memset(&r, 0, sizeof r);
+        r.host_thread = host::has_x4() ? kPriorHostThreadX4 : kPriorHostThread;
+        r.host_memory = kPriorHostMemory;
+        r.link_pinned = kPriorLinkPinned;
+        r.link_pageable = kPriorLinkPageable;
+        r.link_inplace = kPriorLinkInplace;
+        return r;
+    }
+    static double ewma(double old, double obs) { return old + kLearnWeight * (obs - old); }
+    std::mutex mu_;
+    stormck_route_rates r_;
+    bool frozen_ = false;
+};
+
+// Aggregate rate of `threads` host threads.
+double host_rate(const stormck_route_rates& r, unsigned threads) {
+    return threads <= 1 ? r.host_thread : std::min(threads * r.host_thread, r.host_memory);
+}
+
+// Threads a host pass of `bytes` uses out of `nt` allowed.
+unsigned host_threads_for(uint64_t bytes, unsigned nt) {
+    return static_cast<unsigned>(std::min<uint64_t>(std::max(1u, nt), std::max<uint64_t>(1, bytes / kHostMinBytesPerThread)));
+}
+
+double now_us() {
+    return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// The devices routed calls may use (stormck_route_devices); empty: the caller's current one.
+std::mutex g_route_mu;
+std::vector<int> g_route_devs;
+
+int route_devices(std::vector<int>* out) {
     {
-        std::vector<uint64_t> pos(start.begin(), start.end() - 1);
-        for (uint64_t i = 0; i < n; ++i) order[pos[height[i]]++] = static_cast<uint32_t>(i);
+        std::lock_guard<std::mutex> g(g_route_mu);
+        *out = g_route_devs;
     }
-    // relocation in commit order (cache/cache.go:114-118)
-    uint64_t last = *last_allocated_block;
-    for (uint64_t k = 0; k < n; ++k) {
-        stormck_dirty_block& b = blocks[order[k]];
-        if (b.birth_revision <= revision) {
-            b.address = ++last;
-            b.birth_revision = revision + 1;
-        }
-    }
-    *last_allocated_block = last;
-    // one height at a time; its blocks in chunks from a shared counter
-    uint8_t* a = static_cast<uint8_t*>(arena);
-    ForkJoin& fj = ForkJoin::get();
-    const unsigned nt = threads ? std::min<unsigned>(threads, fj.size()) : fj.size();
-    for (uint32_t l = 0; l <= max_h; ++l) {
-        const uint64_t lo = start[l], cnt = start[l + 1] - lo;
-        // a fork/join costs ~10 us: a height with little to hash stays on this thread
-        uint64_t level_bytes = 0;
-        for (uint64_t k = lo; k < lo + cnt; ++k) level_bytes += blocks[order[k]].length;
-        const unsigned pl = static_cast<unsigned>(std::min<uint64_t>(nt, std::max<uint64_t>(1, level_bytes / kHostMinBytesPerThread)));
-        const uint64_t chunk = std::max<uint64_t>(1, cnt / (uint64_t{pl} * 8));
-        std::atomic<uint64_t> next{0};
-        auto work = [&](unsigned) {
-            for (;;) {
-                const uint64_t k0 = next.fetch_add(chunk, std::memory_order_relaxed);
-                if (k0 >= cnt) return;
-                const uint64_t k1 = std::min(cnt, k0 + chunk);
-                auto store = [&](uint64_t i, uint64_t h) {
-                    const stormck_dirty_block& b = blocks[i];
-                    out_checksums[i] = h;
-                    if (b.origin_pointer != STORMCK_NO_ORIGIN) {
-                        const uint64_t ptr[3] = {h, b.address, b.birth_revision};
-                        std::memcpy(a + b.origin_pointer, ptr, sizeof ptr);
-                        a[b.origin_type] = b.type;
-                    }
-                };
-                uint64_t k = k0;
-                for (; host::has_x4() && k + 4 <= k1; k += 4) {  // four blocks' chains at once (AVX-512)
-                    const unsigned char* p4[4];
-                    size_t n4[4];
-                    uint64_t h4[4];
-                    for (int q = 0; q < 4; ++q) {
-                        const stormck_dirty_block& b = blocks[order[lo + k + q]];
-                        p4[q] = a + b.data_offset;
-                        n4[q] = b.length;
-                    }
-                    host::xxh64_x4(p4, n4, h4);
-                    for (int q = 0; q < 4; ++q) store(order[lo + k + q], h4[q]);
-                }
-                for (; k < k1; ++k) {
-                    const uint64_t i = order[lo + k];
-                    store(i, host::xxh64(a + blocks[i].data_offset, blocks[i].length));
-                }
-            }
-        };
-        fj.run(static_cast<unsigned>(std::min<uint64_t>(pl, (cnt + chunk - 1) / chunk)), work);
+    if (out->empty()) {
+        int dev = 0;
+        HIP_TRY(hipGetDevice(&dev));
+        out->push_back(dev);
     }
     return STORMCK_OK;
 }
 
-// ---- f1, the routed commit --------------------------------------------------------
-// Cost model of the two legs (us), fitted to the end-to-end table measured on MI355X
-// ("End to end from host memory", profiles/r04_commit_e2e/): the host
-// leg hashes a height on one thread at kHostCoreBytesPerUs, or, when the height has at
-// least kHostMinBytesPerThread per thread, on up to nt threads plus a fork/join; the
-// device leg pays a call, then per height a launch and the longer of one XXH64 chain
-// over its longest block and its bytes over the link (in-place reads of the registered
-// arena). Measured (profiles/r04_commit_e2e/x4_host_leg.log): c5 forest 783 us device in
-// place (link 49 GB/s), 745 us on one host thread hashing four blocks at once (51 GB/s;
-// 1,740 us scalar, storm's own rate), 104-144 us on 16; the 3-block commit 63 us device,
-// 4.8 us host.
-namespace {
-constexpr double kHostCoreBytesPerUs = 24000.0;  // one EPYC 9575F thread, scalar XXH64 of 32 KiB blocks
-constexpr double kHostCoreX4BytesPerUs = 48000.0;  // the same thread hashing four blocks at once (AVX-512)
-constexpr double kHostLevelUs = 10.0;            // fork/join of a parallel height
-constexpr double kDevCallUs = 10.0;
-constexpr double kDevChainBytesPerUs = 1600.0;   // one 4-lane chain on gfx950 (32 KiB in ~20 us)
-constexpr double kDevLevelUs = 6.0;
-constexpr double kLinkBytesPerUs = 50000.0;      // PCIe Gen5 x16, in-place reads of registered host memory
-}  // namespace
+// Visible gfx950 devices, each once, in the order given.
+int check_devices(const int* devices, int n_devices, std::vector<int>* out) {
+    if (!devices || n_devices <= 0 || n_devices > 64) return fail(STORMCK_EINVAL, "devices: 1..64 entries");
+    int count = 0;
+    HIP_TRY(hipGetDeviceCount(&count));
+    out->clear();
+    for (int k = 0; k < n_devices; ++k) {
+        if (devices[k] < 0 || devices[k] >= count)
+            return fail(STORMCK_EINVAL, "devices[" + std::to_string(k) + "] = " + std::to_string(devices[k]) +
+                                            " is not a visible device");
+        hipDeviceProp_t prop;
+        HIP_TRY(hipGetDeviceProperties(&prop, devices[k]));
+        if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+            return fail(STORMCK_ENODEV, "devices[" + std::to_string(k) + "] is not gfx950: " + prop.gcnArchName);
+        if (std::find(out->begin(), out->end(), devices[k]) == out->end()) out->push_back(devices[k]);
+    }
+    return STORMCK_OK;
+}
 
-namespace {  // cost model helpers (internal)
+// Threads the host part of a routed call may use: host_threads (0 = the pool), or only the
+// calling thread while another call holds the pool (whose pieces it would wait behind).
+unsigned routed_threads(uint32_t host_threads) {
+    ForkJoin& fj = ForkJoin::get();
+    if (fj.busy()) return 1;
+    return host_threads ? std::min<unsigned>(host_threads, fj.size()) : fj.size();
+}
 
+// One persistent host thread per device drives that device's part of a split (a thread per
+// call would cost ~30 us to start). A call owns a worker from post() to wait(); a balanced
+// split whose worker another call owns runs without that device.
+class DevWorker {
+  public:
+    static DevWorker* of(int dev) {
+        if (dev < 0 || dev >= 64) return nullptr;
+        static std::once_flag once;
+        std::call_once(once, [] {
+            pthread_atfork(nullptr, nullptr, [] {  // a fork()ed child has none of the threads
+                for (auto& w : table_) w = nullptr;
+            });
+        });
+        std::lock_guard<std::mutex> g(make_mu_);
+        if (!table_[dev]) table_[dev] = new DevWorker(dev);  // never destroyed: its thread may be parked at exit
+        return table_[dev];
+    }
+    bool post(std::function<void()> fn, bool wait_if_busy) {
+        if (wait_if_busy) {
+            own_.lock();
+        } else if (!own_.try_lock()) {
+            return false;
+        }
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            job_ = std::move(fn);
+            pending_ = true;
+        }
+        cv_.notify_all();
+        return true;
+    }
+    void wait() {
+        {
+            std::unique_lock<std::mutex> lk(mu_);
+            cv_.wait(lk, [&] { return !pending_; });
+            job_ = nullptr;
+        }
+        own_.unlock();
+    }
+
+  private:
+    explicit DevWorker(int dev) : dev_(dev) { std::thread([this] { loop(); }).detach(); }
+    void loop() {
+        (void)hipSetDevice(dev_);
+        (void)hipGetLastError();
+        for (;;) {
+            std::function<void()> fn;
+            {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [&] { return pending_ && job_ != nullptr; });
+                fn = job_;
+            }
+            fn();
+            {
+                std::lock_guard<std::mutex> g(mu_);
+                pending_ = false;
+            }
+            cv_.notify_all();
+        }
+    }
+    static inline DevWorker* table_[64] = {};
+    static inline std::mutex make_mu_;
+    int dev_;
+    std::mutex own_, mu_;
+    std::condition_variable cv_;
+    std::function<void()> job_;
+    bool pending_ = false;
+};
+
+// n host blocks: block i at base + (offs ? offs[i] : i * stride), (lens ? lens[i] : len) bytes.
+struct Blocks {
+    const uint8_t* base = nullptr;
+    uint64_t stride = 0;
+    const uint64_t* offs = nullptr;
+    const uint32_t* lens = nullptr;
+    uint32_t len = 0;
+    uint64_t n = 0;
+    const uint8_t* at(uint64_t i) const { return base + (offs ? offs[i] : i * stride); }
+    uint64_t len_of(uint64_t i) const { return lens ? lens[i] : len; }
+    uint64_t bytes(uint64_t a, uint64_t b) const {
+        if (!lens) return (b - a) * len;
+        uint64_t s = 0;
+        for (uint64_t i = a; i < b; ++i) s += lens[i];
+        return s;
+    }
+    uint64_t longest() const {
+        if (!lens) return len;
+        uint64_t m = 0;
+        for (uint64_t i = 0; i < n; ++i) m = std::max<uint64_t>(m, lens[i]);
+        return m;
+    }
+};
+
+// XXH64 of blocks [a, b), four chains at once where the CPU has AVX-512: take(i, hash).
+template <class Take>
+void hash_blocks(const Blocks& B, uint64_t a, uint64_t b, Take&& take) {
+    uint64_t i = a;
+    for (; host::has_x4() && i + 4 <= b; i += 4) {
+        const unsigned char* p4[4];
+        size_t n4[4];
+        uint64_t h4[4];
+        for (int q = 0; q < 4; ++q) {
+            p4[q] = B.at(i + q);
+            n4[q] = B.len_of(i + q);
+        }
+        host::xxh64_x4(p4, n4, h4);
+        for (int q = 0; q < 4; ++q) take(i + q, h4[q]);
+    }
+    for (; i < b; ++i) take(i, host::xxh64(B.at(i), B.len_of(i)));
+}
+
+// Where a call's checksums go: called from host threads and device workers at once, on
+// disjoint blocks.
+struct Sink {
+    virtual ~Sink() = default;
+    virtual void one(uint64_t i, uint64_t h) = 0;
+    virtual void range(uint64_t i0, uint64_t cnt, const uint64_t* cs) {
+        for (uint64_t k = 0; k < cnt; ++k) one(i0 + k, cs[k]);
+    }
+};
+
+struct OutSink final : Sink {
+    uint64_t* out;
+    explicit OutSink(uint64_t* o) : out(o) {}
+    void one(uint64_t i, uint64_t h) override { out[i] = h; }
+    void range(uint64_t i0, uint64_t cnt, const uint64_t* cs) override { std::memcpy(out + i0, cs, cnt * 8); }
+};
+
+// The blocks of one call, shared by its host threads (from the front) and its devices
+// (from the back). Balanced: a device claims b bytes so that, with I bytes in flight and
+// rate r_d, it finishes no later than the host threads and the other devices (rate r_o)
+// finish the R bytes nobody has claimed:
+//     L + (I + b) / r_d = (R - b) / r_o   ->   b = (R / r_o - L - I / r_d) / (1 / r_d + 1 / r_o)
+// (L: the chunk's latency); a claim below kSplitMinClaimBytes ends the device's part.
+// Fixed: the devices own exactly the last `fixed` blocks, the host threads the others.
+class SplitQueue {
+  public:
+    SplitQueue(uint64_t n, uint64_t fixed, double bytes_per_block, double r_host, double r_dev, unsigned ndev)
+        : lo_(0), hi_(n), split_(fixed == STORMCK_SPLIT_BALANCED ? UINT64_MAX : n - std::min(fixed, n)),
+          bpb_(bytes_per_block), r_host_(r_host), r_dev_(r_dev), ndev_(ndev) {}
+    bool host(uint64_t piece, uint64_t* a, uint64_t* b) {
+        std::lock_guard<std::mutex> g(mu_);
+        const uint64_t end = split_ != UINT64_MAX ? split_ : hi_;
+        if (lo_ >= end) return false;
+        *a = lo_;
+        *b = std::min(end, lo_ + piece);
+        lo_ = *b;
+        return true;
+    }
+    bool device(double inflight, double lat_us, uint64_t max_blocks, uint64_t* a, uint64_t* b) {
+        std::lock_guard<std::mutex> g(mu_);
+        uint64_t cnt = 0;
+        if (split_ != UINT64_MAX) {
+            if (hi_ <= split_) return false;
+            cnt = std::min(max_blocks, hi_ - split_);
+        } else {
+            if (hi_ <= lo_) return false;
+            const uint64_t avail = hi_ - lo_;
+            const double R = static_cast<double>(avail) * bpb_;
+            const double r_o = r_host_ + (ndev_ - 1) * r_dev_;
+            const double want = r_o <= 0 ? R : (R / r_o - lat_us - inflight / r_dev_) / (1.0 / r_dev_ + 1.0 / r_o);
+            if (want < kSplitMinClaimBytes) return false;
+            cnt = std::min<uint64_t>({static_cast<uint64_t>(want / bpb_), max_blocks, avail});
+            if (cnt == 0) return false;
+        }
+        *a = hi_ - cnt;
+        *b = hi_;
+        hi_ -= cnt;
+        return true;
+    }
+
+  private:
+    std::mutex mu_;
+    uint64_t lo_, hi_, split_;
+    double bpb_, r_host_, r_dev_;
+    unsigned ndev_;
+};
+
+struct SplitArgs {
+    Blocks B;
+    uint32_t plan_len = 0;               // the longest block, which the kernels plan with
+    const uint64_t* expected = nullptr;  // verify: compare instead of returning checksums
+    Sink* sink = nullptr;                // checksums
+    bool in_place = false;               // devices read B.base in place (mapped memory), not by DMA copies
+};
+
+struct DevRun {
+    int rc = STORMCK_OK;
+    std::string err;
+    uint64_t blocks = 0, bytes = 0, first_bad = UINT64_MAX, n_bad = 0;
+    double busy_us = 0;
+};
+
+// Wait for `e` without holding a core: the worker shares the box with the host threads.
+hipError_t wait_event(hipEvent_t e) {
+    for (int spin = 0;; ++spin) {
+        const hipError_t s = hipEventQuery(e);
+        if (s != hipErrorNotReady) return s;
+        (void)hipGetLastError();
+        if (spin < 32) std::this_thread::yield();
+        else std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
+}
+
+// One device's part of a split, on its worker thread (the current device is its own):
+// chunks claimed from the back of the queue through the device context's two stages.
+// DMA mode copies a chunk's contiguous rows into HBM and hashes them there (the host
+// pipeline's stage); in-place mode hands the kernels the chunk's offsets and lets them read
+// the mapped host memory over the link (a commit's blocks are scattered over cache.data).
+void device_part(const SplitArgs& A, SplitQueue& q, double lat_us, DevRun* r) {
+    auto failed = [&](int rc) {
+        r->rc = rc;
+        r->err = g_last_error;
+    };
+    DeviceCtx* c = nullptr;
+    int rc = get_ctx(&c);
+    if (rc) return failed(rc);
+    std::lock_guard<std::mutex> g(c->mu);
+    rc = ensure_ready(c);
+    if (rc) return failed(rc);
+    const Blocks& B = A.B;
+    const uint8_t* d_base = nullptr;
+    if (A.in_place) {
+        void* d = nullptr;
+        const hipError_t e = hipHostGetDevicePointer(&d, const_cast<uint8_t*>(B.base), 0);
+        if (e != hipSuccess)
+            return failed(fail(STORMCK_EHIP, std::string("split: hipHostGetDevicePointer: ") + hipGetErrorString(e)));
+        d_base = static_cast<const uint8_t*>(d);
+    }
+    const double bpb = std::max(1.0, static_cast<double>(B.bytes(0, B.n)) / static_cast<double>(B.n));
+    // blocks per chunk: what the staging chunk holds (DMA), or the offsets and lengths its
+    // pinned buffer holds, about a chunk's worth of bytes (in place)
+    const uint64_t step = B.n == 1 ? std::max<uint64_t>(B.len_of(0), 8) : std::max<uint64_t>(B.stride, 8);
+    const uint64_t max_blocks = A.in_place
+        ? std::max<uint64_t>(1, std::min<uint64_t>(kChunkBytes / 12, static_cast<uint64_t>(kChunkBytes / bpb)))
+        : std::max<uint64_t>(1, kChunkBytes / step);
+    double inflight = 0, t0 = 0, t_end = 0;
+    double stage_bytes[kStages] = {};
+    using ull = unsigned long long;
+
+    auto drain = [&](int k) -> int {
+        Stage& s = c->st[k];
+        if (!s.busy) return STORMCK_OK;
+        const hipError_t e = wait_event(s.done);
+        s.busy = false;
+        inflight -= stage_bytes[k];
+        if (e != hipSuccess) return fail(STORMCK_EHIP, std::string("split: ") + hipGetErrorString(e));
+        const int frc = take_fault(c->device, s.stream);  // a stalled ring kernel left blocks unhashed
+        if (frc) return frc;
+        if (A.expected) {
+            if (s.h_result[1] > 0) {
+                r->n_bad += s.h_result[1];
+                r->first_bad = std::min<uint64_t>(r->first_bad, s.first + s.h_result[0]);
+            }
+        } else {
+            A.sink->range(s.first, s.count, s.h_out);
+        }
+        r->blocks += s.count;
+        r->bytes += static_cast<uint64_t>(stage_bytes[k]);
+        t_end = now_us();
+        return STORMCK_OK;
+    };
+    auto issue = [&](int k, uint64_t a, uint64_t cnt) -> int {
+        Stage& s = c->st[k];
+        const uint8_t* base = nullptr;
+        uint64_t stride = 0;
+        const uint64_t* offs = nullptr;
+        if (!A.in_place) {
+            const uint64_t bytes = (cnt - 1) * B.stride + B.len_of(a + cnt - 1);
+            HIP_TRY(hipMemcpyAsync(s.d_data, B.at(a), bytes, hipMemcpyHostToDevice, s.stream));
+            if (B.lens) HIP_TRY(hipMemcpyAsync(s.d_lens, B.lens + a, cnt * 4, hipMemcpyHostToDevice, s.stream));
+            base = s.d_data;
+            stride = B.stride;
+        } else {
+            uint64_t* po = reinterpret_cast<uint64_t*>(s.pinned);
+            for (uint64_t j = 0; j < cnt; ++j) po[j] = B.offs ? B.offs[a + j] : (a + j) * B.stride;
+            HIP_TRY(hipMemcpyAsync(s.d_offs, po, cnt * 8, hipMemcpyHostToDevice, s.stream));
+            if (B.lens) {
+                uint32_t* pl = reinterpret_cast<uint32_t*>(s.pinned + cnt * 8);
+                std::memcpy(pl, B.lens + a, cnt * 4);
+                HIP_TRY(hipMemcpyAsync(s.d_lens, pl, cnt * 4, hipMemcpyHostToDevice, s.stream));
+            }
+            base = d_base;
+            offs = s.d_offs;
+        }
+        const uint32_t* dl = B.lens ? s.d_lens : nullptr;
+        const uint32_t plan = B.lens ? A.plan_len : B.len;
+        int lrc;
+        if (A.expected) {
+            HIP_TRY(hipMemcpyAsync(s.d_expected, A.expected + a, cnt * 8, hipMemcpyHostToDevice, s.stream));
+            s.h_result[0] = cnt;
+            s.h_result[1] = 0;
+            HIP_TRY(hipMemcpyAsync(s.d_result, s.h_result, 16, hipMemcpyHostToDevice, s.stream));
+            lrc = launch_checksum(base, stride, dl, plan, offs, cnt, nullptr, s.d_expected,
+                                  reinterpret_cast<ull*>(s.d_result), reinterpret_cast<ull*>(s.d_result + 1), s.stream);
+            if (lrc) return lrc;
+            HIP_TRY(hipMemcpyAsync(s.h_result, s.d_result, 16, hipMemcpyDeviceToHost, s.stream));
+        } else {
+            lrc = launch_checksum(base, stride, dl, plan, offs, cnt, s.d_out, nullptr, nullptr, nullptr, s.stream);
+            if (lrc) return lrc;
+            HIP_TRY(hipMemcpyAsync(s.h_out, s.d_out, cnt * 8, hipMemcpyDeviceToHost, s.stream));
+        }
+        HIP_TRY(hipEventRecord(s.done, s.stream));
+        s.first = a;
+        s.count = cnt;
+        s.busy = true;
+        return STORMCK_OK;
+    };
+
+    for (uint64_t k = 0;; ++k) {
+        const int st = static_cast<int>(k % kStages);
+        rc = drain(st);
+        if (rc) break;
+        uint64_t a = 0, b = 0;
+        if (!q.device(inflight, inflight > 0 ? kSplitChunkUs : lat_us, max_blocks, &a, &b)) break;
+        if (t0 == 0) t0 = now_us();
+        stage_bytes[st] = static_cast<double>(B.bytes(a, b));
+        inflight += stage_bytes[st];
+        rc = issue(st, a, b - a);
+        if (rc) break;
+    }
+    for (int k = 0; k < kStages && rc == STORMCK_OK; ++k) rc = drain(k);
+    if (rc) {  // nothing of this call may stay in flight: the stages are reused
+        for (Stage& s : c->st) {
+            (void)hipStreamSynchronize(s.stream);
+            s.busy = false;
+        }
+        return failed(rc);
+    }
+    r->busy_us = t_end > t0 ? t_end - t0 : 0;
+}
+
+struct SplitResult {
+    uint64_t first_bad = 0, n_bad = 0, device_blocks = 0;
+};
+
+// One call's blocks on `pl` host threads and the devices `devs` at once (the host leg when
+// devs is empty). fixed: STORMCK_SPLIT_BALANCED, or the number of blocks (the last ones)
+// the devices hash. Verify (A.expected): *R gets the lowest mismatching index (n if none)
+// and the count over both sides.
+int split_run(const SplitArgs& A, const std::vector<int>& devs, unsigned pl, uint64_t fixed, SplitResult* R) {
+    const Blocks& B = A.B;
+    const uint64_t n = B.n;
+    R->first_bad = n;
+    R->n_bad = 0;
+    R->device_blocks = 0;
+    if (n == 0) return STORMCK_OK;
+    const uint64_t bytes = B.bytes(0, n);
+    const double bpb = std::max(1.0, static_cast<double>(bytes) / static_cast<double>(n));
+    const stormck_route_rates rt = RouteModel::get().now();
+    ForkJoin& fj = ForkJoin::get();
+    pl = std::max(1u, std::min(pl, fj.size()));
+    const unsigned nd = static_cast<unsigned>(devs.size());
+    const double r_dev = A.in_place ? rt.link_inplace : rt.link_pinned;
+    SplitQueue q(n, nd ? fixed : 0, bpb, host_rate(rt, pl), r_dev, nd);
+    const double lat = kDevBatchCallUs + static_cast<double>(A.plan_len) / kDevChainBytesPerUs + kSplitStartUs;
+
+    std::vector<DevRun> runs(nd);
+    std::vector<DevWorker*> posted;
+    for (unsigned k = 0; k < nd; ++k) {
+        DevWorker* w = DevWorker::of(devs[k]);
+        if (!w) {
+            runs[k].rc = STORMCK_EINVAL;
+            runs[k].err = "device index beyond 64";
+            continue;
+        }
+        DevRun* out = &runs[k];
+        // balanced: a worker that another call owns is left out (the host takes its share)
+        if (w->post([&A, &q, lat, out] { device_part(A, q, lat, out); }, fixed != STORMCK_SPLIT_BALANCED))
+            posted.push_back(w);
+    }
+
+    // the host part: pieces from the front, small enough near the meeting point to balance
+    const uint64_t want = nd ? static_cast<uint64_t>(static_cast<double>(bytes) / (64.0 * pl) / bpb) : n / (uint64_t{pl} * 8);
+    const uint64_t piece = (std::max<uint64_t>(4, nd ? std::min<uint64_t>(want, 1024) : want) + 3) / 4 * 4;
+    std::atomic<uint64_t> host_blocks{0}, host_bytes{0}, bad_n{0}, bad_first{n};
+    auto work = [&](unsigned) {
+        uint64_t my_n = 0, my_first = n, my_blocks = 0, my_bytes = 0, a = 0, b = 0;
+        while (q.host(piece, &a, &b)) {
+            hash_blocks(B, a, b, [&](uint64_t i, uint64_t h) {
+                if (!A.expected) {
+                    A.sink->one(i, h);
+                } else if (h != A.expected[i]) {
+                    ++my_n;
+                    my_first = std::min(my_first, i);
+                }
+            });
+            my_blocks += b - a;
+            my_bytes += B.bytes(a, b);
+        }
+        host_blocks.fetch_add(my_blocks, std::memory_order_relaxed);
+        host_bytes.fetch_add(my_bytes, std::memory_order_relaxed);
+        if (my_n) {
+            bad_n.fetch_add(my_n, std::memory_order_relaxed);
+            uint64_t cur = bad_first.load(std::memory_order_relaxed);
+            while (my_first < cur && !bad_first.compare_exchange_weak(cur, my_first, std::memory_order_relaxed)) {
+            }
+        }
+    };
+    const unsigned parts = static_cast<unsigned>(std::min<uint64_t>(pl, (n + piece - 1) / piece));
+    const double h0 = now_us();
+    fj.run(parts, work);
+    const double h_us = now_us() - h0;
+    for (DevWorker* w : posted) w->wait();
+
+    uint64_t fb = bad_first.load(), nb = bad_n.load();
+    for (unsigned k = 0; k < nd; ++k) {
+        const DevRun& r = runs[k];
+        if (r.rc) return fail(r.rc, "device " + std::to_string(devs[k]) + ": " + r.err);
+        R->device_blocks += r.blocks;
+        if (r.n_bad) {
+            nb += r.n_bad;
+            fb = std::min(fb, r.first_bad);
+        }
+    }
+    if (host_blocks.load() + R->device_blocks != n)
+        return fail(STORMCK_EHIP, "split: " + std::to_string(n - host_blocks.load() - R->device_blocks) +
+                                      " blocks left unhashed");
+    R->first_bad = fb;
+    R->n_bad = nb;
+    RouteModel& m = RouteModel::get();
+    m.learn_host(host_bytes.load(), parts, h_us);
+    const double fixed_us = kDevBatchCallUs + static_cast<double>(A.plan_len) / kDevChainBytesPerUs;
+    for (const DevRun& r : runs) m.learn_link(A.in_place ? Link::kInplace : Link::kPinned, r.bytes, r.busy_us - fixed_us);
+    return STORMCK_OK;
+}
+
+// ---- the batch cost model ----------------------------------------------------------
+struct BatchShape {
+    uint64_t bytes = 0, longest = 0;
+};
+
+// Bytes hashed and the longest block; false: blocks overlap (stride below a length).
+bool batch_shape(uint64_t stride, const uint32_t* lens, uint32_t len, uint64_t n, BatchShape* s) {
+    if (lens) {
+        for (uint64_t i = 0; i < n; ++i) {
+            s->bytes += lens[i];
+            s->longest = std::max<uint64_t>(s->longest, lens[i]);
+        }
+    } else {
+        s->bytes = uint64_t{len} * n;
+        s->longest = len;
+    }
+    return n <= 1 || stride >= s->longest;
+}
+
+struct LegPlan {
+    uint32_t leg = STORMCK_LEG_HOST;
+    double us[3] = {0, INFINITY, INFINITY};  // host, device, split
+};
+
+void pick_leg(LegPlan* p) {
+    double best = p->us[0];
+    p->leg = STORMCK_LEG_HOST;
+    if (p->us[1] < best) {
+        best = p->us[1];
+        p->leg = STORMCK_LEG_DEVICE;
+    }
+    if (p->us[2] < kSplitGain * best) p->leg = STORMCK_LEG_SPLIT;
+}
+
+// Time of a split that hashes `bytes` on host threads at r_h and devices at r_d together,
+// or INFINITY if it beats the host alone (host_us) by nothing.
+double split_us(double bytes, double r_h, double r_d, double lat, double overhead, double host_us) {
+    const double t = (bytes + r_d * lat) / (r_h + r_d) + overhead;
+    return t < host_us ? t : INFINITY;
+}
+
+// The three legs of a host-memory batch: the host threads; the device pipeline (a call, one
+// chain over the longest block, the bytes over ndev links, and for pageable memory the first
+// chunk's staging copy, which nothing overlaps); the split (pinned memory only: from
+// pageable memory the devices need host threads to copy, which hash faster than they copy).
+LegPlan plan_batch(const stormck_route_rates& r, uint64_t n, const BatchShape& s, bool pinned, bool staged_ok,
+                   unsigned nt, unsigned ndev) {
+    LegPlan p;
+    const unsigned pl = host_threads_for(s.bytes, nt);
+    const double bytes = static_cast<double>(s.bytes), chain = static_cast<double>(s.longest) / kDevChainBytesPerUs;
+    const double level = pl > 1 ? kHostLevelUs : 0.0;
+    p.us[0] = bytes / host_rate(r, pl) + level;
+    if (ndev && staged_ok) {
+        const double link = pinned ? r.link_pinned : r.link_pageable;
+        const double fill = pinned ? 0.0 : static_cast<double>(std::min<uint64_t>(s.bytes, kChunkBytes)) / kStageCopyBytesPerUs;
+        p.us[1] = kDevBatchCallUs + chain + bytes / (ndev * link) + fill;
+        if (pinned && n >= 2)
+            p.us[2] = split_us(bytes, host_rate(r, pl), ndev * r.link_pinned, kDevBatchCallUs + chain + kSplitStartUs,
+                               level, p.us[0]);
+    }
+    pick_leg(&p);
+    return p;
+}
+
+// ---- the commit cost model ----------------------------------------------------------
 struct CommitShape {
     std::vector<uint64_t> cnt, bytes, longest;  // per height
 };
@@ -2558,174 +3192,151 @@ bool commit_shape(const stormck_dirty_block* blocks, uint64_t n, CommitShape* s)
     return true;
 }
 
-double host_leg_us(const CommitShape& s, unsigned nt) {
-    const double core = host::has_x4() ? kHostCoreX4BytesPerUs : kHostCoreBytesPerUs;
-    double t = 0;
-    for (size_t l = 0; l < s.cnt.size(); ++l) {
-        // the split stormck_commit_host makes
-        const uint64_t pl = std::min<uint64_t>(nt, std::max<uint64_t>(1, s.bytes[l] / kHostMinBytesPerThread));
-        if (pl == 1) {
-            t += static_cast<double>(s.bytes[l]) / core;
-            continue;
+// One height on the host threads: its bytes at the threads' rate, at least one block's
+// chain, and a fork/join when it is spread.
+double host_height_us(const stormck_route_rates& r, const CommitShape& s, size_t l, unsigned nt) {
+    const unsigned pl = host_threads_for(s.bytes[l], nt);
+    const double t = std::max(static_cast<double>(s.bytes[l]) / host_rate(r, pl),
+                              static_cast<double>(s.longest[l]) / r.host_thread);
+    return t + (pl > 1 ? kHostLevelUs : 0.0);
+}
+
+// The three legs of a commit: the host threads, height by height; the device in place over
+// the link (a call, then per height a launch and the longer of one chain over its longest
+// block and its bytes over the link); the split (height 0, the leaves, on both; the upper
+// heights on the host). The device legs need a registered arena.
+LegPlan plan_commit(const stormck_route_rates& r, const CommitShape& s, bool registered, unsigned nt, unsigned ndev) {
+    LegPlan p;
+    p.us[0] = 0;
+    for (size_t l = 0; l < s.cnt.size(); ++l) p.us[0] += host_height_us(r, s, l, nt);
+    if (registered && ndev && !s.cnt.empty()) {
+        p.us[1] = kDevCallUs;
+        for (size_t l = 0; l < s.cnt.size(); ++l)
+            p.us[1] += kDevLevelUs + std::max(static_cast<double>(s.longest[l]) / kDevChainBytesPerUs,
+                                              static_cast<double>(s.bytes[l]) / r.link_inplace);
+        if (s.cnt[0] >= 2) {
+            const double h0 = host_height_us(r, s, 0, nt);
+            const unsigned pl = host_threads_for(s.bytes[0], nt);
+            const double t0 = split_us(static_cast<double>(s.bytes[0]), host_rate(r, pl), ndev * r.link_inplace,
+                                       kDevBatchCallUs + static_cast<double>(s.longest[0]) / kDevChainBytesPerUs +
+                                           kSplitStartUs,
+                                       pl > 1 ? kHostLevelUs : 0.0, h0);
+            p.us[2] = p.us[0] - h0 + t0;
         }
-        const double per_block = static_cast<double>(s.bytes[l]) / static_cast<double>(s.cnt[l]);
-        const uint64_t rounds = (s.cnt[l] + pl - 1) / pl;
-        t += std::max(static_cast<double>(rounds) * per_block, static_cast<double>(s.longest[l])) / core + kHostLevelUs;
     }
-    return t;
+    pick_leg(&p);
+    return p;
 }
 
-double device_leg_us(const CommitShape& s) {
-    double t = kDevCallUs;
-    for (size_t l = 0; l < s.cnt.size(); ++l)
-        t += kDevLevelUs + std::max(static_cast<double>(s.longest[l]) / kDevChainBytesPerUs,
-                                    static_cast<double>(s.bytes[l]) / kLinkBytesPerUs);
-    return t;
-}
-
-}  // namespace
-
-int stormck_commit(void* arena, stormck_dirty_block* blocks, uint64_t n, uint64_t revision,
-                   uint64_t* last_allocated_block, uint64_t* out_checksums, void* stream, uint32_t host_threads,
-                   uint32_t* leg_used) {
-    if (leg_used) *leg_used = STORMCK_LEG_NONE;
-    if (n == 0) return STORMCK_OK;
-    if (!arena || !blocks || !last_allocated_block || !out_checksums) return fail(STORMCK_EINVAL, "null argument");
-    int rc = device_check();  // the routed commit is the GPU engine's: no device, no commit
-    if (rc) return rc;
-    hipPointerAttribute_t attr;
-    const bool known = hipPointerGetAttributes(&attr, arena) == hipSuccess;
-    if (!known) (void)hipGetLastError();
-    if (known && attr.type == hipMemoryTypeDevice) {  // an HBM arena: only the device reaches it
-        if (leg_used) *leg_used = STORMCK_LEG_DEVICE;
-        return stormck_commit_device(arena, blocks, n, revision, last_allocated_block, out_checksums, stream);
-    }
-    const bool registered = known && (attr.type == hipMemoryTypeHost || attr.type == hipMemoryTypeManaged) &&
-                            attr.devicePointer != nullptr;
-    const unsigned nt = host_threads ? std::min<unsigned>(host_threads, ForkJoin::get().size()) : ForkJoin::get().size();
-    CommitShape shape;
-    bool device = false;
-    if (registered && commit_shape(blocks, n, &shape)) device = device_leg_us(shape) < host_leg_us(shape, nt);
-    if (!device) {  // pageable memory, a malformed forest (the host leg says why) or the cheaper leg
-        if (leg_used) *leg_used = STORMCK_LEG_HOST;
-        return stormck_commit_host(arena, blocks, n, revision, last_allocated_block, out_checksums, nt);
-    }
-    if (leg_used) *leg_used = STORMCK_LEG_DEVICE;
-    void* d_arena = nullptr;  // the kernels read and write the registered arena in place
-    HIP_TRY(hipHostGetDevicePointer(&d_arena, arena, 0));
-    return stormck_commit_device(d_arena, blocks, n, revision, last_allocated_block, out_checksums, stream);
-}
-
-// ---- host-memory batches: the host leg and the routed batch ------------------------
-// A batch that lives in host memory (the Go shim's ChecksumBatch / VerifyChecksumBatch)
-// crosses the PCIe link on the device leg (stormck_checksum_host: ~52 GiB/s end to end,
-// DESIGN.md §5), while the host's own threads hash the same bytes four blocks at a time
-// (AVX-512) until host memory bandwidth binds. stormck_checksum_batch routes each batch
-// to the leg the cost model below predicts is faster, as stormck_commit routes a commit.
-namespace {
-// Fitted to the batch table measured on MI355X with its EPYC 9575F host (DESIGN.md §5,
-// "Host-memory batches, routed", profiles/r04_batch_e2e/): 16 host threads streaming an
-// 8 GiB batch from DRAM hash 8.59 GB in 48.0 ms (179 GB/s), below 16 x
-// kHostCoreX4BytesPerUs; the device pipeline moves 8 GiB in 153-154 ms from pageable or
-// registered memory (55.7 GB/s), and a pageable batch first copies its first 256 MiB
-// chunk into pinned staging with nothing to overlap (16K blocks: 15.6 ms pageable against
-// 11.6 ms registered).
-constexpr double kHostMemBytesPerUs = 180000.0;
-constexpr double kPipeBytesPerUs = 55000.0;       // H2D of the pipelined device leg
-constexpr double kStageCopyBytesPerUs = 55000.0;  // pageable -> pinned staging copy (8 threads)
-constexpr double kDevBatchCallUs = 16.0;          // stage, launch, copy back, sync of one small batch
-
-struct BatchShape {
-    uint64_t bytes = 0, longest = 0;
+// ---- f1 on the host threads: the plan and the heights ---------------------------------
+struct CommitPlan {
+    std::vector<uint32_t> order;  // commit position -> the caller's index
+    std::vector<uint64_t> start;  // height h: commit positions [start[h], start[h + 1])
+    std::vector<uint64_t> off;    // commit position -> data_offset
+    std::vector<uint32_t> len;    // commit position -> length
 };
 
-// Bytes hashed and the longest block; false: blocks overlap (stride below a length).
-bool batch_shape(uint64_t stride, const uint32_t* lens, uint32_t len, uint64_t n, BatchShape* s) {
-    if (lens) {
-        for (uint64_t i = 0; i < n; ++i) {
-            s->bytes += lens[i];
-            s->longest = std::max<uint64_t>(s->longest, lens[i]);
-        }
-    } else {
-        s->bytes = uint64_t{len} * n;
-        s->longest = len;
+// Validation, heights, the commit order (by height, index order within a height) and the
+// relocation in that order (cache/cache.go:114-118), with stormck_commit_device's rules and
+// messages; a failure changes nothing.
+int commit_plan(stormck_dirty_block* blocks, uint64_t n, uint64_t revision, uint64_t* last_allocated_block,
+                CommitPlan* P) {
+    if (n > 0xffffffffULL) return fail(STORMCK_EINVAL, "more than 2^32 dirty blocks");
+    std::vector<uint32_t> height(n, 0);
+    for (uint64_t i = 0; i < n; ++i) {
+        const stormck_dirty_block& b = blocks[i];
+        if (b.parent != STORMCK_NO_PARENT && (b.parent < 0 || static_cast<uint64_t>(b.parent) >= n))
+            return fail(STORMCK_EINVAL, "parent index out of range");
+        if (b.origin_pointer != STORMCK_NO_ORIGIN && (b.origin_pointer & 7) != 0)
+            return fail(STORMCK_EINVAL, "origin_pointer must be 8-byte aligned (Go blocks.Pointer alignment)");
     }
-    return n <= 1 || stride >= s->longest;
-}
-
-unsigned batch_threads(const BatchShape& s, unsigned nt) {
-    return static_cast<unsigned>(std::min<uint64_t>(nt, std::max<uint64_t>(1, s.bytes / kHostMinBytesPerThread)));
-}
-
-double batch_host_us(const BatchShape& s, unsigned nt) {
-    const double core = host::has_x4() ? kHostCoreX4BytesPerUs : kHostCoreBytesPerUs;
-    const unsigned pl = batch_threads(s, nt);
-    if (pl == 1) return static_cast<double>(s.bytes) / core;
-    return static_cast<double>(s.bytes) / std::min(core * pl, kHostMemBytesPerUs) + kHostLevelUs;
-}
-
-// The device pipeline: a call, one chain over the longest block, the bytes over the link,
-// and for pageable memory the first chunk's staging copy, which nothing overlaps.
-double batch_device_us(const BatchShape& s, bool pinned) {
-    const double fill = pinned ? 0.0 : static_cast<double>(std::min<uint64_t>(s.bytes, kChunkBytes)) / kStageCopyBytesPerUs;
-    return kDevBatchCallUs + static_cast<double>(s.longest) / kDevChainBytesPerUs +
-           static_cast<double>(s.bytes) / kPipeBytesPerUs + fill;
-}
-
-// The host leg: blocks in pieces from a shared counter on `threads` pool threads (0 = the
-// pool), four at a time where the CPU has AVX-512. Verify mode (expected != null) counts
-// mismatches and keeps the lowest failing index, as the device kernels do.
-int batch_host_leg(const uint8_t* base, uint64_t stride, const uint32_t* lens, uint32_t len, uint64_t n,
-                   uint64_t* out, const uint64_t* expected, uint64_t* first_bad, uint64_t* n_bad, unsigned threads) {
-    BatchShape s;
-    if (!batch_shape(stride, lens, len, n, &s)) return fail(STORMCK_EINVAL, "stride smaller than a block length (blocks overlap)");
-    ForkJoin& fj = ForkJoin::get();
-    const unsigned nt = threads ? std::min<unsigned>(threads, fj.size()) : fj.size();
-    const unsigned pl = batch_threads(s, nt);
-    const uint64_t piece = std::max<uint64_t>(4, (n / (uint64_t{pl} * 8) + 3) / 4 * 4);
-    std::atomic<uint64_t> next{0}, bad_n{0}, bad_first{n};
-    auto work = [&](unsigned) {
-        uint64_t my_n = 0, my_first = n;
-        auto take = [&](uint64_t i, uint64_t h) {
-            if (!expected) {
-                out[i] = h;
-            } else if (h != expected[i]) {
-                ++my_n;
-                my_first = std::min(my_first, i);
-            }
-        };
-        for (;;) {
-            const uint64_t i0 = next.fetch_add(piece, std::memory_order_relaxed);
-            if (i0 >= n) break;
-            const uint64_t i1 = std::min(n, i0 + piece);
-            uint64_t i = i0;
-            for (; host::has_x4() && i + 4 <= i1; i += 4) {
-                const unsigned char* p4[4];
-                size_t n4[4];
-                uint64_t h4[4];
-                for (int q = 0; q < 4; ++q) {
-                    p4[q] = base + (i + q) * stride;
-                    n4[q] = lens ? lens[i + q] : len;
-                }
-                host::xxh64_x4(p4, n4, h4);
-                for (int q = 0; q < 4; ++q) take(i + q, h4[q]);
-            }
-            for (; i < i1; ++i) take(i, host::xxh64(base + i * stride, lens ? lens[i] : len));
+    uint32_t max_h = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        uint64_t cur = i;
+        uint32_t hh = 0;
+        while (blocks[cur].parent != STORMCK_NO_PARENT) {
+            cur = static_cast<uint64_t>(blocks[cur].parent);
+            if (++hh > n) return fail(STORMCK_EINVAL, "parent links form a cycle");
+            if (height[cur] >= hh) break;  // an earlier walk carries it upward
+            height[cur] = hh;
+            max_h = std::max(max_h, hh);
         }
-        if (my_n) {
-            bad_n.fetch_add(my_n, std::memory_order_relaxed);
-            uint64_t cur = bad_first.load(std::memory_order_relaxed);
-            while (my_first < cur && !bad_first.compare_exchange_weak(cur, my_first, std::memory_order_relaxed)) {
-            }
+    }
+    P->start.assign(static_cast<size_t>(max_h) + 2, 0);
+    for (uint64_t i = 0; i < n; ++i) P->start[height[i] + 1]++;
+    if (P->start[1] == 0) return fail(STORMCK_EINVAL, "parent links form a cycle");
+    for (uint32_t l = 0; l <= max_h; ++l) P->start[l + 1] += P->start[l];
+    P->order.resize(n);
+    {
+        std::vector<uint64_t> pos(P->start.begin(), P->start.end() - 1);
+        for (uint64_t i = 0; i < n; ++i) P->order[pos[height[i]]++] = static_cast<uint32_t>(i);
+    }
+    uint64_t last = *last_allocated_block;
+    P->off.resize(n);
+    P->len.resize(n);
+    for (uint64_t k = 0; k < n; ++k) {
+        stormck_dirty_block& b = blocks[P->order[k]];
+        if (b.birth_revision <= revision) {
+            b.address = ++last;
+            b.birth_revision = revision + 1;
         }
-    };
-    fj.run(static_cast<unsigned>(std::min<uint64_t>(pl, (n + piece - 1) / piece)), work);
-    if (first_bad) *first_bad = bad_first.load();
-    if (n_bad) *n_bad = bad_n.load();
+        P->off[k] = b.data_offset;
+        P->len[k] = b.length;
+    }
+    *last_allocated_block = last;
     return STORMCK_OK;
 }
 
-// Host arguments of the batch entry points, checked the same way for both legs.
+// A height's checksums: the caller's out_checksums and, through the block's origin, the
+// Pointer and type its parent keeps (PostCommitFunc, cache/trace.go:274-320).
+struct CommitSink final : Sink {
+    uint8_t* arena;
+    const stormck_dirty_block* blocks;
+    const uint32_t* order;  // this height's slice of the commit order
+    uint64_t* out;
+    CommitSink(uint8_t* a, const stormck_dirty_block* b, const uint32_t* o, uint64_t* c)
+        : arena(a), blocks(b), order(o), out(c) {}
+    void one(uint64_t k, uint64_t h) override {
+        const uint64_t i = order[k];
+        const stormck_dirty_block& b = blocks[i];
+        out[i] = h;
+        if (b.origin_pointer != STORMCK_NO_ORIGIN) {
+            const uint64_t ptr[3] = {h, b.address, b.birth_revision};
+            std::memcpy(arena + b.origin_pointer, ptr, sizeof ptr);
+            arena[b.origin_type] = b.type;
+        }
+    }
+};
+
+// The heights of a planned commit, children first: height 0 (the leaves) on the host
+// threads and `devs` at once (devices read the registered arena in place), every other
+// height on the host threads (they hold a few pointer blocks).
+int commit_heights(uint8_t* arena, stormck_dirty_block* blocks, const CommitPlan& P, uint64_t* out, unsigned nt,
+                   const std::vector<int>& devs, uint64_t device_leaves, uint64_t* device_done) {
+    const std::vector<int> none;
+    for (size_t l = 0; l + 1 < P.start.size(); ++l) {
+        const uint64_t lo = P.start[l], cnt = P.start[l + 1] - lo;
+        if (cnt == 0) continue;
+        SplitArgs A;
+        A.B.base = arena;
+        A.B.offs = P.off.data() + lo;
+        A.B.lens = P.len.data() + lo;
+        A.B.n = cnt;
+        A.plan_len = static_cast<uint32_t>(std::max<uint64_t>(A.B.longest(), 1));
+        A.in_place = true;
+        CommitSink sink(arena, blocks, P.order.data() + lo, out);
+        A.sink = &sink;
+        const bool split = l == 0 && !devs.empty();
+        SplitResult R;
+        const int rc = split_run(A, split ? devs : none, host_threads_for(A.B.bytes(0, cnt), nt),
+                                 split ? device_leaves : STORMCK_SPLIT_BALANCED, &R);
+        if (rc) return rc;
+        if (split && device_done) *device_done = R.device_blocks;
+    }
+    return STORMCK_OK;
+}
+
+// Host arguments of the batch entry points, checked the same way for every leg.
 int batch_args(const void* base, uint64_t n, const uint64_t* out_or_expected) {
     if (n == 0) return STORMCK_OK;
     if (!base) return fail(STORMCK_EINVAL, "base is null");
@@ -2733,17 +3344,58 @@ int batch_args(const void* base, uint64_t n, const uint64_t* out_or_expected) {
     return STORMCK_OK;
 }
 
-// Whether `p` is device memory, which host threads cannot read.
-bool on_device(const void* p) {
-    hipPointerAttribute_t a;
-    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
-        (void)hipGetLastError();
-        return false;
-    }
-    return a.type == hipMemoryTypeDevice;
+Blocks batch_blocks(const void* base, uint64_t stride, const uint32_t* lens, uint32_t len, uint64_t n) {
+    Blocks B;
+    B.base = static_cast<const uint8_t*>(base);
+    B.stride = stride;
+    B.lens = lens;
+    B.len = len;
+    B.n = n;
+    return B;
 }
 
-// The routed batch: the leg the cost model predicts is faster (*leg_used).
+// The host leg of a batch on `threads` pool threads (0 = the pool): no device involved.
+int batch_host_leg(const void* base, uint64_t stride, const uint32_t* lens, uint32_t len, uint64_t n, uint64_t* out,
+                   const uint64_t* expected, uint64_t* first_bad, uint64_t* n_bad, uint32_t threads) {
+    BatchShape s;
+    if (!batch_shape(stride, lens, len, n, &s)) return fail(STORMCK_EINVAL, "stride smaller than a block length (blocks overlap)");
+    if (!host_readable(base, (n - 1) * stride + (lens ? lens[n - 1] : len)))
+        return fail(STORMCK_EINVAL, "base is not readable host memory");
+    ForkJoin& fj = ForkJoin::get();
+    const unsigned nt = threads ? std::min<unsigned>(threads, fj.size()) : fj.size();
+    SplitArgs A;
+    A.B = batch_blocks(base, stride, lens, len, n);
+    A.expected = expected;
+    OutSink sink(out);
+    A.sink = &sink;
+    SplitResult R;
+    const int rc = split_run(A, {}, host_threads_for(s.bytes, nt), STORMCK_SPLIT_BALANCED, &R);
+    if (rc) return rc;
+    if (first_bad) *first_bad = R.first_bad;
+    if (n_bad) *n_bad = R.n_bad;
+    return STORMCK_OK;
+}
+
+// The split leg of a batch (stormck_checksum_split / the routed batch's split).
+int batch_split_leg(const void* base, uint64_t stride, const uint32_t* lens, uint32_t len, uint64_t n, uint64_t* out,
+                    const uint64_t* expected, uint64_t* first_bad, uint64_t* n_bad, const std::vector<int>& devs,
+                    unsigned pl, uint64_t device_blocks, uint64_t* device_done) {
+    SplitArgs A;
+    A.B = batch_blocks(base, stride, lens, len, n);
+    A.plan_len = lens ? static_cast<uint32_t>(std::max<uint64_t>(A.B.longest(), 1)) : len;
+    A.expected = expected;
+    OutSink sink(out);
+    A.sink = &sink;
+    SplitResult R;
+    const int rc = split_run(A, devs, pl, device_blocks, &R);
+    if (rc) return rc;
+    if (first_bad) *first_bad = R.first_bad;
+    if (n_bad) *n_bad = R.n_bad;
+    if (device_done) *device_done = R.device_blocks;
+    return STORMCK_OK;
+}
+
+// The routed batch: the leg the cost model predicts is fastest (*leg_used).
 int batch_routed(const void* base, uint64_t stride, const uint32_t* lens, uint32_t len, uint64_t n, uint64_t* out,
                  const uint64_t* expected, uint64_t* first_bad, uint64_t* n_bad, uint32_t host_threads,
                  uint32_t* leg_used) {
@@ -2759,26 +3411,158 @@ int batch_routed(const void* base, uint64_t stride, const uint32_t* lens, uint32
         if (n_bad) *n_bad = 0;
         return STORMCK_OK;
     }
-    if (on_device(base)) return fail(STORMCK_EINVAL, "base is device memory: use the _device entry points");
-    const unsigned nt = host_threads ? std::min<unsigned>(host_threads, ForkJoin::get().size()) : ForkJoin::get().size();
+    const Mem mem = classify(base, (n - 1) * stride + (lens ? lens[n - 1] : len));
+    if (mem == Mem::kDevice || mem == Mem::kUnreadable) return not_host_memory(mem);
+    std::vector<int> devs;
+    rc = route_devices(&devs);
+    if (rc) return rc;
+    const unsigned nt = routed_threads(host_threads);
     // the device pipeline stages whole blocks through 256 MiB chunks
     const uint64_t step = n == 1 ? std::max<uint64_t>(s.longest, 8) : std::max<uint64_t>(stride, 8);
-    const bool device = step <= kChunkBytes && batch_device_us(s, is_pinned(base)) < batch_host_us(s, nt);
-    if (!device) {
-        if (leg_used) *leg_used = STORMCK_LEG_HOST;
-        return batch_host_leg(static_cast<const uint8_t*>(base), stride, lens, len, n, out, expected, first_bad, n_bad, nt);
+    const bool pinned = mem != Mem::kPageable;
+    const LegPlan p = plan_batch(RouteModel::get().now(), n, s, pinned, step <= kChunkBytes, nt,
+                                 static_cast<unsigned>(devs.size()));
+    if (leg_used) *leg_used = p.leg;
+    if (p.leg == STORMCK_LEG_DEVICE) {
+        const double t0 = now_us();
+        int cur = 0;
+        HIP_TRY(hipGetDevice(&cur));
+        rc = devs.size() == 1 && devs[0] == cur
+                 ? host_pipeline(base, stride, lens, len, n, out, expected, first_bad, n_bad)
+                 : host_pipeline_multi(base, stride, lens, len, n, out, expected, first_bad, n_bad, devs.data(),
+                                       static_cast<int>(devs.size()));
+        if (rc == STORMCK_OK)
+            RouteModel::get().learn_link(pinned ? Link::kPinned : Link::kPageable, s.bytes / devs.size(),
+                                         now_us() - t0 - kDevBatchCallUs -
+                                             static_cast<double>(s.longest) / kDevChainBytesPerUs);
+        return rc;
     }
-    if (leg_used) *leg_used = STORMCK_LEG_DEVICE;
-    return host_pipeline(base, stride, lens, len, n, out, expected, first_bad, n_bad);
+    const unsigned pl = host_threads_for(s.bytes, nt);
+    if (p.leg == STORMCK_LEG_SPLIT)
+        return batch_split_leg(base, stride, lens, len, n, out, expected, first_bad, n_bad, devs, pl,
+                               STORMCK_SPLIT_BALANCED, nullptr);
+    return batch_host_leg(base, stride, lens, len, n, out, expected, first_bad, n_bad, pl);
+}
+
+// The explicit split entry points: pinned or registered memory, the listed devices (or the
+// route devices), the host part on host_threads threads (0 = the pool).
+int split_entry(const void* base, uint64_t stride, const uint32_t* lens, uint32_t len, uint64_t n, uint64_t* out,
+                const uint64_t* expected, uint64_t* first_bad, uint64_t* n_bad, const int* devices, int n_devices,
+                uint32_t host_threads, uint64_t device_blocks, uint64_t* device_done) {
+    if (device_done) *device_done = 0;
+    int rc = batch_args(base, n, expected ? expected : out);
+    if (rc) return rc;
+    BatchShape s;
+    if (!batch_shape(stride, lens, len, n, &s)) return fail(STORMCK_EINVAL, "stride smaller than a block length (blocks overlap)");
+    rc = device_check();
+    if (rc) return rc;
+    std::vector<int> devs;
+    rc = (devices || n_devices) ? check_devices(devices, n_devices, &devs) : route_devices(&devs);
+    if (rc) return rc;
+    if (n == 0) {
+        if (first_bad) *first_bad = 0;
+        if (n_bad) *n_bad = 0;
+        return STORMCK_OK;
+    }
+    const Mem mem = classify(base, (n - 1) * stride + (lens ? lens[n - 1] : len));
+    if (mem == Mem::kDevice || mem == Mem::kUnreadable) return not_host_memory(mem);
+    if (mem == Mem::kPageable)
+        return fail(STORMCK_EINVAL, "the split leg needs pinned or registered host memory (stormck_host_register)");
+    const uint64_t step = n == 1 ? std::max<uint64_t>(s.longest, 8) : std::max<uint64_t>(stride, 8);
+    if (step > kChunkBytes) return fail(STORMCK_EINVAL, "block stride exceeds the staging chunk (256 MiB)");
+    ForkJoin& fj = ForkJoin::get();
+    const unsigned nt = host_threads ? std::min<unsigned>(host_threads, fj.size()) : fj.size();
+    return batch_split_leg(base, stride, lens, len, n, out, expected, first_bad, n_bad, devs,
+                           host_threads_for(s.bytes, nt), device_blocks, device_done);
 }
 
 }  // namespace
 
+extern "C" {
+
+// ---- f1: the host leg, the split and the routed commit ----------------------------------
+int stormck_commit_host(void* arena, stormck_dirty_block* blocks, uint64_t n, uint64_t revision,
+                        uint64_t* last_allocated_block, uint64_t* out_checksums, uint32_t threads) {
+    if (n == 0) return STORMCK_OK;
+    if (!arena || !blocks || !last_allocated_block || !out_checksums) return fail(STORMCK_EINVAL, "null argument");
+    CommitPlan P;
+    const int rc = commit_plan(blocks, n, revision, last_allocated_block, &P);
+    if (rc) return rc;
+    ForkJoin& fj = ForkJoin::get();
+    const unsigned nt = threads ? std::min<unsigned>(threads, fj.size()) : fj.size();
+    return commit_heights(static_cast<uint8_t*>(arena), blocks, P, out_checksums, nt, {}, 0, nullptr);
+}
+
+int stormck_commit_split(void* arena, stormck_dirty_block* blocks, uint64_t n, uint64_t revision,
+                         uint64_t* last_allocated_block, uint64_t* out_checksums, const int* devices, int n_devices,
+                         uint32_t host_threads, uint64_t device_leaves, uint64_t* device_done) {
+    if (device_done) *device_done = 0;
+    if (n == 0) return STORMCK_OK;
+    if (!arena || !blocks || !last_allocated_block || !out_checksums) return fail(STORMCK_EINVAL, "null argument");
+    int rc = device_check();
+    if (rc) return rc;
+    std::vector<int> devs;
+    rc = (devices || n_devices) ? check_devices(devices, n_devices, &devs) : route_devices(&devs);
+    if (rc) return rc;
+    const Mem mem = classify(arena, 1);
+    if (mem != Mem::kMapped)
+        return fail(STORMCK_EINVAL, "the split commit needs the arena registered (stormck_host_register)");
+    CommitPlan P;
+    rc = commit_plan(blocks, n, revision, last_allocated_block, &P);
+    if (rc) return rc;
+    ForkJoin& fj = ForkJoin::get();
+    const unsigned nt = host_threads ? std::min<unsigned>(host_threads, fj.size()) : fj.size();
+    return commit_heights(static_cast<uint8_t*>(arena), blocks, P, out_checksums, nt, devs, device_leaves, device_done);
+}
+
+int stormck_commit(void* arena, stormck_dirty_block* blocks, uint64_t n, uint64_t revision,
+                   uint64_t* last_allocated_block, uint64_t* out_checksums, void* stream, uint32_t host_threads,
+                   uint32_t* leg_used) {
+    if (leg_used) *leg_used = STORMCK_LEG_NONE;
+    if (n == 0) return STORMCK_OK;
+    if (!arena || !blocks || !last_allocated_block || !out_checksums) return fail(STORMCK_EINVAL, "null argument");
+    int rc = device_check();  // the routed commit is the GPU engine's: no device, no commit
+    if (rc) return rc;
+    const Mem mem = classify(arena, 1);
+    if (mem == Mem::kDevice) {  // an HBM arena: only the device reaches it
+        if (leg_used) *leg_used = STORMCK_LEG_DEVICE;
+        return stormck_commit_device(arena, blocks, n, revision, last_allocated_block, out_checksums, stream);
+    }
+    if (mem == Mem::kUnreadable) return not_host_memory(mem);
+    const bool registered = mem == Mem::kMapped;
+    std::vector<int> devs;
+    rc = route_devices(&devs);
+    if (rc) return rc;
+    const unsigned nt = routed_threads(host_threads);
+    CommitShape shape;
+    LegPlan p;  // host unless the arena is registered and the forest well formed (the host leg says why not)
+    if (registered && commit_shape(blocks, n, &shape))
+        p = plan_commit(RouteModel::get().now(), shape, true, nt, static_cast<unsigned>(devs.size()));
+    if (leg_used) *leg_used = p.leg;
+    if (p.leg == STORMCK_LEG_DEVICE) {
+        void* d_arena = nullptr;  // the kernels read and write the registered arena in place
+        HIP_TRY(hipHostGetDevicePointer(&d_arena, arena, 0));
+        return stormck_commit_device(d_arena, blocks, n, revision, last_allocated_block, out_checksums, stream);
+    }
+    // host threads read the arena now: device work the caller queued on `stream` (e.g. a
+    // kernel writing blocks into the registered arena) must have landed first
+    if (registered) HIP_TRY(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
+    if (p.leg == STORMCK_LEG_SPLIT) {
+        CommitPlan P;
+        rc = commit_plan(blocks, n, revision, last_allocated_block, &P);
+        if (rc) return rc;
+        return commit_heights(static_cast<uint8_t*>(arena), blocks, P, out_checksums, nt, devs, STORMCK_SPLIT_BALANCED,
+                              nullptr);
+    }
+    return stormck_commit_host(arena, blocks, n, revision, last_allocated_block, out_checksums, nt);
+}
+
+// ---- host-memory batches ---------------------------------------------------------------
 int stormck_checksum_host_leg(const void* base, uint64_t stride, const uint32_t* lens, uint32_t len, uint64_t n,
                               uint64_t* out, uint32_t threads) {
     const int rc = batch_args(base, n, out);
     if (rc || n == 0) return rc;
-    return batch_host_leg(static_cast<const uint8_t*>(base), stride, lens, len, n, out, nullptr, nullptr, nullptr, threads);
+    return batch_host_leg(base, stride, lens, len, n, out, nullptr, nullptr, nullptr, threads);
 }
 
 int stormck_verify_host_leg(const void* base, uint64_t stride, const uint32_t* lens, uint32_t len, uint64_t n,
@@ -2788,8 +3572,7 @@ int stormck_verify_host_leg(const void* base, uint64_t stride, const uint32_t* l
     *n_bad = 0;
     int rc = batch_args(base, n, expected);
     if (rc || n == 0) return rc;
-    rc = batch_host_leg(static_cast<const uint8_t*>(base), stride, lens, len, n, nullptr, expected, first_bad, n_bad,
-                        threads);
+    rc = batch_host_leg(base, stride, lens, len, n, nullptr, expected, first_bad, n_bad, threads);
     if (rc) return rc;
     if (*n_bad > 0) return fail(STORMCK_EMISMATCH, "checksum mismatch");
     return STORMCK_OK;
@@ -2808,6 +3591,83 @@ int stormck_verify_batch(const void* base, uint64_t stride, const uint32_t* lens
     const int rc = batch_routed(base, stride, lens, len, n, nullptr, expected, first_bad, n_bad, host_threads, leg_used);
     if (rc) return rc;
     if (*n_bad > 0) return fail(STORMCK_EMISMATCH, "checksum mismatch");
+    return STORMCK_OK;
+}
+
+int stormck_checksum_split(const void* base, uint64_t stride, const uint32_t* lens, uint32_t len, uint64_t n,
+                           uint64_t* out, const int* devices, int n_devices, uint32_t host_threads,
+                           uint64_t device_blocks, uint64_t* device_done) {
+    return split_entry(base, stride, lens, len, n, out, nullptr, nullptr, nullptr, devices, n_devices, host_threads,
+                       device_blocks, device_done);
+}
+
+int stormck_verify_split(const void* base, uint64_t stride, const uint32_t* lens, uint32_t len, uint64_t n,
+                         const uint64_t* expected, uint64_t* first_bad, uint64_t* n_bad, const int* devices,
+                         int n_devices, uint32_t host_threads, uint64_t device_blocks, uint64_t* device_done) {
+    if (!first_bad || !n_bad) return fail(STORMCK_EINVAL, "null argument");
+    const int rc = split_entry(base, stride, lens, len, n, nullptr, expected, first_bad, n_bad, devices, n_devices,
+                               host_threads, device_blocks, device_done);
+    if (rc) return rc;
+    if (*n_bad > 0) return fail(STORMCK_EMISMATCH, "checksum mismatch");
+    return STORMCK_OK;
+}
+
+// ---- the route model, for callers and tests --------------------------------------------
+int stormck_route_get_rates(stormck_route_rates* rates) {
+    if (!rates) return fail(STORMCK_EINVAL, "rates is null");
+    *rates = RouteModel::get().now();
+    return STORMCK_OK;
+}
+
+int stormck_route_set_rates(const stormck_route_rates* rates, uint32_t flags) {
+    if (flags & ~STORMCK_RATES_FREEZE) return fail(STORMCK_EINVAL, "unknown flags");
+    if (rates && !(rates->host_thread > 0 && rates->host_memory > 0 && rates->link_pinned > 0 &&
+                   rates->link_pageable > 0 && rates->link_inplace > 0))
+        return fail(STORMCK_EINVAL, "every rate must be positive");
+    RouteModel::get().set(rates, (flags & STORMCK_RATES_FREEZE) != 0);
+    return STORMCK_OK;
+}
+
+int stormck_route_devices(const int* devices, int n_devices) {
+    std::vector<int> devs;
+    if (n_devices != 0) {
+        if (!devices || n_devices < 0 || n_devices > 64) return fail(STORMCK_EINVAL, "devices: 1..64 entries");
+        int rc = device_check();
+        if (rc) return rc;
+        rc = check_devices(devices, n_devices, &devs);
+        if (rc) return rc;
+    }
+    std::lock_guard<std::mutex> g(g_route_mu);
+    g_route_devs = devs;
+    return STORMCK_OK;
+}
+
+int stormck_route_plan_batch(uint64_t stride, const uint32_t* lens, uint32_t len, uint64_t n, uint32_t memory,
+                             uint32_t host_threads, uint32_t n_devices, uint32_t* leg, double* predicted_us) {
+    if (!leg) return fail(STORMCK_EINVAL, "leg is null");
+    if (memory > STORMCK_MEM_PINNED) return fail(STORMCK_EINVAL, "unknown memory kind");
+    BatchShape s;
+    if (!batch_shape(stride, lens, len, n, &s)) return fail(STORMCK_EINVAL, "stride smaller than a block length (blocks overlap)");
+    const unsigned nt = host_threads ? std::min<unsigned>(host_threads, ForkJoin::get().size()) : ForkJoin::get().size();
+    const uint64_t step = n == 1 ? std::max<uint64_t>(s.longest, 8) : std::max<uint64_t>(stride, 8);
+    const LegPlan p = plan_batch(RouteModel::get().now(), n, s, memory == STORMCK_MEM_PINNED, step <= kChunkBytes, nt,
+                                 n_devices);
+    *leg = n ? p.leg : STORMCK_LEG_NONE;
+    if (predicted_us) std::memcpy(predicted_us, p.us, sizeof p.us);
+    return STORMCK_OK;
+}
+
+int stormck_route_plan_commit(const stormck_dirty_block* blocks, uint64_t n, uint32_t memory, uint32_t host_threads,
+                              uint32_t n_devices, uint32_t* leg, double* predicted_us) {
+    if (!leg) return fail(STORMCK_EINVAL, "leg is null");
+    if (memory > STORMCK_MEM_PINNED) return fail(STORMCK_EINVAL, "unknown memory kind");
+    if (n > 0 && !blocks) return fail(STORMCK_EINVAL, "blocks is null");
+    CommitShape shape;
+    if (!commit_shape(blocks, n, &shape)) return fail(STORMCK_EINVAL, "malformed forest (parent range or cycle)");
+    const unsigned nt = host_threads ? std::min<unsigned>(host_threads, ForkJoin::get().size()) : ForkJoin::get().size();
+    const LegPlan p = plan_commit(RouteModel::get().now(), shape, memory == STORMCK_MEM_PINNED, nt, n_devices);
+    *leg = n ? p.leg : STORMCK_LEG_NONE;
+    if (predicted_us) std::memcpy(predicted_us, p.us, sizeof p.us);
     return STORMCK_OK;
 }
 

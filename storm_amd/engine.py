@@ -39,13 +39,21 @@ def may_ring(n: int) -> bool:
 
 def _after_launch(n: int, stream: int, check_status) -> None:
     # check_status: True = synchronise `stream` and raise on a ring fault of this stream
-    # (stormck_device_status); None = do so when the batch could have taken a ring kernel
-    # and the stream is not being captured into a graph (a captured launch reports into
-    # the slot of the stream it was captured on: check that stream after a replay);
-    # False = the caller checks (device_status) itself, e.g. after a series of launches.
+    # (stormck_device_status); None (the default) = do so only when the batch could have
+    # taken a ring kernel, which makes those mid-size launches synchronous; False = the
+    # caller checks (device_status) itself, e.g. once after a series of launches, and the
+    # launch stays asynchronous. A stream that is being captured into a graph is not
+    # checked here (the library reports that for the stream passed, not torch's current
+    # one): a captured launch reports into the slot of the stream it was captured on, so
+    # check that stream after a replay.
     if check_status is None:
-        import torch
-        check_status = may_ring(n) and not torch.cuda.is_current_stream_capturing()
+        check_status = may_ring(n)
+        if check_status:
+            rc = lib.stormck_device_status(stream or None)
+            if rc == _lib.EINVAL and "being captured" in _lib.last_error():
+                return
+            check(rc)
+            return
     if check_status:
         device_status(stream)
 
@@ -143,12 +151,25 @@ def device_alloc(nbytes: int) -> int:
 
 
 def device_alloc_placed(nbytes: int, mode: int, chunk_bytes: int = 0) -> Tuple[int, int]:
-    """A block arena in placement `mode` (_lib.ALLOC_PLAIN / ALLOC_VMM / ALLOC_CONTIGUOUS);
-    returns (device pointer, physical chunk bytes of a VMM arena, else 0)."""
+    """Probe build only (STORMCK_LIBRARY=tools/libstormck_probes.so): a block arena in
+    placement `mode` (_lib.ALLOC_PLAIN / ALLOC_VMM / ALLOC_CONTIGUOUS), the modes measured
+    and rejected in round 4; returns (device pointer, physical chunk bytes of a VMM arena,
+    else 0). The product library allocates with hipMalloc only (device_alloc)."""
     import ctypes
+    if not hasattr(lib, "stormck_device_alloc_placed"):
+        if mode == _lib.ALLOC_PLAIN:
+            return device_alloc(nbytes), 0
+        raise RuntimeError("arena placement modes are in the probe build only: "
+                           "STORMCK_LIBRARY=tools/libstormck_probes.so")
     p, ch = ctypes.c_void_p(), ctypes.c_uint64(0)
     check(lib.stormck_device_alloc_placed(nbytes, mode, chunk_bytes, ctypes.byref(p), ctypes.byref(ch)))
     return int(p.value), int(ch.value)
+
+
+def stream_forget(stream: int) -> None:
+    """Release `stream`'s ring-fault slot before the stream is destroyed (raises if a
+    fault was still pending there)."""
+    check(lib.stormck_stream_forget(stream or None))
 
 
 def device_free(d_ptr: int) -> None:

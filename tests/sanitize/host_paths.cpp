@@ -15,7 +15,8 @@
 //     arena and are compared with the oracle's serial commit; the host pipeline
 //     (pageable and registered sources, parallel staging copies, both stages), the
 //     batched verify and the file read-verify reader threads, and four host threads
-//     calling the library at once.
+//     calling the library at once; the split leg (host threads and the device worker
+//     on one call, fixed and balanced, checksum, verify and commit) from two callers.
 // Exit status 0 = every check passed and the sanitizer reported nothing (sanitizer
 // reports abort the process: halt_on_error / -fno-sanitize-recover).
 #include <fcntl.h>
@@ -373,6 +374,68 @@ static void host_pipeline_paths() {
     unlink(path);
 }
 
+// The split leg: one call's blocks on the host threads (from the front) and the device
+// worker thread (from the back) at once, with fixed boundaries and balanced, checksum and
+// verify, from two caller threads (one call owns the device worker at a time; a balanced
+// call that finds it busy runs without it), then the split commit on a registered arena.
+static void split_paths() {
+    const uint64_t n = 3000, stride = 32768;
+    std::mt19937_64 rng(17);
+    std::vector<uint8_t> buf(n * stride);
+    for (size_t i = 0; i < buf.size(); i += 8) buf[i] = static_cast<uint8_t>(rng());
+    std::vector<uint32_t> lens(n);
+    for (auto& l : lens) l = static_cast<uint32_t>(rng() % (stride + 1));
+    std::vector<uint64_t> want(n);
+    for (uint64_t i = 0; i < n; ++i) want[i] = oracle_xxh64(buf.data() + i * stride, lens[i]);
+    CHECK(stormck_host_register(buf.data(), buf.size()) == STORMCK_OK);
+    const stormck_route_rates slow_host = {2000.0, 8000.0, 55000.0, 50000.0, 50000.0, 0};
+    CHECK(stormck_route_set_rates(&slow_host, STORMCK_RATES_FREEZE) == STORMCK_OK);
+    auto run = [&](int t) {
+        std::vector<uint64_t> got(n);
+        for (uint64_t d : {uint64_t{0}, uint64_t{1}, n / 2, n, STORMCK_SPLIT_BALANCED}) {
+            uint64_t done = 0, fb = 0, nb = 0;
+            std::fill(got.begin(), got.end(), 0);
+            CHECK(stormck_checksum_split(buf.data(), stride, lens.data(), 0, n, got.data(), nullptr, 0, 0, d, &done) ==
+                      STORMCK_OK &&
+                  got == want && (d == STORMCK_SPLIT_BALANCED ? done <= n : done == d));
+            auto bad = want;
+            bad[n / 2 - 1 + t] ^= 1;
+            CHECK(stormck_verify_split(buf.data(), stride, lens.data(), 0, n, bad.data(), &fb, &nb, nullptr, 0, 0, d,
+                                       &done) == STORMCK_EMISMATCH &&
+                  fb == n / 2 - 1 + t && nb == 1);
+        }
+        uint32_t leg = 0;
+        std::fill(got.begin(), got.end(), 0);
+        CHECK(stormck_checksum_batch(buf.data(), stride, lens.data(), 0, n, got.data(), 0, &leg) == STORMCK_OK &&
+              got == want);
+    };
+    std::vector<std::thread> th;
+    for (int t = 0; t < 2; ++t) th.emplace_back(run, t);
+    for (auto& x : th) x.join();
+    CHECK(stormck_host_unregister(buf.data()) == STORMCK_OK);
+    for (uint64_t dl : {uint64_t{0}, uint64_t{1}, uint64_t{700}, STORMCK_SPLIT_BALANCED}) {
+        Forest f = make_forest(2000, 100, 4096, 5, rng, true);
+        const uint64_t nb = f.b.size();
+        std::vector<uint8_t> host(f.arena_bytes, 0);
+        for (uint64_t i = 0; i < nb; ++i)
+            if (f.b[i].type == STORMCK_LEAF_BLOCK)
+                for (uint32_t k = 0; k < f.b[i].length; k += 8) host[f.b[i].data_offset + k] = static_cast<uint8_t>(rng());
+        auto ref_arena = host;
+        auto ref = f.b;
+        uint64_t ref_last = f.last, last = f.last, done = 0;
+        std::vector<uint64_t> ref_cs(nb, 0), cs(nb, 0);
+        CHECK(oracle_commit(ref_arena.data(), ref.data(), nb, 5, &ref_last, ref_cs.data()) == 0);
+        CHECK(stormck_host_register(host.data(), host.size()) == STORMCK_OK);
+        CHECK(stormck_commit_split(host.data(), f.b.data(), nb, 5, &last, cs.data(), nullptr, 0, 0, dl, &done) ==
+                  STORMCK_OK &&
+              (dl == STORMCK_SPLIT_BALANCED || done == dl));
+        CHECK(last == ref_last && cs == ref_cs && host == ref_arena);
+        CHECK(std::memcmp(ref.data(), f.b.data(), nb * sizeof(stormck_dirty_block)) == 0);
+        CHECK(stormck_host_unregister(host.data()) == STORMCK_OK);
+    }
+    CHECK(stormck_route_set_rates(nullptr, STORMCK_RATES_LEARN) == STORMCK_OK);
+}
+
 // Several host threads on one device at once, as cgo callers on many goroutines would
 // be (stormck.h: the library is safe for concurrent callers; host pipelines sharing a
 // device are serialised inside). Each thread hashes and verifies its own batch, makes
@@ -445,6 +508,8 @@ int main() {
     if (device) host_pipeline_paths();
     if (device) concurrent_callers();
     if (device) std::printf("concurrent callers: done\n");
+    if (device) split_paths();
+    if (device) std::printf("split leg: done\n");
     stormck_shutdown();
     std::printf("%s: %d failure(s)\n", g_fail.load() ? "FAILED" : "ok", g_fail.load());
     return g_fail ? 1 : 0;

@@ -40,7 +40,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version():
     from storm_amd import _lib, ABI_VERSION
-    assert _lib.lib.stormck_abi_version() == ABI_VERSION == 4
+    assert _lib.lib.stormck_abi_version() == ABI_VERSION == 5
 
 
 def test_library_build_id_is_the_tree_sources_hash():
@@ -118,8 +118,26 @@ def test_argument_errors_precede_the_device_check():
         ("register empty", lambda: L.stormck_host_register(None, 0)),
         ("alloc null", lambda: L.stormck_device_alloc(16, None)),
         ("alloc 0 bytes", lambda: L.stormck_device_alloc(0, ctypes.byref(ctypes.c_void_p()))),
-        ("placed null", lambda: L.stormck_device_alloc_placed(16, 1, 0, None, None)),
-        ("placed mode", lambda: L.stormck_device_alloc_placed(16, 7, 0, ctypes.byref(ctypes.c_void_p()), None)),
+        ("split null base", lambda: L.stormck_checksum_split(None, 32, None, 32, 4, ctypes.addressof(out), None, 0,
+                                                             0, 0, None)),
+        ("split null out", lambda: L.stormck_checksum_split(1 << 20, 32, None, 32, 4, None, None, 0, 0, 0, None)),
+        ("split overlap", lambda: L.stormck_checksum_split(1 << 20, 16, None, 32, 4, ctypes.addressof(out), None, 0,
+                                                           0, 0, None)),
+        ("verify split null result", lambda: L.stormck_verify_split(1 << 20, 32, None, 32, 4, ctypes.addressof(out),
+                                                                    None, None, None, 0, 0, 0, None)),
+        ("commit split null", lambda: L.stormck_commit_split(None, None, 3, 1, None, None, None, 0, 0, 0, None)),
+        ("route rates null", lambda: L.stormck_route_get_rates(None)),
+        ("route set flags", lambda: L.stormck_route_set_rates(None, 6)),
+        ("route set zero rate", lambda: L.stormck_route_set_rates(ctypes.byref(_lib.RouteRates()), 0)),
+        ("route devices null", lambda: L.stormck_route_devices(None, 2)),
+        ("route devices count", lambda: L.stormck_route_devices((ctypes.c_int * 1)(0), -1)),
+        ("plan leg null", lambda: L.stormck_route_plan_batch(32, None, 32, 4, 0, 0, 1, None, None)),
+        ("plan memory kind", lambda: L.stormck_route_plan_batch(32, None, 32, 4, 5, 0, 1, ctypes.byref(
+            ctypes.c_uint32()), None)),
+        ("plan overlap", lambda: L.stormck_route_plan_batch(16, None, 32, 4, 0, 0, 1, ctypes.byref(ctypes.c_uint32()),
+                                                            None)),
+        ("plan commit null", lambda: L.stormck_route_plan_commit(None, 3, 1, 0, 1, ctypes.byref(ctypes.c_uint32()),
+                                                                 None)),
         ("routed commit null", lambda: L.stormck_commit(None, None, 3, 1, None, None, None, 0, None)),
         ("host leg null", lambda: L.stormck_commit_host(None, None, 3, 1, None, None, 1)),
         ("device pointer null", lambda: L.stormck_host_device_pointer(None, None)),

@@ -957,15 +957,18 @@ def test_device_entry_points_are_graph_capturable(dev):
         assert engine.as_tuple(root) == o.merkle_root(want, 0, n, 1, 1200)
 
 
-@pytest.mark.parametrize("mode,chunk", [(1, 0), (1, 1 << 21), (2, 0), (0, 0)])
-def test_arena_placement_modes(dev, mode, chunk):
-    """stormck_device_alloc_placed: plain hipMalloc, a VMM reservation with one or several
-    physical allocations, a contiguous allocation. A 384 MiB arena in each
-    mode hashes like the oracle through the LDS-DMA kernel and frees cleanly; a VMM
-    arena's VA is the reservation's and its chunk is reported."""
-    from oracle import oracle as o
-    from storm_amd import engine
-    n, stride = 12288, 32768
+PLACEMENT_CHILD = r"""
+import sys
+import numpy as np
+import torch
+sys.path.insert(0, sys.argv[1])
+from oracle import oracle as o
+from storm_amd import _lib, engine, commit as sc
+torch.cuda.init()
+engine.init(0)
+n, stride = 12288, 32768
+want = o.checksum_batch(o.fill_synthetic(n, stride, 7), n, stride, stride, threads=8)
+for mode, chunk in ((1, 0), (1, 1 << 21), (2, 0), (0, 0)):
     ptr, mapped = engine.device_alloc_placed(n * stride, mode, chunk)
     try:
         assert ptr % 4096 == 0
@@ -974,10 +977,42 @@ def test_arena_placement_modes(dev, mode, chunk):
         else:
             assert mapped == 0
         engine.fill_synthetic_device(ptr, stride, n, 7, o.SYNTH_SEED)
-        out = torch.empty(n, dtype=torch.int64, device=dev)
+        out = torch.empty(n, dtype=torch.int64, device="cuda")
         engine.checksum_device(ptr, stride, n, out.data_ptr(), stride)
         torch.cuda.synchronize()
-        want = o.checksum_batch(o.fill_synthetic(n, stride, 7), n, stride, stride, threads=8)
-        assert np.array_equal(_u64(out), want)
+        assert np.array_equal(out.cpu().numpy().view(np.uint64), want), mode
+        # the routed entries know the arena for device memory: the batch refuses it, the
+        # commit takes the device leg (host threads never dereference it)
+        cs = np.zeros(4, dtype=np.uint64)
+        rc = _lib.lib.stormck_checksum_batch(ptr, stride, None, stride, 4, cs.ctypes.data, 0, None)
+        assert rc == _lib.EINVAL and "device memory" in _lib.last_error(), (mode, rc, _lib.last_error())
+        b, size, last = sc.pointer_forest(8, 1000, 10, slot=stride, revision=1)
+        host = o.fill_synthetic(size // stride, stride, 7).reshape(-1).copy()
+        b_ref = b.copy()
+        cs_ref, last_ref = o.commit(host, b_ref, 1, last)
+        got, last_got, leg = sc.commit(ptr, b, 1, last)
+        assert leg == _lib.LEG_DEVICE and last_got == last_ref and np.array_equal(got, cs_ref), mode
+        assert np.array_equal(b, b_ref)
     finally:
         engine.device_free(ptr)
+print("placement modes ok")
+"""
+
+
+def test_arena_placement_modes_probe_build(dev):
+    """The arena placement modes measured and rejected in round 4 (stormck_device_alloc_placed:
+    plain hipMalloc, a VMM reservation with one or several physical allocations, a contiguous
+    allocation; DESIGN_LOG.md) live in the probe build only. Through it, in a child process:
+    a 384 MiB arena in each mode hashes like the oracle through the LDS-DMA kernel and frees
+    cleanly; a VMM arena's chunk is reported; and the routed entry points recognise every
+    mode's arena as device memory (the batch refuses it, the commit takes the device leg and
+    matches the oracle) rather than handing it to host threads."""
+    import subprocess
+    import sys
+    from storm_amd import build as sb
+    from tests.conftest import ROOT
+    env = dict(os.environ, STORMCK_LIBRARY=sb.PROBES_LIB)
+    r = subprocess.run([sys.executable, "-c", PLACEMENT_CHILD, ROOT], cwd=ROOT, capture_output=True, text=True,
+                       env=env, timeout=300)
+    assert r.returncode == 0 and "placement modes ok" in r.stdout, r.stdout + r.stderr
+

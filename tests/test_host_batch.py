@@ -74,6 +74,15 @@ def test_host_leg_verify():
 
 
 def test_host_leg_needs_no_device_but_the_routed_batch_does():
+    """Decided: the routed entry points keep STORMCK_ENODEV without a
+    gfx950 device, even where their cost model would pick the host leg. They are the GPU
+    engine's batch calls, and a library that quietly hashed on the CPU when its device is
+    missing is the silent fallback this build must not have. The operational consequence,
+    stated in INTEGRATION.md §2: a `-tags stormck` storm on a box whose GPU is absent or
+    claimed fails ChecksumBatch / VerifyChecksumBatch / CommitBatch with the library's
+    error (cache.Commit returns it) instead of committing; such a box runs storm built
+    without the tag. The host leg itself (stormck_checksum_host_leg, stormck_commit_host)
+    needs no device and stays callable for a caller that chooses it explicitly."""
     from tests.test_abi import _has_gpu
     if _has_gpu():
         pytest.skip("a device is present")

@@ -58,3 +58,18 @@ def test_probe_build_is_the_larger_one():
     """The rejected variants are template instances the product no longer carries."""
     from storm_amd import build as sb
     assert os.path.getsize(sb.PROBES_LIB) > os.path.getsize(_product())
+
+
+def test_product_library_has_one_allocation_mode():
+    """The arena placement modes (VMM reservations, contiguous allocations) were measured no
+    better than hipMalloc in round 4 and live in the probe build only: the product neither
+    exports stormck_device_alloc_placed nor imports the HIP VMM API."""
+    import ctypes
+    from storm_amd import build as sb
+    lib = ctypes.CDLL(_product())
+    assert not hasattr(lib, "stormck_device_alloc_placed")
+    data = open(_product(), "rb").read()
+    for sym in (b"hipMemCreate", b"hipMemAddressReserve", b"hipMemMap", b"hipExtMallocWithFlags"):
+        assert sym not in data, sym
+    probes = open(sb.PROBES_LIB, "rb").read()
+    assert b"hipMemCreate" in probes and b"stormck_device_alloc_placed" in probes

@@ -1,0 +1,197 @@
+"""The routing model (CPU, no device): which leg a host-memory call takes, and how the
+rates it decides with are measured at run time.
+
+The routed entry points (stormck_checksum_batch / _verify_batch, stormck_commit: the Go
+shim's ChecksumBatch, VerifyChecksumBatch and CommitBatch, which storm's Cache.Commit data
+phase drives, /root/reference/cache/cache.go:87-137) run on the host threads, the
+device(s) over PCIe, or both at once (the split leg). stormck_route_plan_batch /
+_plan_commit expose the decision without a device, so these tests inject rates and check
+the choice and the predicted times against the model's formulas (include/stormck.h,
+"routing of host-memory work"). The learning tests run the host leg itself,
+which needs no device, and watch the rates move.
+"""
+import math
+
+import numpy as np
+import pytest
+
+from storm_amd import _lib, blocks
+from storm_amd import commit as sc
+
+RATES = dict(host_thread=40000.0, host_memory=180000.0, link_pinned=55000.0, link_pageable=50000.0,
+             link_inplace=50000.0)
+LEVEL_US, CALL_US, CHAIN, START_US = 10.0, 16.0, 1600.0, 30.0  # stormck.hip kHostLevelUs ... kSplitStartUs
+POOL = 16
+GIB8 = 262144  # 8 GiB of 32 KiB blocks
+
+
+@pytest.fixture
+def rates():
+    """Freeze the model at RATES (overridable per test); restore the priors after."""
+    def set_(**kw):
+        r = dict(RATES)
+        r.update(kw)
+        blocks.SetRouteRates(r, freeze=True)
+        return r
+    set_()
+    yield set_
+    blocks.SetRouteRates(None)
+
+
+def _pool():
+    # the library pool: min(16, hardware threads) (stormck.hip ForkJoin)
+    import os
+    return min(16, os.cpu_count() or 1)
+
+
+def test_rates_set_get_and_priors(rates):
+    got = blocks.RouteRates()
+    for k, v in RATES.items():
+        assert got[k] == v, k
+    assert got["observations"] == 0
+    blocks.SetRouteRates(None)
+    pri = blocks.RouteRates()
+    assert pri["host_memory"] == 180000.0 and pri["link_pinned"] == 55000.0 and pri["link_inplace"] == 50000.0
+    assert pri["host_thread"] in (24000.0, 48000.0)  # scalar / AVX-512 four-block prior
+
+
+def test_small_batches_stay_on_the_host(rates):
+    for n, length in ((3, 31808), (100, 536), (1, 72)):
+        leg, us = blocks.PlanBatch(n, 32768, length, pinned=True)
+        assert leg == _lib.LEG_HOST, (n, length, us)
+        assert us[0] < us[1]
+
+
+def test_host_time_formula(rates):
+    n, L = 16384, 32768
+    leg, us = blocks.PlanBatch(n, L, L, pinned=False, host_threads=4)
+    assert us[0] == pytest.approx(n * L / min(4 * RATES["host_thread"], RATES["host_memory"]) + LEVEL_US)
+    leg, us = blocks.PlanBatch(n, L, L, pinned=False, host_threads=1)
+    assert us[0] == pytest.approx(n * L / RATES["host_thread"])
+
+
+def test_device_time_formula_pageable_and_pinned(rates):
+    n, L = 16384, 32768
+    B = n * L
+    _, us = blocks.PlanBatch(n, L, L, pinned=False, host_threads=1)
+    fill = min(B, 256 << 20) / 55000.0
+    assert us[1] == pytest.approx(CALL_US + L / CHAIN + B / RATES["link_pageable"] + fill)
+    assert math.isinf(us[2])  # pageable memory: no split (the devices would need host copies)
+    _, us = blocks.PlanBatch(n, L, L, pinned=True, host_threads=1)
+    assert us[1] == pytest.approx(CALL_US + L / CHAIN + B / RATES["link_pinned"])
+
+
+def test_split_formula_and_choice(rates):
+    """The split: (B + k r_d L) / (r_h + k r_d) + fork/join, taken when 5% faster than both
+    single legs; more devices, more links."""
+    L = 32768
+    B = GIB8 * L
+    pl = _pool()
+    r_h = min(pl * RATES["host_thread"], RATES["host_memory"]) if pl > 1 else RATES["host_thread"]
+    lat = CALL_US + L / CHAIN + START_US
+    prev = None
+    for k in (1, 2, 8):
+        leg, us = blocks.PlanBatch(GIB8, L, L, pinned=True, n_devices=k)
+        r_d = k * RATES["link_pinned"]
+        want = (B + r_d * lat) / (r_h + r_d) + (LEVEL_US if pl > 1 else 0)
+        assert us[2] == pytest.approx(want), k
+        assert leg == _lib.LEG_SPLIT, (k, us)
+        if prev is not None:
+            assert us[2] < prev
+        prev = us[2]
+
+
+def test_no_device_means_host(rates):
+    leg, us = blocks.PlanBatch(GIB8, 32768, 32768, pinned=True, n_devices=0)
+    assert leg == _lib.LEG_HOST and math.isinf(us[1]) and math.isinf(us[2])
+
+
+def test_one_host_thread_large_pageable_goes_to_the_device(rates):
+    leg, us = blocks.PlanBatch(GIB8, 32768, 32768, pinned=False, host_threads=1)
+    assert leg == _lib.LEG_DEVICE, us
+
+
+def test_a_slow_link_keeps_everything_on_the_host(rates):
+    rates(link_pinned=500.0, link_pageable=500.0, link_inplace=500.0)
+    for pinned in (False, True):
+        leg, us = blocks.PlanBatch(GIB8, 32768, 32768, pinned=pinned)
+        assert leg == _lib.LEG_HOST, (pinned, us)
+
+
+def test_a_fast_host_makes_the_split_a_tie_and_keeps_the_host(rates):
+    """When the link adds under 5% to the host's rate the split is not taken (no flapping
+    between two legs of about the same time)."""
+    rates(host_thread=400000.0, host_memory=4000000.0)
+    leg, us = blocks.PlanBatch(GIB8, 32768, 32768, pinned=True)
+    if _pool() > 1:
+        assert leg == _lib.LEG_HOST, us
+
+
+def _forest(n_leaves, length=32768):
+    b, size, last = sc.pointer_forest(n_leaves, length, 1200, slot=32768, revision=1)
+    return b
+
+
+def test_commit_plan(rates):
+    big = _forest(131072)
+    leg, us = sc.plan_commit(big, registered=True)
+    assert leg == _lib.LEG_SPLIT and us[2] < 0.95 * min(us[0], us[1]), us
+    leg, us = sc.plan_commit(big, registered=False)
+    assert leg == _lib.LEG_HOST and math.isinf(us[1]) and math.isinf(us[2])
+    leg, us = sc.plan_commit(big, registered=True, n_devices=0)
+    assert leg == _lib.LEG_HOST
+    three = _forest(2, 31808)
+    leg, us = sc.plan_commit(three, registered=True)
+    assert leg == _lib.LEG_HOST and us[0] < 20, us
+    # the split only ever touches the leaves: its time is the host's minus the leaf height's gain
+    assert us[2] == math.inf or us[2] < us[0]
+
+
+def test_commit_plan_rejects_a_malformed_forest(rates):
+    b = _forest(25)
+    b["parent"][3] = 10 ** 6
+    import ctypes
+    leg = ctypes.c_uint32()
+    assert _lib.lib.stormck_route_plan_commit(b.ctypes.data, len(b), 1, 0, 1, ctypes.byref(leg), None) == _lib.EINVAL
+
+
+def _rows(n, stride, seed):
+    return np.random.default_rng(seed).integers(0, 256, size=n * stride, dtype=np.uint8)
+
+
+def test_host_leg_measures_the_per_thread_rate():
+    """A one-thread host leg of >= 8 MiB moves host_thread toward its observed rate
+    (EWMA weight 1/4); a frozen model does not move."""
+    n, stride = 512, 32768  # 16 MiB
+    buf = _rows(n, stride, 3)
+    r = dict(RATES, host_thread=1.0)
+    blocks.SetRouteRates(r)  # learning
+    try:
+        blocks.ChecksumBatchHost(buf, n, stride, stride, threads=1)
+        got = blocks.RouteRates()
+        assert got["observations"] == 1
+        assert got["host_thread"] > 1000.0  # 1 + (observed - 1) / 4, observed in GB/s
+        assert got["host_memory"] == RATES["host_memory"]
+        blocks.SetRouteRates(r, freeze=True)
+        blocks.ChecksumBatchHost(buf, n, stride, stride, threads=1)
+        assert blocks.RouteRates()["host_thread"] == 1.0
+        # below 8 MiB nothing is learned
+        blocks.SetRouteRates(r)
+        blocks.ChecksumBatchHost(buf, 64, stride, stride, threads=1)
+        assert blocks.RouteRates()["observations"] == 0
+    finally:
+        blocks.SetRouteRates(None)
+
+
+def test_pool_pass_below_the_threads_rate_measures_the_memory_cap():
+    if _pool() < 2:
+        pytest.skip("one hardware thread")
+    n, stride = 1024, 32768  # 32 MiB
+    buf = _rows(n, stride, 4)
+    blocks.SetRouteRates(dict(RATES, host_thread=1e9, host_memory=1.0))
+    try:
+        blocks.ChecksumBatchHost(buf, n, stride, stride, threads=2)
+        got = blocks.RouteRates()
+        assert got["observations"] == 1 and got["host_memory"] > 1000.0 and got["host_thread"] == 1e9
+    finally:
+        blocks.SetRouteRates(None)

@@ -1,0 +1,63 @@
+#!/bin/bash
+# One GPU session on the MI355X box (the one runner; it replaces the per-session scripts of
+# rounds 1-4, whose logs stay under profiles/):
+#
+#   gpurun -- 'bash tools/gpu_session.sh <tag> <step> [<step> ...]'
+#
+# Output goes to gpurun_out/<tag>/. Each step runs under its own time limit, and the
+# session stops at the first step that fails (a fault, an abort or a timeout ends it: no
+# retries). Steps:
+#   tests                  every -m gpu test
+#   tests:<file>[,<file>]  the -m gpu tests of those files
+#   smoke                  __graft_entry__.smoke()
+#   bench                  the default bench line (c3, BASELINE metric)
+#   batch_e2e commit_e2e gather c5 commit keytags
+#                          bench.py --workload <step> --steps 7
+#   prof                   rocprofv3 --kernel-trace --stats of a 5-step c3 bench
+#   pmc                    FETCH_SIZE / WRITE_SIZE of the c3 kernel (separate passes)
+set -o pipefail
+tag=${1:?usage: gpu_session.sh <tag> <step>...}
+shift
+out=gpurun_out/$tag
+mkdir -p "$out"
+export TMPDIR=/tmp
+PYTEST=(python -u -m pytest -m gpu -x -v --timeout 300 --timeout-method thread)
+for step in "$@"; do
+    echo "== $step $(date +%T)"
+    case $step in
+        tests)
+            timeout -k 10 1500 "${PYTEST[@]}" tests > "$out/tests.log" 2>&1; rc=$?
+            grep -E "passed|failed|error" "$out/tests.log" | tail -3 ;;
+        tests:*)
+            files=${step#tests:}
+            name=$(echo "$files" | tr ',/' '__')
+            timeout -k 10 900 "${PYTEST[@]}" ${files//,/ } > "$out/tests_$name.log" 2>&1; rc=$?
+            grep -E "passed|failed|error" "$out/tests_$name.log" | tail -3 ;;
+        smoke)
+            timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$out/smoke.log" 2>&1; rc=$?
+            tail -1 "$out/smoke.log" ;;
+        bench)
+            timeout -k 10 400 python bench.py > "$out/bench.log" 2>&1; rc=$?
+            tail -c 400 "$out/bench.log"; echo ;;
+        batch_e2e|commit_e2e|gather|c5|commit|keytags)
+            timeout -k 10 900 python bench.py --workload "$step" --steps 7 > "$out/$step.log" 2>&1; rc=$?
+            tail -c 300 "$out/$step.log"; echo ;;
+        prof)
+            timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$out/prof" -o run -- \
+                python3 bench.py --steps 5 --no-cpu > "$out/prof.log" 2>&1; rc=$?
+            tail -c 300 "$out/prof.log"; echo ;;
+        pmc)
+            rc=0
+            for c in FETCH_SIZE WRITE_SIZE; do
+                timeout -s KILL 300 rocprofv3 --pmc "$c" -d "$out/pmc_$c" -o run -- \
+                    python3 bench.py --steps 2 --warmup 1 --settle 0 --no-cpu > "$out/pmc_$c.log" 2>&1 || { rc=$?; break; }
+            done ;;
+        *)
+            echo "unknown step $step"; rc=2 ;;
+    esac
+    if [ "$rc" -ne 0 ]; then
+        echo "step $step failed: $rc"
+        exit "$rc"
+    fi
+done
+echo "== done $(date +%T)"
