@@ -346,14 +346,17 @@ int stormck_commit(void* arena, stormck_dirty_block* blocks, uint64_t n, uint64_
  *                       host does, until they meet. The devices DMA (batch) or read in place
  *                       (commit) pinned or registered memory, with no host copy.
  * The choice is the smallest time a cost model predicts. Its rates (bytes per microsecond)
- * start at priors measured on an MI355X box and are measured again by the calls themselves:
- * every host, device or split leg large enough to time updates its rate (EWMA). */
+ * and the devices' start latency start at priors measured on an MI355X box and are measured
+ * again by the calls themselves: every host, device or split leg large enough to time
+ * updates its rate (EWMA). */
 typedef struct stormck_route_rates {
     double host_thread;    /* one host thread (four blocks at once where the CPU has AVX-512) */
     double host_memory;    /* the host pool's cap (host memory bandwidth, shared cores) */
     double link_pinned;    /* one device's pipeline from pinned or registered host memory */
     double link_pageable;  /* one device's pipeline from pageable memory (through pinned staging) */
     double link_inplace;   /* one device's kernels reading registered host memory in place */
+    double device_latency; /* microseconds from a split's start until a device's first chunk is
+                            * back, beyond that chunk's bytes over the link (wake, launch, sync) */
     uint64_t observations; /* calls that updated the rates since the priors or the last set */
 } stormck_route_rates;
 int stormck_route_get_rates(stormck_route_rates* rates);

@@ -49,11 +49,13 @@ class NoDeviceError(StormckError):
 
 
 class RouteRates(ctypes.Structure):
-    """stormck_route_rates: the routing model's rates, bytes per microsecond."""
+    """stormck_route_rates: the routing model's rates (bytes per microsecond) and the
+    devices' start latency in a split (microseconds)."""
 
     _fields_ = [("host_thread", ctypes.c_double), ("host_memory", ctypes.c_double),
                 ("link_pinned", ctypes.c_double), ("link_pageable", ctypes.c_double),
-                ("link_inplace", ctypes.c_double), ("observations", c_uint64)]
+                ("link_inplace", ctypes.c_double), ("device_latency", ctypes.c_double),
+                ("observations", c_uint64)]
 
     def as_dict(self) -> dict:
         return {f: getattr(self, f) for f, _ in self._fields_}

@@ -49,22 +49,27 @@ class ForkJoin {
         return *instance_;
     }
     unsigned size() const { return nw_ + 1; }
-    // Whether another caller's job holds the pool right now (advisory: a routed call that
-    // finds it busy plans its host work for its own thread, which run() never queues).
-    bool busy() {
-        if (!run_mu_.try_lock()) return true;
-        run_mu_.unlock();
-        return false;
+    // How long another caller's job is predicted to hold the pool, in microseconds (0: the
+    // pool is free; advisory). A routed call that finds the pool held either waits for it or
+    // runs on its own thread, which run() never queues, whichever it predicts is faster.
+    double busy_for_us() {
+        if (run_mu_.try_lock()) {
+            run_mu_.unlock();
+            return 0.0;
+        }
+        return std::max(1.0, busy_until_.load(std::memory_order_relaxed) - clock_us());
     }
-    // fn(t) for t in [0, parts); parts is clamped to size(); the caller runs t = 0
+    // fn(t) for t in [0, parts); parts is clamped to size(); the caller runs t = 0.
+    // expected_us: how long the job is predicted to take (what busy_for_us reports).
     template <class F>
-    void run(unsigned parts, F&& fn) {
+    void run(unsigned parts, F&& fn, double expected_us = 0) {
         parts = std::min(parts, size());
         if (parts <= 1) {
             fn(0u);
             return;
         }
         std::lock_guard<std::mutex> serial(run_mu_);
+        busy_until_.store(clock_us() + expected_us, std::memory_order_relaxed);
         std::function<void(unsigned)> job = [&](unsigned t) {
             if (t < parts) fn(t);
         };
@@ -103,8 +108,12 @@ class ForkJoin {
             remaining_.fetch_sub(1, std::memory_order_release);
         }
     }
+    static double clock_us() {
+        return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+    }
     static inline ForkJoin* instance_ = nullptr;
     static inline std::mutex make_mu_;
+    std::atomic<double> busy_until_{0.0};
     unsigned nw_ = 0;
     std::mutex run_mu_, mu_;
     std::condition_variable cv_;
@@ -2529,7 +2538,6 @@ constexpr double kDevLevelUs = 6.0;               // device commit: a launch per
 constexpr double kDevChainBytesPerUs = 1600.0;    // one 4-lane XXH64 chain on gfx950 (32 KiB in ~20 us)
 constexpr double kDevBatchCallUs = 16.0;          // stage, launch, copy back and sync one small batch
 constexpr double kStageCopyBytesPerUs = 55000.0;  // pageable -> pinned staging copy (8 threads)
-constexpr double kSplitStartUs = 30.0;            // a device worker wakes and starts its first chunk
 constexpr double kSplitChunkUs = 8.0;             // a chunk issued behind one in flight: launch, copy back
 constexpr double kSplitMinClaimBytes = 1 << 20;   // a smaller device claim costs about what it saves
 constexpr double kSplitGain = 0.95;               // the split is taken only when predicted 5% faster
@@ -2541,7 +2549,9 @@ constexpr double kPriorHostThread = 24000.0;    // one thread, scalar XXH64 (no 
 constexpr double kPriorHostMemory = 180000.0;   // the pool: host memory bound (the slower box, 179 GB/s)
 constexpr double kPriorLinkPinned = 55000.0;    // the device pipeline from pinned / registered memory
 constexpr double kPriorLinkPageable = 55000.0;  // the same through pinned staging, copy overlapped
-constexpr double kPriorLinkInplace = 50000.0;   // kernels reading registered memory in place (49-52 GB/s)
+constexpr double kPriorLinkInplace = 50000.0;   // kernels reading registered memory in place (49-55 GB/s)
+constexpr double kPriorDeviceLatencyUs = 150.0; // a split's device part until its first chunk is back
+                                                // (profiles/r05_first/: c5-size splits ~150 us over the host)
 constexpr double kLearnWeight = 0.25;           // EWMA weight of one call's observed rate
 constexpr uint64_t kLearnMinHostBytes = 8ULL << 20;   // below: fork/join noise
 constexpr uint64_t kLearnMinLinkBytes = 64ULL << 20;  // below: launch and sync noise
@@ -2592,6 +2602,16 @@ class RouteModel {
         r = ewma(r, rate);
         ++r_.observations;
     }
+    // A split's device part: its first chunk came back `us` after the call posted it, of
+    // which `bytes` over the link at the current rate account for `bytes / rate`.
+    void learn_latency(uint64_t bytes, double rate, double us) {
+        if (us <= 0 || rate <= 0) return;
+        const double lat = std::max(1.0, us - static_cast<double>(bytes) / rate);
+        std::lock_guard<std::mutex> g(mu_);
+        if (frozen_) return;
+        r_.device_latency = ewma(r_.device_latency, lat);
+        ++r_.observations;
+    }
 
   private:
     RouteModel() : r_(priors()) {}
@@ -2603,6 +2623,7 @@ class RouteModel {
         r.link_pinned = kPriorLinkPinned;
         r.link_pageable = kPriorLinkPageable;
         r.link_inplace = kPriorLinkInplace;
+        r.device_latency = kPriorDeviceLatencyUs;
         return r;
     }
     static double ewma(double old, double obs) { return old + kLearnWeight * (obs - old); }
@@ -2661,12 +2682,19 @@ int check_devices(const int* devices, int n_devices, std::vector<int>* out) {
     return STORMCK_OK;
 }
 
-// Threads the host part of a routed call may use: host_threads (0 = the pool), or only the
-// calling thread while another call holds the pool (whose pieces it would wait behind).
-unsigned routed_threads(uint32_t host_threads) {
+// Threads the host part of a routed call may use: host_threads (0 = the pool). While another
+// call holds the pool, waiting for it pays only when the predicted wait plus this call's
+// time on the pool beats this call on its own thread (a small call behind a large one runs
+// at once on its caller's thread; a large one queues behind it). time_with(t): the call's
+// predicted time with t threads.
+template <class TimeWith>
+unsigned routed_threads(uint32_t host_threads, TimeWith&& time_with) {
     ForkJoin& fj = ForkJoin::get();
-    if (fj.busy()) return 1;
-    return host_threads ? std::min<unsigned>(host_threads, fj.size()) : fj.size();
+    const unsigned nt = host_threads ? std::min<unsigned>(host_threads, fj.size()) : fj.size();
+    if (nt <= 1) return 1;
+    const double busy = fj.busy_for_us();
+    if (busy <= 0) return nt;
+    return busy + time_with(nt) < time_with(1) ? nt : 1;
 }
 
 // One persistent host thread per device drives that device's part of a split (a thread per
@@ -2860,24 +2888,32 @@ struct DevRun {
     std::string err;
     uint64_t blocks = 0, bytes = 0, first_bad = UINT64_MAX, n_bad = 0;
     double busy_us = 0;
+    double first_done = 0;     // when its first chunk came back (now_us clock; 0: none)
+    uint64_t first_bytes = 0;  // that chunk's bytes
 };
 
-// Wait for `e` without holding a core: the worker shares the box with the host threads.
+// Wait for `e`. The worker polls, yielding its core to the host threads between polls, for
+// up to kSplitSpinUs (a sleep costs ~60 us of timer slack, which at the end of a split is
+// time the whole call waits), then sleeps between polls.
+constexpr double kSplitSpinUs = 2000.0;
 hipError_t wait_event(hipEvent_t e) {
-    for (int spin = 0;; ++spin) {
+    const double t0 = now_us();
+    for (;;) {
         const hipError_t s = hipEventQuery(e);
         if (s != hipErrorNotReady) return s;
         (void)hipGetLastError();
-        if (spin < 32) std::this_thread::yield();
+        if (now_us() - t0 < kSplitSpinUs) std::this_thread::yield();
         else std::this_thread::sleep_for(std::chrono::microseconds(20));
     }
 }
 
 // One device's part of a split, on its worker thread (the current device is its own):
 // chunks claimed from the back of the queue through the device context's two stages.
-// DMA mode copies a chunk's contiguous rows into HBM and hashes them there (the host
-// pipeline's stage); in-place mode hands the kernels the chunk's offsets and lets them read
-// the mapped host memory over the link (a commit's blocks are scattered over cache.data).
+// In-place mode (mapped memory: registered, as the Go binding's cache.data) lets the kernels
+// read the chunk's blocks over the link where they are, strided or at the offsets of a
+// commit's scattered blocks, and needs no copy engine: a chunk is one launch and one small
+// copy back, so the first one returns soonest. DMA mode (page-locked memory the device cannot
+// map) copies the chunk's rows into HBM first, as the host pipeline's stages do.
 void device_part(const SplitArgs& A, SplitQueue& q, double lat_us, DevRun* r) {
     auto failed = [&](int rc) {
         r->rc = rc;
@@ -2929,6 +2965,10 @@ void device_part(const SplitArgs& A, SplitQueue& q, double lat_us, DevRun* r) {
         r->blocks += s.count;
         r->bytes += static_cast<uint64_t>(stage_bytes[k]);
         t_end = now_us();
+        if (r->first_done == 0) {
+            r->first_done = t_end;
+            r->first_bytes = static_cast<uint64_t>(stage_bytes[k]);
+        }
         return STORMCK_OK;
     };
     auto issue = [&](int k, uint64_t a, uint64_t cnt) -> int {
@@ -2943,16 +2983,21 @@ void device_part(const SplitArgs& A, SplitQueue& q, double lat_us, DevRun* r) {
             base = s.d_data;
             stride = B.stride;
         } else {
-            uint64_t* po = reinterpret_cast<uint64_t*>(s.pinned);
-            for (uint64_t j = 0; j < cnt; ++j) po[j] = B.offs ? B.offs[a + j] : (a + j) * B.stride;
-            HIP_TRY(hipMemcpyAsync(s.d_offs, po, cnt * 8, hipMemcpyHostToDevice, s.stream));
-            if (B.lens) {
-                uint32_t* pl = reinterpret_cast<uint32_t*>(s.pinned + cnt * 8);
-                std::memcpy(pl, B.lens + a, cnt * 4);
-                HIP_TRY(hipMemcpyAsync(s.d_lens, pl, cnt * 4, hipMemcpyHostToDevice, s.stream));
+            uint8_t* pin = s.pinned;
+            if (B.offs) {  // a gather (a commit height): the chunk's offsets
+                std::memcpy(pin, B.offs + a, cnt * 8);
+                HIP_TRY(hipMemcpyAsync(s.d_offs, pin, cnt * 8, hipMemcpyHostToDevice, s.stream));
+                pin += cnt * 8;
+                base = d_base;
+                offs = s.d_offs;
+            } else {  // strided rows, read where they are
+                base = d_base + a * B.stride;
+                stride = B.stride;
             }
-            base = d_base;
-            offs = s.d_offs;
+            if (B.lens) {
+                std::memcpy(pin, B.lens + a, cnt * 4);
+                HIP_TRY(hipMemcpyAsync(s.d_lens, pin, cnt * 4, hipMemcpyHostToDevice, s.stream));
+            }
         }
         const uint32_t* dl = B.lens ? s.d_lens : nullptr;
         const uint32_t plan = B.lens ? A.plan_len : B.len;
@@ -3023,8 +3068,10 @@ int split_run(const SplitArgs& A, const std::vector<int>& devs, unsigned pl, uin
     pl = std::max(1u, std::min(pl, fj.size()));
     const unsigned nd = static_cast<unsigned>(devs.size());
     const double r_dev = A.in_place ? rt.link_inplace : rt.link_pinned;
-    SplitQueue q(n, nd ? fixed : 0, bpb, host_rate(rt, pl), r_dev, nd);
-    const double lat = kDevBatchCallUs + static_cast<double>(A.plan_len) / kDevChainBytesPerUs + kSplitStartUs;
+    const double r_host = host_rate(rt, pl);
+    SplitQueue q(n, nd ? fixed : 0, bpb, r_host, r_dev, nd);
+    const double lat = rt.device_latency;
+    const double t_post = now_us();
 
     std::vector<DevRun> runs(nd);
     std::vector<DevWorker*> posted;
@@ -3070,7 +3117,7 @@ int split_run(const SplitArgs& A, const std::vector<int>& devs, unsigned pl, uin
     };
     const unsigned parts = static_cast<unsigned>(std::min<uint64_t>(pl, (n + piece - 1) / piece));
     const double h0 = now_us();
-    fj.run(parts, work);
+    fj.run(parts, work, static_cast<double>(bytes) / (r_host + nd * r_dev));
     const double h_us = now_us() - h0;
     for (DevWorker* w : posted) w->wait();
 
@@ -3092,7 +3139,10 @@ int split_run(const SplitArgs& A, const std::vector<int>& devs, unsigned pl, uin
     RouteModel& m = RouteModel::get();
     m.learn_host(host_bytes.load(), parts, h_us);
     const double fixed_us = kDevBatchCallUs + static_cast<double>(A.plan_len) / kDevChainBytesPerUs;
-    for (const DevRun& r : runs) m.learn_link(A.in_place ? Link::kInplace : Link::kPinned, r.bytes, r.busy_us - fixed_us);
+    for (const DevRun& r : runs) {
+        m.learn_link(A.in_place ? Link::kInplace : Link::kPinned, r.bytes, r.busy_us - fixed_us);
+        if (r.first_done > 0) m.learn_latency(r.first_bytes, r_dev, r.first_done - t_post);
+    }
     return STORMCK_OK;
 }
 
@@ -3118,6 +3168,7 @@ bool batch_shape(uint64_t stride, const uint32_t* lens, uint32_t len, uint64_t n
 struct LegPlan {
     uint32_t leg = STORMCK_LEG_HOST;
     double us[3] = {0, INFINITY, INFINITY};  // host, device, split
+    double best() const { return us[leg == STORMCK_LEG_DEVICE ? 1 : (leg == STORMCK_LEG_SPLIT ? 2 : 0)]; }
 };
 
 void pick_leg(LegPlan* p) {
@@ -3140,7 +3191,8 @@ double split_us(double bytes, double r_h, double r_d, double lat, double overhea
 // The three legs of a host-memory batch: the host threads; the device pipeline (a call, one
 // chain over the longest block, the bytes over ndev links, and for pageable memory the first
 // chunk's staging copy, which nothing overlaps); the split (pinned memory only: from
-// pageable memory the devices need host threads to copy, which hash faster than they copy).
+// pageable memory the devices need host threads to copy, which hash faster than they copy),
+// the devices reading in place after their start latency.
 LegPlan plan_batch(const stormck_route_rates& r, uint64_t n, const BatchShape& s, bool pinned, bool staged_ok,
                    unsigned nt, unsigned ndev) {
     LegPlan p;
@@ -3153,8 +3205,7 @@ LegPlan plan_batch(const stormck_route_rates& r, uint64_t n, const BatchShape& s
         const double fill = pinned ? 0.0 : static_cast<double>(std::min<uint64_t>(s.bytes, kChunkBytes)) / kStageCopyBytesPerUs;
         p.us[1] = kDevBatchCallUs + chain + bytes / (ndev * link) + fill;
         if (pinned && n >= 2)
-            p.us[2] = split_us(bytes, host_rate(r, pl), ndev * r.link_pinned, kDevBatchCallUs + chain + kSplitStartUs,
-                               level, p.us[0]);
+            p.us[2] = split_us(bytes, host_rate(r, pl), ndev * r.link_inplace, r.device_latency, level, p.us[0]);
     }
     pick_leg(&p);
     return p;
@@ -3218,9 +3269,7 @@ LegPlan plan_commit(const stormck_route_rates& r, const CommitShape& s, bool reg
             const double h0 = host_height_us(r, s, 0, nt);
             const unsigned pl = host_threads_for(s.bytes[0], nt);
             const double t0 = split_us(static_cast<double>(s.bytes[0]), host_rate(r, pl), ndev * r.link_inplace,
-                                       kDevBatchCallUs + static_cast<double>(s.longest[0]) / kDevChainBytesPerUs +
-                                           kSplitStartUs,
-                                       pl > 1 ? kHostLevelUs : 0.0, h0);
+                                       r.device_latency, pl > 1 ? kHostLevelUs : 0.0, h0);
             p.us[2] = p.us[0] - h0 + t0;
         }
     }
@@ -3379,9 +3428,10 @@ int batch_host_leg(const void* base, uint64_t stride, const uint32_t* lens, uint
 // The split leg of a batch (stormck_checksum_split / the routed batch's split).
 int batch_split_leg(const void* base, uint64_t stride, const uint32_t* lens, uint32_t len, uint64_t n, uint64_t* out,
                     const uint64_t* expected, uint64_t* first_bad, uint64_t* n_bad, const std::vector<int>& devs,
-                    unsigned pl, uint64_t device_blocks, uint64_t* device_done) {
+                    unsigned pl, uint64_t device_blocks, uint64_t* device_done, bool in_place) {
     SplitArgs A;
     A.B = batch_blocks(base, stride, lens, len, n);
+    A.in_place = in_place;
     A.plan_len = lens ? static_cast<uint32_t>(std::max<uint64_t>(A.B.longest(), 1)) : len;
     A.expected = expected;
     OutSink sink(out);
@@ -3416,12 +3466,15 @@ int batch_routed(const void* base, uint64_t stride, const uint32_t* lens, uint32
     std::vector<int> devs;
     rc = route_devices(&devs);
     if (rc) return rc;
-    const unsigned nt = routed_threads(host_threads);
     // the device pipeline stages whole blocks through 256 MiB chunks
     const uint64_t step = n == 1 ? std::max<uint64_t>(s.longest, 8) : std::max<uint64_t>(stride, 8);
     const bool pinned = mem != Mem::kPageable;
-    const LegPlan p = plan_batch(RouteModel::get().now(), n, s, pinned, step <= kChunkBytes, nt,
-                                 static_cast<unsigned>(devs.size()));
+    const stormck_route_rates rt = RouteModel::get().now();
+    auto plan_for = [&](unsigned t) {
+        return plan_batch(rt, n, s, pinned, step <= kChunkBytes, t, static_cast<unsigned>(devs.size()));
+    };
+    const unsigned nt = routed_threads(host_threads, [&](unsigned t) { return plan_for(t).best(); });
+    const LegPlan p = plan_for(nt);
     if (leg_used) *leg_used = p.leg;
     if (p.leg == STORMCK_LEG_DEVICE) {
         const double t0 = now_us();
@@ -3440,7 +3493,7 @@ int batch_routed(const void* base, uint64_t stride, const uint32_t* lens, uint32
     const unsigned pl = host_threads_for(s.bytes, nt);
     if (p.leg == STORMCK_LEG_SPLIT)
         return batch_split_leg(base, stride, lens, len, n, out, expected, first_bad, n_bad, devs, pl,
-                               STORMCK_SPLIT_BALANCED, nullptr);
+                               STORMCK_SPLIT_BALANCED, nullptr, mem == Mem::kMapped);
     return batch_host_leg(base, stride, lens, len, n, out, expected, first_bad, n_bad, pl);
 }
 
@@ -3473,7 +3526,7 @@ int split_entry(const void* base, uint64_t stride, const uint32_t* lens, uint32_
     ForkJoin& fj = ForkJoin::get();
     const unsigned nt = host_threads ? std::min<unsigned>(host_threads, fj.size()) : fj.size();
     return batch_split_leg(base, stride, lens, len, n, out, expected, first_bad, n_bad, devs,
-                           host_threads_for(s.bytes, nt), device_blocks, device_done);
+                           host_threads_for(s.bytes, nt), device_blocks, device_done, mem == Mem::kMapped);
 }
 
 }  // namespace
@@ -3533,11 +3586,16 @@ int stormck_commit(void* arena, stormck_dirty_block* blocks, uint64_t n, uint64_
     std::vector<int> devs;
     rc = route_devices(&devs);
     if (rc) return rc;
-    const unsigned nt = routed_threads(host_threads);
     CommitShape shape;
-    LegPlan p;  // host unless the arena is registered and the forest well formed (the host leg says why not)
-    if (registered && commit_shape(blocks, n, &shape))
-        p = plan_commit(RouteModel::get().now(), shape, true, nt, static_cast<unsigned>(devs.size()));
+    const bool planned = commit_shape(blocks, n, &shape);  // false: malformed (the host leg says why)
+    const stormck_route_rates rt = RouteModel::get().now();
+    auto plan_for = [&](unsigned t) {
+        return plan_commit(rt, shape, registered, t, static_cast<unsigned>(devs.size()));
+    };
+    const unsigned nt = planned ? routed_threads(host_threads, [&](unsigned t) { return plan_for(t).best(); })
+                                : routed_threads(host_threads, [](unsigned) { return 0.0; });
+    LegPlan p;  // host unless the arena is registered and the forest well formed
+    if (planned) p = plan_for(nt);
     if (leg_used) *leg_used = p.leg;
     if (p.leg == STORMCK_LEG_DEVICE) {
         void* d_arena = nullptr;  // the kernels read and write the registered arena in place
@@ -3622,8 +3680,8 @@ int stormck_route_get_rates(stormck_route_rates* rates) {
 int stormck_route_set_rates(const stormck_route_rates* rates, uint32_t flags) {
     if (flags & ~STORMCK_RATES_FREEZE) return fail(STORMCK_EINVAL, "unknown flags");
     if (rates && !(rates->host_thread > 0 && rates->host_memory > 0 && rates->link_pinned > 0 &&
-                   rates->link_pageable > 0 && rates->link_inplace > 0))
-        return fail(STORMCK_EINVAL, "every rate must be positive");
+                   rates->link_pageable > 0 && rates->link_inplace > 0 && rates->device_latency >= 0))
+        return fail(STORMCK_EINVAL, "every rate must be positive (and the latency not negative)");
     RouteModel::get().set(rates, (flags & STORMCK_RATES_FREEZE) != 0);
     return STORMCK_OK;
 }

@@ -19,8 +19,8 @@ from storm_amd import _lib, blocks
 from storm_amd import commit as sc
 
 RATES = dict(host_thread=40000.0, host_memory=180000.0, link_pinned=55000.0, link_pageable=50000.0,
-             link_inplace=50000.0)
-LEVEL_US, CALL_US, CHAIN, START_US = 10.0, 16.0, 1600.0, 30.0  # stormck.hip kHostLevelUs ... kSplitStartUs
+             link_inplace=52000.0, device_latency=120.0)
+LEVEL_US, CALL_US, CHAIN = 10.0, 16.0, 1600.0  # stormck.hip kHostLevelUs, kDevBatchCallUs, kDevChainBytesPerUs
 POOL = 16
 GIB8 = 262144  # 8 GiB of 32 KiB blocks
 
@@ -52,6 +52,7 @@ def test_rates_set_get_and_priors(rates):
     blocks.SetRouteRates(None)
     pri = blocks.RouteRates()
     assert pri["host_memory"] == 180000.0 and pri["link_pinned"] == 55000.0 and pri["link_inplace"] == 50000.0
+    assert pri["device_latency"] == 150.0
     assert pri["host_thread"] in (24000.0, 48000.0)  # scalar / AVX-512 four-block prior
 
 
@@ -82,17 +83,18 @@ def test_device_time_formula_pageable_and_pinned(rates):
 
 
 def test_split_formula_and_choice(rates):
-    """The split: (B + k r_d L) / (r_h + k r_d) + fork/join, taken when 5% faster than both
-    single legs; more devices, more links."""
+    """The split: (B + k r_d L) / (r_h + k r_d) + fork/join, with r_d the in-place link rate
+    and L the devices' measured start latency, taken when 5% faster than both single legs;
+    more devices, more links."""
     L = 32768
     B = GIB8 * L
     pl = _pool()
     r_h = min(pl * RATES["host_thread"], RATES["host_memory"]) if pl > 1 else RATES["host_thread"]
-    lat = CALL_US + L / CHAIN + START_US
+    lat = RATES["device_latency"]
     prev = None
     for k in (1, 2, 8):
         leg, us = blocks.PlanBatch(GIB8, L, L, pinned=True, n_devices=k)
-        r_d = k * RATES["link_pinned"]
+        r_d = k * RATES["link_inplace"]
         want = (B + r_d * lat) / (r_h + r_d) + (LEVEL_US if pl > 1 else 0)
         assert us[2] == pytest.approx(want), k
         assert leg == _lib.LEG_SPLIT, (k, us)
@@ -116,6 +118,22 @@ def test_a_slow_link_keeps_everything_on_the_host(rates):
     for pinned in (False, True):
         leg, us = blocks.PlanBatch(GIB8, 32768, 32768, pinned=pinned)
         assert leg == _lib.LEG_HOST, (pinned, us)
+
+
+def test_the_start_latency_keeps_short_calls_off_the_split(rates):
+    """A split pays the devices' start latency before they return anything: with the pool,
+    a c5-size batch (38 MB, ~200 us on the host) does not split when the latency is a large
+    part of it, and does when it is small; with one host thread it splits either way."""
+    c5 = [31808] * 1200 + [30000, 72]
+    rates(device_latency=150.0, host_memory=400000.0)
+    leg, us = blocks.PlanBatch(len(c5), 32768, lens=c5, pinned=True)
+    if _pool() >= 8:
+        assert leg == _lib.LEG_HOST, us
+    leg, us = blocks.PlanBatch(len(c5), 32768, lens=c5, pinned=True, host_threads=1)
+    assert leg == _lib.LEG_SPLIT, us
+    rates(device_latency=1.0, host_memory=100000.0)
+    leg, us = blocks.PlanBatch(len(c5), 32768, lens=c5, pinned=True)
+    assert leg == _lib.LEG_SPLIT, us
 
 
 def test_a_fast_host_makes_the_split_a_tie_and_keeps_the_host(rates):

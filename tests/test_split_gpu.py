@@ -297,7 +297,8 @@ def test_route_devices_and_rates_learned_on_the_gpu():
     reg = _filled(n, stride, 9)
     try:
         # the device leg is the model's choice (a 1-byte/us host), the link prior far too low
-        blocks.SetRouteRates(dict(SLOW_HOST, link_pinned=1000.0, host_thread=1.0, host_memory=1.0))
+        blocks.SetRouteRates(dict(SLOW_HOST, link_pinned=1000.0, link_inplace=1000.0, host_thread=1.0,
+                                  host_memory=1.0))
         got, leg = blocks.ChecksumBatchLeg(reg.a, n, stride, stride, host_threads=1)
         assert leg == _lib.LEG_DEVICE
         r = blocks.RouteRates()
