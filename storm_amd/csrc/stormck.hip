@@ -94,7 +94,10 @@ class ForkJoin {
         uint64_t seen = 0;
         for (;;) {
             uint64_t g = gen_.load(std::memory_order_acquire);
-            for (int spin = 0; g == seen && spin < 4096; ++spin) {
+            // a short spin catches the next pass of the same call (the commit issues its
+            // passes back to back); longer ones would burn the CPU quota a GPU box gives the
+            // process (16 CPUs there, with 256 in the affinity mask) while nothing runs
+            for (const double t0 = clock_us(); g == seen && clock_us() - t0 < kSpinUs;) {
                 std::this_thread::yield();
                 g = gen_.load(std::memory_order_acquire);
             }
@@ -108,6 +111,7 @@ class ForkJoin {
             remaining_.fetch_sub(1, std::memory_order_release);
         }
     }
+    static constexpr double kSpinUs = 50.0;
     static double clock_us() {
         return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
     }
@@ -963,6 +967,7 @@ constexpr int kStages = 2;
 struct Stage {
     hipStream_t stream = nullptr;
     hipEvent_t done = nullptr;
+    hipEvent_t ready = nullptr;     // split leg: the same, waited for without spinning (blocking sync)
     uint8_t* pinned = nullptr;      // staging for pageable sources
     uint8_t* d_data = nullptr;
     uint32_t* d_lens = nullptr;
@@ -1014,6 +1019,7 @@ int ensure_ready(DeviceCtx* c) {
     for (Stage& s : c->st) {
         HIP_TRY(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
         HIP_TRY(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&s.ready, hipEventDisableTiming | hipEventBlockingSync));
         HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&s.pinned), kChunkBytes, hipHostMallocDefault));
         HIP_TRY(hipMalloc(&s.d_data, kChunkBytes));
         const uint64_t maxb = kChunkBytes / 8;  // smallest admissible stride is 8 bytes per block
@@ -1046,6 +1052,7 @@ void release_ctx(DeviceCtx* c) {
         (void)hipHostFree(s.h_out);
         (void)hipHostFree(s.h_result);
         if (s.done) (void)hipEventDestroy(s.done);
+        if (s.ready) (void)hipEventDestroy(s.ready);
         if (s.stream) (void)hipStreamDestroy(s.stream);
         s = Stage();
     }
@@ -2540,6 +2547,7 @@ constexpr double kDevBatchCallUs = 16.0;          // stage, launch, copy back an
 constexpr double kStageCopyBytesPerUs = 55000.0;  // pageable -> pinned staging copy (8 threads)
 constexpr double kSplitChunkUs = 8.0;             // a chunk issued behind one in flight: launch, copy back
 constexpr double kSplitMinClaimBytes = 1 << 20;   // a smaller device claim costs about what it saves
+constexpr double kSplitDmaBytes = 32 << 20;       // strided claims from this size take the copy engine
 constexpr double kSplitGain = 0.95;               // the split is taken only when predicted 5% faster
 
 // Priors, bytes/us: the rates measured on an MI355X box with its EPYC 9575F host
@@ -2888,24 +2896,16 @@ struct DevRun {
     std::string err;
     uint64_t blocks = 0, bytes = 0, first_bad = UINT64_MAX, n_bad = 0;
     double busy_us = 0;
-    double first_done = 0;     // when its first chunk came back (now_us clock; 0: none)
-    uint64_t first_bytes = 0;  // that chunk's bytes
+    double started = 0, first_issue = 0;  // when the worker began, issued its first chunk (now_us clock)
+    double first_done = 0;                // when its first chunk came back (0: none)
+    double finished = 0;
+    uint64_t first_bytes = 0;             // that chunk's bytes
 };
 
-// Wait for `e`. The worker polls, yielding its core to the host threads between polls, for
-// up to kSplitSpinUs (a sleep costs ~60 us of timer slack, which at the end of a split is
-// time the whole call waits), then sleeps between polls.
-constexpr double kSplitSpinUs = 2000.0;
-hipError_t wait_event(hipEvent_t e) {
-    const double t0 = now_us();
-    for (;;) {
-        const hipError_t s = hipEventQuery(e);
-        if (s != hipErrorNotReady) return s;
-        (void)hipGetLastError();
-        if (now_us() - t0 < kSplitSpinUs) std::this_thread::yield();
-        else std::this_thread::sleep_for(std::chrono::microseconds(20));
-    }
-}
+// A split's device worker waits for its chunks in the kernel (a blocking-sync event: an
+// interrupt wakes it), holding no CPU: the host threads it runs beside use all the CPU the
+// process gets (a GPU box caps it by quota, so a spinning waiter would throttle them).
+hipError_t wait_event(hipEvent_t e) { return hipEventSynchronize(e); }
 
 // One device's part of a split, on its worker thread (the current device is its own):
 // chunks claimed from the back of the queue through the device context's two stages.
@@ -2948,7 +2948,7 @@ void device_part(const SplitArgs& A, SplitQueue& q, double lat_us, DevRun* r) {
     auto drain = [&](int k) -> int {
         Stage& s = c->st[k];
         if (!s.busy) return STORMCK_OK;
-        const hipError_t e = wait_event(s.done);
+        const hipError_t e = wait_event(s.ready);
         s.busy = false;
         inflight -= stage_bytes[k];
         if (e != hipSuccess) return fail(STORMCK_EHIP, std::string("split: ") + hipGetErrorString(e));
@@ -2976,7 +2976,10 @@ void device_part(const SplitArgs& A, SplitQueue& q, double lat_us, DevRun* r) {
         const uint8_t* base = nullptr;
         uint64_t stride = 0;
         const uint64_t* offs = nullptr;
-        if (!A.in_place) {
+        // strided rows go through the copy engine when the chunk is large (55.7 GB/s against
+        // ~43 for kernels reading in place, profiles/r05_second/), in place when it is small
+        // (no copy to wait for: the first chunk returns sooner)
+        if (!B.offs && (!A.in_place || stage_bytes[k] >= kSplitDmaBytes)) {
             const uint64_t bytes = (cnt - 1) * B.stride + B.len_of(a + cnt - 1);
             HIP_TRY(hipMemcpyAsync(s.d_data, B.at(a), bytes, hipMemcpyHostToDevice, s.stream));
             if (B.lens) HIP_TRY(hipMemcpyAsync(s.d_lens, B.lens + a, cnt * 4, hipMemcpyHostToDevice, s.stream));
@@ -3016,20 +3019,21 @@ void device_part(const SplitArgs& A, SplitQueue& q, double lat_us, DevRun* r) {
             if (lrc) return lrc;
             HIP_TRY(hipMemcpyAsync(s.h_out, s.d_out, cnt * 8, hipMemcpyDeviceToHost, s.stream));
         }
-        HIP_TRY(hipEventRecord(s.done, s.stream));
+        HIP_TRY(hipEventRecord(s.ready, s.stream));
         s.first = a;
         s.count = cnt;
         s.busy = true;
         return STORMCK_OK;
     };
 
+    r->started = now_us();
     for (uint64_t k = 0;; ++k) {
         const int st = static_cast<int>(k % kStages);
         rc = drain(st);
         if (rc) break;
         uint64_t a = 0, b = 0;
         if (!q.device(inflight, inflight > 0 ? kSplitChunkUs : lat_us, max_blocks, &a, &b)) break;
-        if (t0 == 0) t0 = now_us();
+        if (t0 == 0) r->first_issue = t0 = now_us();
         stage_bytes[st] = static_cast<double>(B.bytes(a, b));
         inflight += stage_bytes[st];
         rc = issue(st, a, b - a);
@@ -3044,11 +3048,19 @@ void device_part(const SplitArgs& A, SplitQueue& q, double lat_us, DevRun* r) {
         return failed(rc);
     }
     r->busy_us = t_end > t0 ? t_end - t0 : 0;
+    r->finished = now_us();
 }
 
 struct SplitResult {
     uint64_t first_bad = 0, n_bad = 0, device_blocks = 0;
 };
+
+constexpr uint64_t kLatencyProbeBytes = 16ULL << 20;
+
+bool trace_on() {
+    static const bool on = std::getenv("STORMCK_TRACE") != nullptr;
+    return on;
+}
 
 // One call's blocks on `pl` host threads and the devices `devs` at once (the host leg when
 // devs is empty). fixed: STORMCK_SPLIT_BALANCED, or the number of blocks (the last ones)
@@ -3090,7 +3102,7 @@ int split_run(const SplitArgs& A, const std::vector<int>& devs, unsigned pl, uin
 
     // the host part: pieces from the front, small enough near the meeting point to balance
     const uint64_t want = nd ? static_cast<uint64_t>(static_cast<double>(bytes) / (64.0 * pl) / bpb) : n / (uint64_t{pl} * 8);
-    const uint64_t piece = (std::max<uint64_t>(4, nd ? std::min<uint64_t>(want, 1024) : want) + 3) / 4 * 4;
+    const uint64_t piece = (std::max<uint64_t>(nd ? 8 : 4, nd ? std::min<uint64_t>(want, 1024) : want) + 3) / 4 * 4;
     std::atomic<uint64_t> host_blocks{0}, host_bytes{0}, bad_n{0}, bad_first{n};
     auto work = [&](unsigned) {
         uint64_t my_n = 0, my_first = n, my_blocks = 0, my_bytes = 0, a = 0, b = 0;
@@ -3141,7 +3153,26 @@ int split_run(const SplitArgs& A, const std::vector<int>& devs, unsigned pl, uin
     const double fixed_us = kDevBatchCallUs + static_cast<double>(A.plan_len) / kDevChainBytesPerUs;
     for (const DevRun& r : runs) {
         m.learn_link(A.in_place ? Link::kInplace : Link::kPinned, r.bytes, r.busy_us - fixed_us);
-        if (r.first_done > 0) m.learn_latency(r.first_bytes, r_dev, r.first_done - t_post);
+        // the start latency, from first chunks small enough that their transfer is a
+        // minor, well-estimated part of the time to their return
+        if (r.first_done > 0 && r.first_bytes <= kLatencyProbeBytes)
+            m.learn_latency(r.first_bytes, r_dev, r.first_done - t_post);
+    }
+    if (trace_on()) {
+        const double t_end = now_us();
+        std::string d;
+        char buf[256];
+        for (size_t k = 0; k < runs.size(); ++k) {
+            const DevRun& r = runs[k];
+            std::snprintf(buf, sizeof buf,
+                          " dev%d{blocks=%llu start=%.1f issue=%.1f first_back=%.1f(%.2fMB) end=%.1f}", devs[k],
+                          static_cast<unsigned long long>(r.blocks), r.started - t_post, r.first_issue - t_post,
+                          r.first_done - t_post, r.first_bytes / 1e6, r.finished - t_post);
+            d += buf;
+        }
+        std::fprintf(stderr, "[stormck] split n=%llu pl=%u host{blocks=%llu end=%.1f} total=%.1f us%s\n",
+                     static_cast<unsigned long long>(n), parts, static_cast<unsigned long long>(host_blocks.load()),
+                     h0 + h_us - t_post, t_end - t_post, d.c_str());
     }
     return STORMCK_OK;
 }
