@@ -400,7 +400,7 @@ def commit_e2e_workload(a):
                    and the device in place (from the back) at once, upper heights on the
                    host (split_dev_share = the leaves the device hashed / all leaves),
       split_1      the same with one host thread,
-      routed       stormck_commit (the library's choice of the three, DESIGN §4),
+      routed       stormck_commit (the library's choice of the three, DESIGN §4.2),
       routed_1     the same with one host thread allowed (host cores kept for storm),
     and, for reference, dev_hbm: the same forest with cache.data in HBM (device-resident,
     the north-star configuration). Forests: storm's c5 commits (BenchmarkKeyStore's
@@ -525,7 +525,7 @@ def batch_e2e_workload(a):
       host_1       stormck_checksum_host_leg on 1 thread (storm's serial xxhash.Sum64 loop
                    costs about twice this: one scalar chain per block),
       host_all     stormck_checksum_host_leg on every usable thread,
-      routed       stormck_checksum_batch (the library's choice, DESIGN §4), pool threads,
+      routed       stormck_checksum_batch (the library's choice, DESIGN §4.2), pool threads,
       routed_1     the same with one host thread allowed (host cores kept for storm);
     then on the same memory registered with stormck_host_register (as the Go binding's
     cache.data):
@@ -1014,7 +1014,7 @@ def block_checksum_workload(a) -> int:
 
     # The arena is the process's first device allocation (at N > 1, after RCCL's own
     # buffers), taken by plain hipMalloc through the library rather than torch's caching
-    # allocator, so a profiled and a plain process place it the same way.
+    # allocator, so a profiled and a plain process place it the same way (DESIGN_LOG.md §5).
     mode, chunk = ALLOC_MODES[a.alloc]
     arena_ptr, mapped_chunk = engine.device_alloc_placed(arena_n * BLOCK, mode, chunk)
     cs = torch.empty(n_gpu, dtype=torch.int64, device=dev)
@@ -1107,7 +1107,7 @@ def block_checksum_workload(a) -> int:
                                            "traffic_over_algorithmic", "placement_spread")}
 
     # The frac depends on where the arena lands in HBM (0.85-0.89 across fresh processes;
-    # neither VMM placement collapses the spread): report this line's frac
+    # neither VMM placement collapses the spread, DESIGN_LOG.md §10.1): report this line's frac
     # beside the committed session's placement spread, the spread widened to include it.
     placement = None
     if prof and prof.get("placement_spread"):
@@ -1122,7 +1122,7 @@ def block_checksum_workload(a) -> int:
 
     # also report against a measured stream-read peak. Measured here, after
     # the timed region, on the same arena: the rate depends on where the arena lands in
-    # HBM, so a peak from another process or box would not compare.
+    # HBM (DESIGN_LOG.md §5), so a peak from another process or box would not compare.
     read_peak = measured_read_peak(arena_ptr, arena_n, stream, achieved)
 
     gather = ""

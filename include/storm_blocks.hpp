@@ -11,7 +11,7 @@
 //
 // Single calls (Checksum, BlockChecksum, VerifyChecksum) hash on the calling thread
 // through stormck_xxh64, the library's single-call leg: one buffer is four serial
-// XXH64 chains, which one host core walks faster than the GPU, and like
+// XXH64 chains, which one host core walks faster than the GPU (DESIGN_LOG.md §5), and like
 // Go's Checksum it cannot fail. Batches run on the gfx950 device, or on the library's
 // host leg when its cost model predicts the PCIe link makes the device slower for a
 // host-memory batch; they need a device either way, and a failure throws

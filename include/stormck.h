@@ -24,7 +24,7 @@
  * never a substitute for a missing device:
  *  - the latency leg of a SINGLE call (stormck_xxh64 / stormck_checksum): one buffer is
  *    four serial XXH64 chains, which one host core walks faster than the GPU at every
- *    length (DESIGN.md §4), so single calls stay on the host by design (SURVEY.md §8b);
+ *    length (DESIGN.md §4.3), so single calls stay on the host by design (SURVEY.md §8b);
  *  - the host legs of data that lives in HOST memory (stormck_commit_host,
  *    stormck_checksum_host_leg), which the routed entry points (stormck_commit,
  *    stormck_checksum_batch) run alone, or beside the devices (the split leg), when the
@@ -185,7 +185,7 @@ int stormck_verify_host_leg(const void* base, uint64_t stride, const uint32_t* l
  * stormck_xxh64: XXH64 seed 0 of p[0..n_bytes) on the calling host thread; cannot
  * fail (p may be NULL only when n_bytes == 0). What the Go shim's Checksum calls.
  * stormck_checksum: the single-call dispatch. Below the measured host/device crossover
- * (never reached: the device single call is slower at every length) it
+ * (never reached: the device single call is slower at every length, DESIGN_LOG.md §5) it
  * is stormck_xxh64; any length, no device needed.
  * stormck_checksum_gpu: the same hash through the device: one k_xxh64_single launch
  * for slices up to 64 KiB, the host pipeline with a batch of one up to 256 MiB;
@@ -314,7 +314,7 @@ int stormck_commit_device(void* d_arena, stormck_dirty_block* blocks, uint64_t n
  * (storm's cache.data) and the blocks of one height hashed on `threads` library pool
  * threads (0 = all of the pool, at most 16; 1 = storm's serial loop). Needs no device:
  * it is the leg stormck_commit picks for forests too small to repay a launch per height
- * and the link. */
+ * and the link (DESIGN_LOG.md §11 f1). */
 int stormck_commit_host(void* arena, stormck_dirty_block* blocks, uint64_t n, uint64_t revision,
                         uint64_t* last_allocated_block, uint64_t* out_checksums, uint32_t threads);
 /* Cache.Commit's data phase as storm's cache calls it (the Go binding's CommitBatch):

@@ -9,13 +9,17 @@
 // identical to blocks/checksum.go:10-27. Those single calls (one block, from
 // cache/trace.go:282,307, cache/cache.go:73,160, persistence/init.go:44) take the
 // library's host leg, stormck_xxh64: one buffer is four serial XXH64 chains, which
-// one core walks faster than a GPU launch (DESIGN.md §5), so unchanged callers pay
+// one core walks faster than a GPU launch (DESIGN_LOG.md §5), so unchanged callers pay
 // what xxhash.Sum64 costs them today, and like Sum64 the call cannot fail.
 // ChecksumBatch / VerifyChecksumBatch / ReadVerifyBatch / CommitBatch are additions
-// for batched callers (level-synchronous commit, batched cold-read verify): those
-// run on the MI355X (gfx950), except that a batch or commit in host memory takes the
-// library's host leg when its measured cost model predicts that the PCIe link would
-// make the GPU slower (ChecksumBatch, CommitBatch).
+// for batched callers (level-synchronous commit, batched cold-read verify). A batch or
+// commit in host memory (storm's cache.data) runs on the leg the library's cost model
+// predicts is fastest: the MI355X (gfx950) over PCIe, the library's host threads, or both
+// at once on one call (the split leg, for the registered cache.data): the host threads
+// take blocks from the front and the GPUs from the back (ChecksumBatch, CommitBatch).
+// Without a gfx950 device these calls return the library's error (STORMCK_ENODEV), even
+// where the host leg would have been chosen: a stormck build needs its GPU
+// (INTEGRATION.md §2).
 //
 // Not compiled in this repository (no Go toolchain in the build image); the C
 // side it binds is exercised by tests/test_abi.py and tests/test_cpp_mirror.py.
@@ -75,14 +79,14 @@ func VerifyChecksum(address BlockAddress, p []byte, expectedChecksum Hash) error
 
 // BatchHostThreads is the number of host threads the host leg of ChecksumBatch and
 // VerifyChecksumBatch may use (0 = the library's pool, up to 16). It also steers the leg
-// choice: with fewer host threads the device leg wins sooner (DESIGN.md §5, "Host-memory
-// batches, routed").
+// choice: with fewer host threads the device and split legs win sooner (DESIGN.md §4.2).
 var BatchHostThreads uint32
 
 // ChecksumBatch computes checksums of n blocks at data[i*stride:], length bytes each.
 // The blocks live in host memory, so libstormck routes the batch (stormck_checksum_batch)
-// to whichever leg its measured cost model predicts is faster: the GPU, through the PCIe
-// link (ChecksumBatchGPU), or its host leg on BatchHostThreads threads. Both are bit-exact.
+// to whichever leg its measured cost model predicts is fastest: the GPU, through the PCIe
+// link (ChecksumBatchGPU), its host leg on BatchHostThreads threads, or, when data is
+// registered (RegisterHostMemory) or otherwise page-locked, both at once. All are bit-exact.
 func ChecksumBatch(data []byte, n, stride, length int, out []Hash) error {
 	if n == 0 {
 		return nil
@@ -238,7 +242,7 @@ var _ = [1]struct{}{}[unsafe.Sizeof(DirtyBlock{})-56]
 
 // CommitHostThreads is the number of host threads CommitBatch's host leg may use (0 = the
 // library's pool, up to 16). It also steers the leg choice: with fewer host threads the
-// device leg wins sooner (DESIGN.md §11 f1, "End to end from host memory").
+// device leg wins sooner (DESIGN_LOG.md §11 f1, "End to end from host memory").
 var CommitHostThreads uint32
 
 // CommitBatch runs Cache.Commit's data phase (cache/cache.go:87-137, trace.go:274-320)
@@ -250,7 +254,7 @@ var CommitHostThreads uint32
 // over CommitHostThreads threads when there is enough to hash). Either leg stores each
 // {checksum, address, birth revision} and type into the parent's origin in the arena.
 // Relocations are written back into dirty; out[i] is dirty[i]'s checksum; leg reports
-// the leg taken (LegHost / LegDevice).
+// the leg taken (LegHost / LegDevice / LegSplit).
 func CommitBatch(arena []byte, dirty []DirtyBlock, revision uint64, lastAllocated *BlockAddress, out []Hash) (leg uint32, err error) {
 	if len(dirty) == 0 {
 		return LegNone, nil
@@ -275,7 +279,23 @@ const (
 	LegNone   = uint32(C.STORMCK_LEG_NONE)
 	LegHost   = uint32(C.STORMCK_LEG_HOST)
 	LegDevice = uint32(C.STORMCK_LEG_DEVICE)
+	LegSplit  = uint32(C.STORMCK_LEG_SPLIT)
 )
+
+// SetBatchDevices lists the GPUs the routed calls (ChecksumBatch, VerifyChecksumBatch,
+// CommitBatch) may use; each brings its own PCIe link to a split. nil: the calling
+// thread's current device (the default). storm is one process, so this is how one commit
+// uses every GPU of a node (stormck_route_devices).
+func SetBatchDevices(devices []int32) error {
+	var p *C.int
+	if len(devices) > 0 {
+		p = (*C.int)(unsafe.Pointer(&devices[0]))
+	}
+	if rc := C.stormck_route_devices(p, C.int(len(devices))); rc != C.STORMCK_OK {
+		return stormckError(rc)
+	}
+	return nil
+}
 
 // UnregisterHostMemory undoes RegisterHostMemory.
 func UnregisterHostMemory(b []byte) error {

@@ -12,7 +12,7 @@ package cache
 // picks: the GPU (one launch per height, reading cache.data in place over PCIe: it is
 // registered host memory, newArena) or the library's host leg (storm's own loop, each
 // height spread over host threads). For storm's per-revision commits the host leg wins
-// on the measured box (DESIGN.md §11 f1, "End to end from host memory"), so the stormck
+// on the measured box (DESIGN_LOG.md §11 f1, "End to end from host memory"), so the stormck
 // build is never slower than storm's loop. The host then finishes what storm's loop
 // leaves behind. The same steps, in the same order, are mirrored in Python by
 // storm_amd/commit.py commit_cache and checked there against a restatement of storm's

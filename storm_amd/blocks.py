@@ -15,11 +15,12 @@ plus the batch entry points the GPU path exists for (``ChecksumBatch``,
 ``VerifyChecksumBatch``, ``ReadVerifyBatch``; f1's batched commit is in
 ``storm_amd.commit``). Batches fail loudly without a device. A batch in host memory
 is routed by the library's measured cost model, as the commit is: the gfx950 kernels
-over PCIe (``ChecksumBatchGPU``) or host threads (``ChecksumBatchHost``), whichever is
-faster for it. A single ``Checksum`` is one buffer, four serial XXH64
+over PCIe (``ChecksumBatchGPU``), host threads (``ChecksumBatchHost``), or both at once on
+pinned or registered memory (``ChecksumBatchSplit``), whichever it predicts is fastest
+(DESIGN.md §4.2). A single ``Checksum`` is one buffer, four serial XXH64
 chains: libstormck hashes it on the calling host thread (stormck_checksum, the
 latency leg SURVEY.md §8b specifies; measured faster than the device single call at
-every length). ``ChecksumGPU`` is the same call through the device
+every length, DESIGN_LOG.md §5). ``ChecksumGPU`` is the same call through the device
 (k_xxh64_single), for tests and A/B.
 """
 from __future__ import annotations
@@ -145,7 +146,7 @@ def _expected_arg(n: int, expected) -> np.ndarray:
 def ChecksumBatchLeg(buf, n: int, stride: int, length: Optional[int] = None,
                      lens: Optional[Sequence[int]] = None, host_threads: int = 0) -> Tuple[np.ndarray, int]:
     """ChecksumBatch, also returning the leg the library took (_lib.LEG_HOST /
-    LEG_DEVICE; LEG_NONE for an empty batch)."""
+    LEG_DEVICE / LEG_SPLIT; LEG_NONE for an empty batch)."""
     a, la, ln, lp = _batch_args(buf, n, stride, length, lens)
     out = np.zeros(n, dtype=np.uint64)
     leg = ctypes.c_uint32(_lib.LEG_NONE)
@@ -161,9 +162,9 @@ def ChecksumBatch(buf, n: int, stride: int, length: Optional[int] = None,
                   host_threads: int = 0) -> np.ndarray:
     """Checksums of ``n`` host blocks at ``buf + i*stride`` (``length`` bytes each or
     ``lens[i]``). Returns uint64[n]. The library routes the batch (stormck_checksum_batch):
-    the device leg over PCIe (ChecksumBatchGPU) or the host leg on ``host_threads``
-    threads (ChecksumBatchHost; 0 = the library pool), whichever its measured cost model
-    predicts is faster. ``devices``: hash on these devices in contiguous ranges, one host
+    the device leg over PCIe (ChecksumBatchGPU), the host leg on ``host_threads`` threads
+    (ChecksumBatchHost; 0 = the library pool) or, for pinned or registered memory, both at
+    once (ChecksumBatchSplit), whichever its measured cost model predicts is fastest. ``devices``: hash on these devices in contiguous ranges, one host
     thread each (stormck_checksum_host_multi) instead of routing."""
     if devices is not None:
         return ChecksumBatchGPU(buf, n, stride, length, lens, devices)
@@ -374,7 +375,7 @@ def RegisterHostMemory(buf) -> None:
     """Page-lock a long-lived host buffer (storm's cache.data, allocated once in
     cache.New, cache/cache.go:36-40): host batches then DMA straight from it, and
     HostDevicePointer gives kernels in-place access to it. Kernels reading it in place
-    run at the PCIe link rate only from 256-byte aligned rows; a
+    run at the PCIe link rate only from 256-byte aligned rows (DESIGN_LOG.md §5); a
     misaligned buffer works, more slowly, and draws a warning."""
     a = _as_u8(buf)
     if a.ctypes.data % 256:

@@ -18,7 +18,7 @@
 //   * k_commit_level*: f1 commit levels; k_pointer_level / _node: Merkle nodes
 //   * k_key_tags*    : f4, one lane per short key
 // (A lane-per-block mapping was measured and rejected: 0.59-0.66 of HBM peak,
-// profiles/r01_probe*.txt; DESIGN.md §4. Its kernel left the library in round 2.)
+// profiles/r01_probe*.txt; DESIGN_LOG.md §4. Its kernel left the library in round 2.)
 // The per-block sizes (stride / explicit offsets) and lengths (uniform / per-block)
 // cover storm's block types: 72, 28808, 30000, 31808, 32768 bytes.
 #pragma once
@@ -32,7 +32,7 @@ typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
 #ifdef STORMCK_DEBUG_QUAD
 // Debug build (tools/libstormck_debug.so): quad merges that ran with part of their quad
 // inactive. update_dpp with bound_ctrl = false returns `old` (0) for a source lane that
-// is not in exec, so such a merge silently reads zeros ("Quad merges").
+// is not in exec, so such a merge silently reads zeros (DESIGN_LOG.md §4, "Quad merges").
 __device__ unsigned long long g_partial_quads;
 #endif
 
@@ -2038,7 +2038,7 @@ __device__ __forceinline__ void pointer_level_pc_body(const uint64_t* __restrict
 }
 
 // Role of a wave in a workgroup of 2C waves: chain waves must not share a SIMD with each
-// other, since a chain is bounded by its wave's VALU issue ("Merkle tree
+// other, since a chain is bounded by its wave's VALU issue (DESIGN_LOG.md §5, "Merkle tree
 // per step"). With SIMD roles, every wave reads the SIMD it was placed on (HW_ID bits
 // 5:4) and takes a rank among the workgroup's waves on that SIMD; the waves are then
 // ordered by (rank, SIMD) and the first C of that order are the chain waves. So the

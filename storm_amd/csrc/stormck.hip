@@ -386,7 +386,7 @@ uint32_t debug_stall(hipStream_t st) {
 
 // Ring depth of the pipelined staging in the wide-multi kernels (kernels.h
 // multi_stage_hash_pipe): kRingSlots; probe knob STORMCK_STAGE_PIPE=0 stages whole blocks
-// first (A/B). 6- and 7-slot rings were measured slower.
+// first (A/B). 6- and 7-slot rings were measured slower (DESIGN_LOG.md §5).
 uint32_t pipe_staging() {
     static const uint32_t slots = [] {
         const char* e = STORMCK_KNOB("STORMCK_STAGE_PIPE");
@@ -452,7 +452,7 @@ int workspace_pool(hipMemPool_t* out) {
 // and short blocks leave most of a step's rows empty (storm's `-tags test` sizes 256 / 536
 // / 728 B: 3.7 against 6.4 G blocks/s strided, 2.8 against 6.2 shuffled, 1M blocks).
 // One length L per batch, strided, var / quad in G blocks/s: 1 KiB 4.29 / 5.73, 2 KiB
-// 2.82 / 2.99, 4 KiB 1.56 / 1.59, 8 KiB 0.85 / 0.76, 16 KiB 0.41 / 0.37 (DESIGN.md §5
+// 2.82 / 2.99, 4 KiB 1.56 / 1.59, 8 KiB 0.85 / 0.76, 16 KiB 0.41 / 0.37 (DESIGN_LOG.md §5
 // "Short blocks", profiles/r04_small_blocks/, r04_small_crossover/).
 constexpr uint64_t kVarMinLen = 4096;
 uint64_t var_min_len() {  // probe knob STORMCK_VAR_MIN_LEN: another threshold (A/B)
@@ -475,7 +475,7 @@ bool order_on() {
 }
 
 // Probe knob STORMCK_GATHER_RANK=1: large gathers with per-block lengths deal each group's
-// rows by length rank (k_order_rank; measured slower).
+// rows by length rank (k_order_rank; measured slower, DESIGN_LOG.md §10).
 [[maybe_unused]] bool rank_on() {
     static const bool on = [] {
         const char* e = STORMCK_KNOB("STORMCK_GATHER_RANK");
@@ -1672,7 +1672,7 @@ int stormck_checksum(const void* p, uint64_t n_bytes, uint64_t* out) {
     // Latency dispatch of a single call. One buffer is four serial chains, so the GPU
     // brings no parallelism to it: measured on MI355X, the device single call
     // (stormck_checksum_gpu) is slower than one host core at every length, 72 B to
-    // 256 MiB ("Single calls"). The crossover is therefore "never";
+    // 256 MiB (DESIGN_LOG.md §5, "Single calls"). The crossover is therefore "never";
     // STORMCK_SINGLE_GPU_MIN=<bytes> sends single calls of at least that many bytes to
     // the device (A/B measurement only).
     static const uint64_t gpu_min = [] {
@@ -1756,7 +1756,7 @@ int stormck_pointer_level_device(const uint64_t* d_child_cs, uint64_t m, uint64_
     // probe knob STORMCK_POINTER_RING: "0" = the register-quad kernel; default: the
     // producer / chain wave pair (k_pointer_level_pc). Measured alternatives (one wave
     // producing and hashing, 30- and 45-stripe tiles, prefetch 4 and 12 tiles, two pairs
-    // per workgroup, one producer for two chain waves): DESIGN.md §5, profiles/r02_merkle/.
+    // per workgroup, one producer for two chain waves): DESIGN_LOG.md §5, profiles/r02_merkle/.
     static const int ring_mode = [] {
         const char* e = STORMCK_KNOB("STORMCK_POINTER_RING");
         return e ? std::atoi(e) : 2;
@@ -1924,7 +1924,7 @@ int stormck_read_verify_fd(int fd, const uint64_t* addresses, const uint32_t* le
     // read with one pread of up to kRunBytes. An O_DIRECT descriptor reaches the device,
     // whose rate needs queue depth: 32 reader threads instead of 16 (STORMCK_READ_THREADS
     // overrides; on the test boxes' overlay filesystem, counts from 8 to 64 measured the
-    // same within its run-to-run noise).
+    // same within its run-to-run noise, DESIGN_LOG.md §11 f2/f3).
     constexpr uint64_t kRunBytes = 1ULL << 20;
     const uint64_t max_run = full && dst_stride == block_size ? std::max<uint64_t>(1, kRunBytes / block_size) : 1;
     unsigned nt = direct ? 32u : std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
@@ -2532,7 +2532,7 @@ int stormck_commit_device(void* d_arena, stormck_dirty_block* blocks, uint64_t n
 //           that the device finishes when everyone else does (SplitQueue), until they meet.
 // One engine runs the host and split legs (split_run; the host leg is a split without
 // devices). The routed entry points take the leg with the smallest predicted time, from
-// rates that start at priors measured on MI355X (DESIGN.md §4) and that every call large
+// rates that start at priors measured on MI355X (DESIGN.md §4.2) and that every call large
 // enough to time measures again (RouteModel).
 namespace {
 

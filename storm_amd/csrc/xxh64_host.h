@@ -4,7 +4,7 @@
 // reads (cache/trace.go:282,307, cache/cache.go:73,160, persistence/init.go:44). One
 // XXH64 is four serial accumulator chains, so one buffer can use at most 4 GPU lanes:
 // a single call costs a launch, a sync and a ~1.3 GB/s chain on the device (35 us for
-// 32 KiB), against ~1.3 us on one host core. Single calls therefore hash
+// 32 KiB, DESIGN_LOG.md §5), against ~1.3 us on one host core. Single calls therefore hash
 // here ("single calls stay on the C++ CPU path"); every batch, where
 // the blocks are independent, goes to the gfx950 kernels. This is not a fallback for a
 // missing device: batched entry points still fail with STORMCK_ENODEV without one.

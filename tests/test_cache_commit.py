@@ -117,7 +117,7 @@ def test_open_trace_is_refused_before_anything_changes():
 
 def _host_leg_run(c, threads):
     """storm's cache.data committed where it lives by the library's host leg (the leg the
-    routed CommitBatch takes for storm's per-revision commits)."""
+    routed CommitBatch takes for storm's per-revision commits, DESIGN_LOG §11 f1)."""
     def run(recs, rev, last):
         return cm.commit_host(c.data, recs, rev, last, threads=threads)
     return run

@@ -225,7 +225,7 @@ def test_storm_patch_applies_to_the_reference(tmp_path):
 
 def test_commit_batch_takes_the_routed_commit():
     """CommitBatch hands storm's registered cache.data (a host pointer) to stormck_commit,
-    which picks the device or host leg by the measured crossover; it no
+    which picks the device or host leg by the measured crossover (DESIGN_LOG §11 f1); it no
     longer calls stormck_commit_device directly. The host-thread knob and the leg
     constants are exported."""
     text = open(SHIM).read()
@@ -250,7 +250,7 @@ def _go_func(text, name):
 def test_batches_take_the_routed_batch():
     """ChecksumBatch / VerifyChecksumBatch hand host blocks to stormck_checksum_batch /
     stormck_verify_batch, which pick the device or host leg by the measured cost model
-    ("Host-memory batches, routed"); ChecksumBatchGPU keeps the device leg alone
+    (DESIGN_LOG §5, "Host-memory batches, routed"); ChecksumBatchGPU keeps the device leg alone
     and ChecksumBatchDevices the multi-GPU one. The host-thread knob is exported."""
     text = open(SHIM).read()
     cb = _go_func(text, "ChecksumBatch")

@@ -4,8 +4,9 @@ ChecksumBatch / VerifyChecksumBatch call.
 
 A batch in host memory crosses PCIe on the device leg (~52 GiB/s end to end), while
 host threads hash the same bytes four blocks at a time; the routed entry takes the leg
-the library's cost model predicts is faster ("Host-memory batches,
-routed"), as stormck_commit does for a commit (/root/reference/cache/cache.go:87-137).
+the library's cost model predicts is fastest (the split leg, both at
+once, has its own tests in tests/test_split_gpu.py), as stormck_commit does for a commit
+(/root/reference/cache/cache.go:87-137).
 
 CPU: the host leg against the C oracle (blocks.Checksum = XXH64 seed 0,
 /root/reference/blocks/checksum.go:15-17) on uniform, per-block, short, tail and

@@ -3,7 +3,7 @@
 Every kernel merges a block's four XXH64 accumulators across the lanes of its quad with
 DPP (kernels.h quad_bcast: update_dpp, bound_ctrl = false, old = 0). A source lane that
 is not in exec then reads as 0: the checksum is silently wrong. A round-3 variant hit
-exactly this ("Quad merges"). The debug build (tools/libstormck_debug.so,
+exactly this (DESIGN_LOG.md §4, "Quad merges"). The debug build (tools/libstormck_debug.so,
 -DSTORMCK_DEBUG_QUAD) counts every merge made with a partially active quad. This test
 runs every kernel family of the shipped dispatch through that build in a child process,
 checks each result against the oracle, and requires the count to be zero. Its self-test

@@ -2,7 +2,7 @@
 
 The reference tests its checksum path through the layers that call it:
 cache/cache_test.go, persistence/store_test.go and persistence/init_test.go. Those
-layers (the cache, the store, memdev) are out of scope here. What they
+layers (the cache, the store, memdev) are out of scope here (DESIGN_LOG.md §0). What they
 assert about checksums is in scope. Each test below follows one reference test. It
 keeps that test's block contents and its checksum checks, and runs them through this
 library's boundary:

@@ -7,7 +7,7 @@ phase drives, /root/reference/cache/cache.go:87-137) run on the host threads, th
 device(s) over PCIe, or both at once (the split leg). stormck_route_plan_batch /
 _plan_commit expose the decision without a device, so these tests inject rates and check
 the choice and the predicted times against the model's formulas (include/stormck.h,
-"routing of host-memory work"; DESIGN.md §4). The learning tests run the host leg itself,
+"routing of host-memory work"; DESIGN.md §4.2). The learning tests run the host leg itself,
 which needs no device, and watch the rates move.
 """
 import math

@@ -1,6 +1,6 @@
 // Does the shipped streaming kernel's rate depend on WHERE its arena lands in HBM?
 // Bench runs in separate processes differ by ~2% while every process is steady
-// (DESIGN.md §5). One process: several 128 GiB arenas from hipMalloc and
+// (DESIGN_LOG.md §5). One process: several 128 GiB arenas from hipMalloc and
 // hipExtMallocWithFlags(hipDeviceMallocContiguous), each filled and timed.
 // Times the shipped large-batch kernel (k_xxh64_glds_skew, 256 workgroups).
 // Usage: alloc_probe [GiB=128] [reps=5]

@@ -4,7 +4,7 @@
 // Variants of k_xxh64_quad's register-quad mapping: the shipped 2-group pipeline
 // ("classic"), D register groups in flight (k_deep), and two bound finders: synthetic
 // words with no loads (VALU floor) and loads with no hash (load floor). All checked
-// bit-exact against a host XXH64 (bound finders excepted). DESIGN.md §5 has results.
+// bit-exact against a host XXH64 (bound finders excepted). DESIGN_LOG.md §5 has results.
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -o tools/chain_probe tools/chain_probe.hip
 #include <hip/hip_runtime.h>
 
@@ -50,7 +50,7 @@ static uint64_t host_xxh64(const uint8_t* p, uint64_t n) {
     return h;
 }
 
-// ---- the stripe chain in folded form (measured, not adopted: DESIGN.md §4) -------
+// ---- the stripe chain in folded form (measured, not adopted: DESIGN_LOG.md §4) -------
 // round(acc, w) = rotl31(acc + w*P2) * P1 puts acc through both multiplies: the
 // compiler folds acc into the w*P2 v_mad_u64_u32, so each round's dependent path is
 // mad -> add3 -> alignbit -> mad -> add3. Carrying x = acc + w*P2 instead (the value

@@ -1,5 +1,5 @@
 // What clock does the shader run at while the c3 kernel streams, and does rocprofv3
-// change it? (the process under `rocprofv3 --kernel-trace` times the
+// change it? (DESIGN_LOG.md §5: the process under `rocprofv3 --kernel-trace` times the
 // shipped kernel 2-5 % slower than the plain bench, and there the hash falls below
 // its own hash-free control.)
 //

@@ -1,6 +1,6 @@
 """Rate drift within one process: one 128 GiB arena, the bench's hash launch timed in
 blocks of 4 launches, with and without idle gaps between blocks (bench variance study,
-DESIGN.md §5). Usage: python tools/drift.py [rounds]"""
+DESIGN_LOG.md §5). Usage: python tools/drift.py [rounds]"""
 import os
 import sys
 import time

@@ -1,7 +1,7 @@
 // Host -> HBM gather of scattered 32 KiB blocks (storm's dirty slots of a registered
 // cache.data): one hipMemcpyBatchAsync of many 32 KiB copies vs per-block
 // hipMemcpyAsync vs one contiguous DMA vs a kernel reading the host pages in place.
-// Decides whether f1 on a host arena should stage blocks in HBM.
+// Decides whether f1 on a host arena should stage blocks in HBM (DESIGN_LOG.md §5).
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -o tools/gather_probe tools/gather_probe.hip
 #include <hip/hip_runtime.h>
 #include <stdio.h>

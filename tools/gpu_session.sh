@@ -13,8 +13,10 @@
 #   bench                  the default bench line (c3, BASELINE metric)
 #   batch_e2e commit_e2e gather c5 commit keytags
 #                          bench.py --workload <step> --steps 7
-#   prof                   rocprofv3 --kernel-trace --stats of a 5-step c3 bench
-#   pmc                    FETCH_SIZE / WRITE_SIZE of the c3 kernel (separate passes)
+#   prof                   tools/profile.sh <tag>: fresh plain c3 processes, the bench under
+#                          rocprofv3 --kernel-trace --stats, separate FETCH_SIZE / WRITE_SIZE
+#                          passes and their calibration, the gather workload likewise
+#                          (then, in the build container: python tools/collect_profile.py <tag>)
 set -o pipefail
 tag=${1:?usage: gpu_session.sh <tag> <step>...}
 shift
@@ -43,15 +45,8 @@ for step in "$@"; do
             timeout -k 10 900 python bench.py --workload "$step" --steps 7 > "$out/$step.log" 2>&1; rc=$?
             tail -c 300 "$out/$step.log"; echo ;;
         prof)
-            timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$out/prof" -o run -- \
-                python3 bench.py --steps 5 --no-cpu > "$out/prof.log" 2>&1; rc=$?
-            tail -c 300 "$out/prof.log"; echo ;;
-        pmc)
-            rc=0
-            for c in FETCH_SIZE WRITE_SIZE; do
-                timeout -s KILL 300 rocprofv3 --pmc "$c" -d "$out/pmc_$c" -o run -- \
-                    python3 bench.py --steps 2 --warmup 1 --settle 0 --no-cpu > "$out/pmc_$c.log" 2>&1 || { rc=$?; break; }
-            done ;;
+            timeout -k 10 1100 bash tools/profile.sh "$tag" > "$out/prof.log" 2>&1; rc=$?
+            tail -3 "$out/prof.log" ;;
         *)
             echo "unknown step $step"; rc=2 ;;
     esac

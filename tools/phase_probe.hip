@@ -1,6 +1,6 @@
 // Does skewing the intra-block offsets that are read at the same moment make the
 // streaming kernel faster, or less dependent on where its arena lands in HBM?
-// (the shipped kernel's rate follows the arena's physical placement,
+// (DESIGN_LOG.md §5: the shipped kernel's rate follows the arena's physical placement,
 // 0.86-0.89 of peak, because every workgroup reads the same 512-byte offset of its
 // 128 blocks at once and XXH64 fixes each block's stripe order.)
 //

@@ -20,7 +20,7 @@
 
 using namespace stormck;
 
-// Rejected alternative kept for the design comparison: one lane per
+// Rejected alternative kept for the design comparison (DESIGN_LOG.md §4): one lane per
 // block, all four accumulators in the lane, dwordx4 loads of whole stripes.
 namespace stormck {
 // ---------------------------------------------------------------------------
@@ -31,7 +31,7 @@ namespace stormck {
 namespace stormck {
 // ---------------------------------------------------------------------------
 // REJECTED (profiles/r01_probe_persist.txt: 0.884-0.886 vs 0.886 for the one-group-per-
-// workgroup kernel). Persistent form of k_xxh64_glds (R = 2, barrier-synchronised ring): one workgroup per
+// workgroup kernel; DESIGN_LOG.md §4). Persistent form of k_xxh64_glds (R = 2, barrier-synchronised ring): one workgroup per
 // CU walks groups g = blockIdx.x, + gridDim.x, ... of 16*WAVES blocks, and the tile
 // stream runs on across group boundaries, so the first tile of the next group is in
 // flight while the current group's last tile hashes and its blocks finish. The
@@ -140,7 +140,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_xxh64_glds_p(const uint8_t* __re
 }  // namespace stormck
 
 namespace stormck {
-// REJECTED, the north star's literal mapping: ONE WAVEFRONT PER BLOCK.
+// REJECTED, the north star's literal mapping (DESIGN_LOG.md §4): ONE WAVEFRONT PER BLOCK.
 // The wave streams its block through a private 2 x 2 KiB LDS ring with coalesced
 // LDS-DMA (64 lanes x 16 B per instruction), and quad 0 hashes each tile (XXH64's four
 // serial accumulators leave no work for the other 60 lanes). Requires len % 2048 == 0.

@@ -2,7 +2,7 @@
 // shipped large-batch kernel's data movement (k_xxh64_glds_skew, LDS-DMA ring, waves
 // 4 KiB apart) with the XXH64 arithmetic replaced by xor, launched on the bench's own
 // arena, so the kernel's fraction of it is measured on the same HBM placement
-// (the rate depends on where the arena lands).
+// (DESIGN_LOG.md §5: the rate depends on where the arena lands).
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -o tools/libreadpeak.so tools/readpeak.hip
 #include <hip/hip_runtime.h>
 

@@ -1,6 +1,6 @@
 // Cycles per XXH64 round for one wave, operands in registers (no memory), timed
 // in-kernel with s_memtime. Which form of the round sets the latency floor of a
-// one-block-per-quad chain (small batches)?
+// one-block-per-quad chain (small batches, DESIGN_LOG.md §4)?
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -o tools/round_probe tools/round_probe.hip
 #include <hip/hip_runtime.h>
 
