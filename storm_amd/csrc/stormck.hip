@@ -19,6 +19,7 @@
 
 #include <fcntl.h>
 #include <pthread.h>
+#include <sys/uio.h>
 #include <unistd.h>
 
 #include <cerrno>
@@ -1065,15 +1066,22 @@ void release_ctx(DeviceCtx* c) {
     (void)hipSetDevice(prev);
 }
 
-// Whether this process can read the first and the last byte of [p, p + bytes): a write of
-// each byte into a pipe fails with EFAULT instead of faulting when the address is not
-// readable (e.g. a device address the CPU mapping leaves inaccessible).
+// Whether this process can read the first and the last byte of [p, p + bytes) (e.g. not a
+// device address the CPU mapping leaves inaccessible), without faulting: one
+// process_vm_readv of the two bytes from this process itself (EFAULT when either is not
+// readable), or, where that syscall is not permitted, a write of each byte into a pipe.
 bool host_readable(const void* p, uint64_t bytes) {
-    static std::mutex mu;
+    const uint8_t* b = static_cast<const uint8_t*>(p);
+    uint8_t got[2];
+    iovec local = {got, 2};
+    iovec remote[2] = {{const_cast<uint8_t*>(b), 1}, {const_cast<uint8_t*>(b + (bytes ? bytes - 1 : 0)), 1}};
+    const ssize_t r = process_vm_readv(getpid(), &local, 1, remote, 2, 0);
+    if (r == 2) return true;
+    if (r >= 0 || errno == EFAULT) return false;
+    static std::mutex mu;  // the syscall is filtered here (seccomp): the pipe
     static int fds[2] = {-1, -1};
     std::lock_guard<std::mutex> g(mu);
     if (fds[0] < 0 && pipe2(fds, O_NONBLOCK | O_CLOEXEC) != 0) return true;  // cannot tell: as before
-    const uint8_t* b = static_cast<const uint8_t*>(p);
     for (const uint8_t* q : {b, b + (bytes ? bytes - 1 : 0)}) {
         if (write(fds[1], q, 1) != 1) return errno != EFAULT;
         uint8_t sink = 0;
@@ -2549,6 +2557,7 @@ constexpr double kSplitChunkUs = 8.0;             // a chunk issued behind one i
 constexpr double kSplitMinClaimBytes = 1 << 20;   // a smaller device claim costs about what it saves
 constexpr double kSplitDmaBytes = 32 << 20;       // strided claims from this size take the copy engine
 constexpr double kSplitGain = 0.95;               // the split is taken only when predicted 5% faster
+constexpr double kHostOnlyUs = 10.0;              // calls one host thread finishes this fast are not planned
 
 // Priors, bytes/us: the rates measured on an MI355X box with its EPYC 9575F host
 // (profiles/r04_batch_e2e/, r04_commit_e2e/).
@@ -3435,11 +3444,13 @@ Blocks batch_blocks(const void* base, uint64_t stride, const uint32_t* lens, uin
 }
 
 // The host leg of a batch on `threads` pool threads (0 = the pool): no device involved.
+// checked: the caller has already classified `base` (the routed call).
 int batch_host_leg(const void* base, uint64_t stride, const uint32_t* lens, uint32_t len, uint64_t n, uint64_t* out,
-                   const uint64_t* expected, uint64_t* first_bad, uint64_t* n_bad, uint32_t threads) {
+                   const uint64_t* expected, uint64_t* first_bad, uint64_t* n_bad, uint32_t threads,
+                   bool checked = false) {
     BatchShape s;
     if (!batch_shape(stride, lens, len, n, &s)) return fail(STORMCK_EINVAL, "stride smaller than a block length (blocks overlap)");
-    if (!host_readable(base, (n - 1) * stride + (lens ? lens[n - 1] : len)))
+    if (!checked && !host_readable(base, (n - 1) * stride + (lens ? lens[n - 1] : len)))
         return fail(STORMCK_EINVAL, "base is not readable host memory");
     ForkJoin& fj = ForkJoin::get();
     const unsigned nt = threads ? std::min<unsigned>(threads, fj.size()) : fj.size();
@@ -3494,13 +3505,19 @@ int batch_routed(const void* base, uint64_t stride, const uint32_t* lens, uint32
     }
     const Mem mem = classify(base, (n - 1) * stride + (lens ? lens[n - 1] : len));
     if (mem == Mem::kDevice || mem == Mem::kUnreadable) return not_host_memory(mem);
+    // A batch that one host thread hashes faster than any device can start returning
+    // (its start latency, tens of microseconds) takes the host leg without planning.
+    const stormck_route_rates rt = RouteModel::get().now();
+    if (static_cast<double>(s.bytes) / rt.host_thread < kHostOnlyUs) {
+        if (leg_used) *leg_used = STORMCK_LEG_HOST;
+        return batch_host_leg(base, stride, lens, len, n, out, expected, first_bad, n_bad, 1, true);
+    }
     std::vector<int> devs;
     rc = route_devices(&devs);
     if (rc) return rc;
     // the device pipeline stages whole blocks through 256 MiB chunks
     const uint64_t step = n == 1 ? std::max<uint64_t>(s.longest, 8) : std::max<uint64_t>(stride, 8);
     const bool pinned = mem != Mem::kPageable;
-    const stormck_route_rates rt = RouteModel::get().now();
     auto plan_for = [&](unsigned t) {
         return plan_batch(rt, n, s, pinned, step <= kChunkBytes, t, static_cast<unsigned>(devs.size()));
     };
@@ -3525,7 +3542,7 @@ int batch_routed(const void* base, uint64_t stride, const uint32_t* lens, uint32
     if (p.leg == STORMCK_LEG_SPLIT)
         return batch_split_leg(base, stride, lens, len, n, out, expected, first_bad, n_bad, devs, pl,
                                STORMCK_SPLIT_BALANCED, nullptr, mem == Mem::kMapped);
-    return batch_host_leg(base, stride, lens, len, n, out, expected, first_bad, n_bad, pl);
+    return batch_host_leg(base, stride, lens, len, n, out, expected, first_bad, n_bad, pl, true);
 }
 
 // The explicit split entry points: pinned or registered memory, the listed devices (or the

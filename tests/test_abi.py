@@ -159,6 +159,8 @@ def test_argument_errors_precede_the_device_check():
         ("host-leg batch null out", lambda: L.stormck_checksum_host_leg(1 << 20, 32, None, 32, 4, None, 1)),
         ("host-leg batch overlap", lambda: L.stormck_checksum_host_leg(1 << 20, 16, None, 32, 4,
                                                                        ctypes.addressof(out), 1)),
+        ("host-leg unreadable base", lambda: L.stormck_checksum_host_leg(1 << 20, 64, None, 64, 4,
+                                                                         ctypes.addressof(out), 1)),
         ("host-leg verify null result", lambda: L.stormck_verify_host_leg(1 << 20, 32, None, 32, 4,
                                                                           ctypes.addressof(out), None, None, 1)),
         ("read-verify slot", lambda: L.stormck_read_verify_fd(0, (ctypes.c_uint64 * 1)(0), (ctypes.c_uint32 * 1)(100),
