@@ -3064,7 +3064,7 @@ struct SplitResult {
     uint64_t first_bad = 0, n_bad = 0, device_blocks = 0;
 };
 
-constexpr uint64_t kLatencyProbeBytes = 16ULL << 20;
+constexpr uint64_t kLatencyProbeBytes = 32ULL << 20;
 
 bool trace_on() {
     static const bool on = std::getenv("STORMCK_TRACE") != nullptr;
@@ -3141,6 +3141,7 @@ int split_run(const SplitArgs& A, const std::vector<int>& devs, unsigned pl, uin
     fj.run(parts, work, static_cast<double>(bytes) / (r_host + nd * r_dev));
     const double h_us = now_us() - h0;
     for (DevWorker* w : posted) w->wait();
+    const double t_back = now_us();  // the caller has every device's results
 
     uint64_t fb = bad_first.load(), nb = bad_n.load();
     for (unsigned k = 0; k < nd; ++k) {
@@ -3162,10 +3163,14 @@ int split_run(const SplitArgs& A, const std::vector<int>& devs, unsigned pl, uin
     const double fixed_us = kDevBatchCallUs + static_cast<double>(A.plan_len) / kDevChainBytesPerUs;
     for (const DevRun& r : runs) {
         m.learn_link(A.in_place ? Link::kInplace : Link::kPinned, r.bytes, r.busy_us - fixed_us);
-        // the start latency, from first chunks small enough that their transfer is a
-        // minor, well-estimated part of the time to their return
-        if (r.first_done > 0 && r.first_bytes <= kLatencyProbeBytes)
-            m.learn_latency(r.first_bytes, r_dev, r.first_done - t_post);
+        // the start latency as the call sees it: from posting the device's part until the
+        // caller holds its results (the caller's own wake-up included when the device
+        // finished last), less its bytes over the link; from parts small enough that the
+        // link time is a minor, well-estimated share of that
+        if (r.first_done > 0 && r.bytes <= kLatencyProbeBytes) {
+            const double back = r.finished > h0 + h_us ? t_back : r.finished;
+            m.learn_latency(r.bytes, r_dev, back - t_post);
+        }
     }
     if (trace_on()) {
         const double t_end = now_us();
