@@ -205,7 +205,47 @@ def test_binding_routed_matches_storm_commit_loop():
     c = _workload(seed=11, **PROD)
     legs = []
     b = _binding(c, _routed_run(c, legs))
-    assert legs and all(x in (_lib.LEG_HOST, _lib.LEG_DEVICE) for x in legs), legs
+    assert legs and all(x in (_lib.LEG_HOST, _lib.LEG_DEVICE, _lib.LEG_SPLIT) for x in legs), legs
+    assert a["sing"] == b["sing"]
+    assert a["store"] == b["store"]
+    assert a["metas"] == b["metas"]
+    assert a["data"] == b["data"]
+
+
+def _split_run(c, device_leaves, done):
+    """stormck_commit_split on the registered cache.data: the leaves hashed by the host
+    threads from the front and the device from the back at once (in place), the host
+    threads storing every Pointer into its parent."""
+    from storm_amd import blocks
+
+    def run(recs, rev, last):
+        blocks.RegisterHostMemory(c.data)
+        try:
+            cs, last2, d = cm.commit_split(c.data, recs, rev, last, device_leaves=device_leaves)
+        finally:
+            blocks.UnregisterHostMemory(c.data)
+        done.append(d)
+        return cs, last2
+    return run
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("device_leaves", [None, 7, 10 ** 9])
+def test_binding_split_matches_storm_commit_loop(device_leaves):
+    """The split commit through the binding's steps against the restated storm loop
+    (oracle/storm_cache.py): store, singularity, cache.data and every block's metadata
+    byte for byte, with the devices taking the rates' share, 7 leaves, or every leaf."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    a = _storm(_workload(seed=13, **PROD))
+    c = _workload(seed=13, **PROD)
+    done = []
+    b = _binding(c, _split_run(c, device_leaves, done))
+    assert done
+    if device_leaves == 7:  # at most 7 (a commit with fewer leaves gives them all)
+        assert all(d <= 7 for d in done) and 7 in done, done
+    if device_leaves == 10 ** 9:
+        assert all(d > 0 for d in done), done
     assert a["sing"] == b["sing"]
     assert a["store"] == b["store"]
     assert a["metas"] == b["metas"]
