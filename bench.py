@@ -477,19 +477,18 @@ def commit_e2e_workload(a):
 
         row = {"forest": name, "blocks": int(len(b0)), "leaves": nl, "hashed_bytes": bytes_hashed}
         shares = {}
-        for leg in ("dev_inplace", "dev_hbm", "host_1", "host_all", "split", "split_1", "routed", "routed_1"):
-            n_reps = reps if not (leg == "host_1" and bytes_hashed > (1 << 30)) else 3
-            for _ in range(2):
-                run(leg)
-            ts = []
-            for _ in range(n_reps):
+        names = ("dev_inplace", "dev_hbm", "host_1", "host_all", "split", "split_1", "routed", "routed_1")
+        ts = {leg: [] for leg in names}
+        for r in range(2 + (reps if bytes_hashed < (1 << 30) else 3)):  # 2 warm-up rounds, interleaved legs
+            for leg in names:
                 dt, out = run(leg)
-                ts.append(dt)
-            ts.sort()
-            med = ts[len(ts) // 2]
+                if r >= 2:
+                    ts[leg].append(dt)
+                outs[leg] = out
+        for leg in names:
+            med = sorted(ts[leg])[len(ts[leg]) // 2]
             row[leg + "_us"] = round(med * 1e6, 1)
             row[leg + "_GiBps"] = round(bytes_hashed / med / 2**30, 2)
-            outs[leg] = out
         for k in ("routed_leg", "routed_1_leg"):
             row[k] = _lib.LEG_NAMES.get(outs.get(k), outs.get(k))
         for k, v in shares.items():
@@ -571,12 +570,16 @@ def batch_e2e_workload(a):
     rows = []
     for name, n, lens in shapes:
         stride = BLOCK
+        # the same blocks twice: pageable (the pageable legs) and registered (the rest), so
+        # every leg runs in every round, interleaved (each sees the others' cache effects)
         raw = np.zeros(n * stride + 4096, dtype=np.uint8)
         off = (-raw.ctypes.data) % 4096
-        buf = raw[off:off + n * stride]
+        reg = raw[off:off + n * stride]
         for lo in range(0, n, 16384):  # synthetic blocks, generated on the device in slices
             hi = min(n, lo + 16384)
-            buf[lo * stride:hi * stride] = engine_fill_host(hi - lo, stride)
+            reg[lo * stride:hi * stride] = engine_fill_host(hi - lo, stride)
+        pg = reg.copy()
+        _lib.check(L.stormck_host_register(reg.ctypes.data, reg.nbytes))
         la = lens if isinstance(lens, np.ndarray) else None
         ln = 0 if la is not None else int(lens)
         lp = la.ctypes.data if la is not None else None
@@ -586,6 +589,7 @@ def batch_e2e_workload(a):
         def run(leg):
             out = np.zeros(n, dtype=np.uint64)
             op = out.ctypes.data
+            buf = pg if leg in ("dev", "host_1", "host_all", "routed", "routed_1") else reg
             t0 = time.perf_counter()
             if leg in ("dev", "dev_reg"):
                 rc = L.stormck_checksum_host(buf.ctypes.data, stride, lp, ln, n, op)
@@ -605,7 +609,7 @@ def batch_e2e_workload(a):
                 def half(k):
                     lo = 0 if k == 0 else h
                     used = ctypes.c_uint32(9)
-                    rcs[k] = L.stormck_checksum_batch(buf.ctypes.data + lo * stride, stride,
+                    rcs[k] = L.stormck_checksum_batch(reg.ctypes.data + lo * stride, stride,
                                                       (la[lo:].ctypes.data if la is not None else None), ln,
                                                       (h if k == 0 else n - h), outs2[k].ctypes.data, 0,
                                                       ctypes.byref(used))
@@ -627,24 +631,20 @@ def batch_e2e_workload(a):
 
         row = {"batch": name, "blocks": n, "hashed_bytes": hashed}
         shares = {}
-        for leg in ("dev", "host_1", "host_all", "routed", "routed_1", "dev_reg", "split", "split_1", "routed_reg",
-                    "routed_reg_1", "routed_x2"):
-            if leg == "dev_reg":
-                _lib.check(L.stormck_host_register(buf.ctypes.data, buf.nbytes))
-            if leg == "routed_x2" and n < 1024:
-                continue
-            for _ in range(2):
-                run(leg)
-            ts = []
-            for _ in range(reps if hashed < (4 << 30) else 3):
+        names = ["dev", "host_1", "host_all", "routed", "routed_1", "dev_reg", "split", "split_1", "routed_reg",
+                 "routed_reg_1"] + (["routed_x2"] if n >= 1024 else [])
+        ts = {leg: [] for leg in names}
+        for r in range(2 + (reps if hashed < (4 << 30) else 3)):  # 2 warm-up rounds, then timed ones
+            for leg in names:
                 dt, out = run(leg)
-                ts.append(dt)
-            ts.sort()
-            med = ts[len(ts) // 2]
+                if r >= 2:
+                    ts[leg].append(dt)
+                outs[leg] = out
+        for leg in names:
+            med = sorted(ts[leg])[len(ts[leg]) // 2]
             row[leg + "_us"] = round(med * 1e6, 1)
             row[leg + "_GiBps"] = round(hashed / med / 2**30, 2)
-            outs[leg] = out
-        _lib.check(L.stormck_host_unregister(buf.ctypes.data))
+        _lib.check(L.stormck_host_unregister(reg.ctypes.data))
         for k in ("routed", "routed_1", "routed_reg", "routed_reg_1"):
             row[k + "_leg"] = legs.get(k)
         row["routed_x2_legs"] = sorted(legs.get("routed_x2", []))
@@ -662,7 +662,7 @@ def batch_e2e_workload(a):
         row["agree"] = all(np.array_equal(outs["host_1"], outs[k]) for k in outs)
         rows.append(row)
         print(json.dumps(row), flush=True)
-        del raw, buf
+        del raw, reg, pg
     res = {"metric": "us per host-memory batch checksum (ChecksumBatch E2E), by leg",
            "value": rows[0]["routed_us"], "unit": "us", "n_gpus": 1, "steps": reps, "warmup": 2,
            "higher_is_better": False, "scaling": "weak", "vs_baseline": None, "dtype": "u64", "data": "synthetic",

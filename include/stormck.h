@@ -351,7 +351,9 @@ int stormck_commit(void* arena, stormck_dirty_block* blocks, uint64_t n, uint64_
  * updates its rate (EWMA). */
 typedef struct stormck_route_rates {
     double host_thread;    /* one host thread (four blocks at once where the CPU has AVX-512) */
-    double host_memory;    /* the host pool's cap (host memory bandwidth, shared cores) */
+    double host_memory;    /* the host pool's cap on passes that stream from host memory */
+    double host_cached;    /* the same on passes of at most 64 MiB, which can run from the host's
+                            * caches (a commit hashes blocks its caller has just written) */
     double link_pinned;    /* one device's pipeline from pinned or registered host memory */
     double link_pageable;  /* one device's pipeline from pageable memory (through pinned staging) */
     double link_inplace;   /* one device's kernels reading registered host memory in place */

@@ -52,7 +52,7 @@ class RouteRates(ctypes.Structure):
     """stormck_route_rates: the routing model's rates (bytes per microsecond) and the
     devices' start latency in a split (microseconds)."""
 
-    _fields_ = [("host_thread", ctypes.c_double), ("host_memory", ctypes.c_double),
+    _fields_ = [("host_thread", ctypes.c_double), ("host_memory", ctypes.c_double), ("host_cached", ctypes.c_double),
                 ("link_pinned", ctypes.c_double), ("link_pageable", ctypes.c_double),
                 ("link_inplace", ctypes.c_double), ("device_latency", ctypes.c_double),
                 ("observations", c_uint64)]

@@ -2572,6 +2572,11 @@ constexpr double kPriorDeviceLatencyUs = 150.0; // a split's device part until i
 constexpr double kLearnWeight = 0.25;           // EWMA weight of one call's observed rate
 constexpr uint64_t kLearnMinHostBytes = 8ULL << 20;   // below: fork/join noise
 constexpr uint64_t kLearnMinLinkBytes = 64ULL << 20;  // below: launch and sync noise
+// A host pass of at most this many bytes can run from the host's caches (a storm commit,
+// ~38 MB, written by the caller just before): the pool's cap on it is learned apart from
+// the cap on passes that stream from DRAM (c5 on the pool: ~100 us = 380 GB/s, against
+// 180-330 GB/s for an 8 GiB batch, profiles/r05_third/).
+constexpr uint64_t kHostCacheBytes = 64ULL << 20;
 
 enum class Link { kPinned, kPageable, kInplace };
 
@@ -2599,13 +2604,14 @@ class RouteModel {
         const double rate = static_cast<double>(bytes) / us;
         std::lock_guard<std::mutex> g(mu_);
         if (frozen_) return;
+        double& cap = bytes <= kHostCacheBytes ? r_.host_cached : r_.host_memory;
         if (threads <= 1) {
             r_.host_thread = ewma(r_.host_thread, rate);
         } else if (rate >= 0.8 * threads * r_.host_thread) {
             r_.host_thread = ewma(r_.host_thread, rate / threads);
-            r_.host_memory = std::max(r_.host_memory, rate);
+            cap = std::max(cap, rate);
         } else {
-            r_.host_memory = ewma(r_.host_memory, rate);
+            cap = ewma(cap, rate);
         }
         ++r_.observations;
     }
@@ -2637,6 +2643,7 @@ class RouteModel {
         std::memset(&r, 0, sizeof r);
         r.host_thread = host::has_x4() ? kPriorHostThreadX4 : kPriorHostThread;
         r.host_memory = kPriorHostMemory;
+        r.host_cached = kPriorHostMemory;
         r.link_pinned = kPriorLinkPinned;
         r.link_pageable = kPriorLinkPageable;
         r.link_inplace = kPriorLinkInplace;
@@ -2650,8 +2657,9 @@ class RouteModel {
 };
 
 // Aggregate rate of `threads` host threads.
-double host_rate(const stormck_route_rates& r, unsigned threads) {
-    return threads <= 1 ? r.host_thread : std::min(threads * r.host_thread, r.host_memory);
+double host_rate(const stormck_route_rates& r, unsigned threads, uint64_t bytes) {
+    const double cap = bytes <= kHostCacheBytes ? r.host_cached : r.host_memory;
+    return threads <= 1 ? r.host_thread : std::min(threads * r.host_thread, cap);
 }
 
 // Threads a host pass of `bytes` uses out of `nt` allowed.
@@ -3089,7 +3097,7 @@ int split_run(const SplitArgs& A, const std::vector<int>& devs, unsigned pl, uin
     pl = std::max(1u, std::min(pl, fj.size()));
     const unsigned nd = static_cast<unsigned>(devs.size());
     const double r_dev = A.in_place ? rt.link_inplace : rt.link_pinned;
-    const double r_host = host_rate(rt, pl);
+    const double r_host = host_rate(rt, pl, bytes);
     SplitQueue q(n, nd ? fixed : 0, bpb, r_host, r_dev, nd);
     const double lat = rt.device_latency;
     const double t_post = now_us();
@@ -3244,13 +3252,14 @@ LegPlan plan_batch(const stormck_route_rates& r, uint64_t n, const BatchShape& s
     const unsigned pl = host_threads_for(s.bytes, nt);
     const double bytes = static_cast<double>(s.bytes), chain = static_cast<double>(s.longest) / kDevChainBytesPerUs;
     const double level = pl > 1 ? kHostLevelUs : 0.0;
-    p.us[0] = bytes / host_rate(r, pl) + level;
+    const double r_h = host_rate(r, pl, s.bytes);
+    p.us[0] = bytes / r_h + level;
     if (ndev && staged_ok) {
         const double link = pinned ? r.link_pinned : r.link_pageable;
         const double fill = pinned ? 0.0 : static_cast<double>(std::min<uint64_t>(s.bytes, kChunkBytes)) / kStageCopyBytesPerUs;
         p.us[1] = kDevBatchCallUs + chain + bytes / (ndev * link) + fill;
         if (pinned && n >= 2)
-            p.us[2] = split_us(bytes, host_rate(r, pl), ndev * r.link_inplace, r.device_latency, level, p.us[0]);
+            p.us[2] = split_us(bytes, r_h, ndev * r.link_inplace, r.device_latency, level, p.us[0]);
     }
     pick_leg(&p);
     return p;
@@ -3292,7 +3301,7 @@ bool commit_shape(const stormck_dirty_block* blocks, uint64_t n, CommitShape* s)
 // chain, and a fork/join when it is spread.
 double host_height_us(const stormck_route_rates& r, const CommitShape& s, size_t l, unsigned nt) {
     const unsigned pl = host_threads_for(s.bytes[l], nt);
-    const double t = std::max(static_cast<double>(s.bytes[l]) / host_rate(r, pl),
+    const double t = std::max(static_cast<double>(s.bytes[l]) / host_rate(r, pl, s.bytes[l]),
                               static_cast<double>(s.longest[l]) / r.host_thread);
     return t + (pl > 1 ? kHostLevelUs : 0.0);
 }
@@ -3313,7 +3322,7 @@ LegPlan plan_commit(const stormck_route_rates& r, const CommitShape& s, bool reg
         if (s.cnt[0] >= 2) {
             const double h0 = host_height_us(r, s, 0, nt);
             const unsigned pl = host_threads_for(s.bytes[0], nt);
-            const double t0 = split_us(static_cast<double>(s.bytes[0]), host_rate(r, pl), ndev * r.link_inplace,
+            const double t0 = split_us(static_cast<double>(s.bytes[0]), host_rate(r, pl, s.bytes[0]), ndev * r.link_inplace,
                                        r.device_latency, pl > 1 ? kHostLevelUs : 0.0, h0);
             p.us[2] = p.us[0] - h0 + t0;
         }
@@ -3732,7 +3741,7 @@ int stormck_route_get_rates(stormck_route_rates* rates) {
 
 int stormck_route_set_rates(const stormck_route_rates* rates, uint32_t flags) {
     if (flags & ~STORMCK_RATES_FREEZE) return fail(STORMCK_EINVAL, "unknown flags");
-    if (rates && !(rates->host_thread > 0 && rates->host_memory > 0 && rates->link_pinned > 0 &&
+    if (rates && !(rates->host_thread > 0 && rates->host_memory > 0 && rates->host_cached > 0 && rates->link_pinned > 0 &&
                    rates->link_pageable > 0 && rates->link_inplace > 0 && rates->device_latency >= 0))
         return fail(STORMCK_EINVAL, "every rate must be positive (and the latency not negative)");
     RouteModel::get().set(rates, (flags & STORMCK_RATES_FREEZE) != 0);

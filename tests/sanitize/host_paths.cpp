@@ -388,7 +388,12 @@ static void split_paths() {
     std::vector<uint64_t> want(n);
     for (uint64_t i = 0; i < n; ++i) want[i] = oracle_xxh64(buf.data() + i * stride, lens[i]);
     CHECK(stormck_host_register(buf.data(), buf.size()) == STORMCK_OK);
-    const stormck_route_rates slow_host = {2000.0, 8000.0, 55000.0, 50000.0, 50000.0, 0};
+    stormck_route_rates slow_host;
+    std::memset(&slow_host, 0, sizeof slow_host);
+    slow_host.host_thread = 2000.0;
+    slow_host.host_memory = slow_host.host_cached = 8000.0;
+    slow_host.link_pinned = 55000.0;
+    slow_host.link_pageable = slow_host.link_inplace = 50000.0;
     CHECK(stormck_route_set_rates(&slow_host, STORMCK_RATES_FREEZE) == STORMCK_OK);
     auto run = [&](int t) {
         std::vector<uint64_t> got(n);

@@ -18,8 +18,8 @@ import pytest
 from storm_amd import _lib, blocks
 from storm_amd import commit as sc
 
-RATES = dict(host_thread=40000.0, host_memory=180000.0, link_pinned=55000.0, link_pageable=50000.0,
-             link_inplace=52000.0, device_latency=120.0)
+RATES = dict(host_thread=40000.0, host_memory=180000.0, host_cached=180000.0, link_pinned=55000.0,
+             link_pageable=50000.0, link_inplace=52000.0, device_latency=120.0)
 LEVEL_US, CALL_US, CHAIN = 10.0, 16.0, 1600.0  # stormck.hip kHostLevelUs, kDevBatchCallUs, kDevChainBytesPerUs
 POOL = 16
 GIB8 = 262144  # 8 GiB of 32 KiB blocks
@@ -51,7 +51,8 @@ def test_rates_set_get_and_priors(rates):
     assert got["observations"] == 0
     blocks.SetRouteRates(None)
     pri = blocks.RouteRates()
-    assert pri["host_memory"] == 180000.0 and pri["link_pinned"] == 55000.0 and pri["link_inplace"] == 50000.0
+    assert pri["host_memory"] == 180000.0 and pri["host_cached"] == 180000.0
+    assert pri["link_pinned"] == 55000.0 and pri["link_inplace"] == 50000.0
     assert pri["device_latency"] == 150.0
     assert pri["host_thread"] in (24000.0, 48000.0)  # scalar / AVX-512 four-block prior
 
@@ -64,9 +65,14 @@ def test_small_batches_stay_on_the_host(rates):
 
 
 def test_host_time_formula(rates):
-    n, L = 16384, 32768
+    """bytes / min(threads x per-thread rate, the pool's cap) + fork/join; the cap of a
+    pass of at most 64 MiB (cache-resident) is learned apart from larger passes'."""
+    rates(host_cached=90000.0)
+    n, L = 16384, 32768  # 512 MiB: the DRAM cap
     leg, us = blocks.PlanBatch(n, L, L, pinned=False, host_threads=4)
     assert us[0] == pytest.approx(n * L / min(4 * RATES["host_thread"], RATES["host_memory"]) + LEVEL_US)
+    leg, us = blocks.PlanBatch(1024, L, L, pinned=False, host_threads=4)  # 32 MiB: the cache-sized cap
+    assert us[0] == pytest.approx(1024 * L / min(4 * RATES["host_thread"], 90000.0) + LEVEL_US)
     leg, us = blocks.PlanBatch(n, L, L, pinned=False, host_threads=1)
     assert us[0] == pytest.approx(n * L / RATES["host_thread"])
 
@@ -125,13 +131,13 @@ def test_the_start_latency_keeps_short_calls_off_the_split(rates):
     a c5-size batch (38 MB, ~200 us on the host) does not split when the latency is a large
     part of it, and does when it is small; with one host thread it splits either way."""
     c5 = [31808] * 1200 + [30000, 72]
-    rates(device_latency=150.0, host_memory=400000.0)
+    rates(device_latency=150.0, host_cached=400000.0)
     leg, us = blocks.PlanBatch(len(c5), 32768, lens=c5, pinned=True)
     if _pool() >= 8:
         assert leg == _lib.LEG_HOST, us
     leg, us = blocks.PlanBatch(len(c5), 32768, lens=c5, pinned=True, host_threads=1)
     assert leg == _lib.LEG_SPLIT, us
-    rates(device_latency=1.0, host_memory=100000.0)
+    rates(device_latency=1.0, host_cached=100000.0)
     leg, us = blocks.PlanBatch(len(c5), 32768, lens=c5, pinned=True)
     assert leg == _lib.LEG_SPLIT, us
 
@@ -139,7 +145,7 @@ def test_the_start_latency_keeps_short_calls_off_the_split(rates):
 def test_a_fast_host_makes_the_split_a_tie_and_keeps_the_host(rates):
     """When the link adds under 5% to the host's rate the split is not taken (no flapping
     between two legs of about the same time)."""
-    rates(host_thread=400000.0, host_memory=4000000.0)
+    rates(host_thread=400000.0, host_memory=4000000.0, host_cached=4000000.0)
     leg, us = blocks.PlanBatch(GIB8, 32768, 32768, pinned=True)
     if _pool() > 1:
         assert leg == _lib.LEG_HOST, us
@@ -189,7 +195,7 @@ def test_host_leg_measures_the_per_thread_rate():
         got = blocks.RouteRates()
         assert got["observations"] == 1
         assert got["host_thread"] > 1000.0  # 1 + (observed - 1) / 4, observed in GB/s
-        assert got["host_memory"] == RATES["host_memory"]
+        assert got["host_memory"] == RATES["host_memory"] and got["host_cached"] == RATES["host_cached"]
         blocks.SetRouteRates(r, freeze=True)
         blocks.ChecksumBatchHost(buf, n, stride, stride, threads=1)
         assert blocks.RouteRates()["host_thread"] == 1.0
@@ -201,15 +207,16 @@ def test_host_leg_measures_the_per_thread_rate():
         blocks.SetRouteRates(None)
 
 
-def test_pool_pass_below_the_threads_rate_measures_the_memory_cap():
+def test_pool_pass_below_the_threads_rate_measures_the_pool_cap():
     if _pool() < 2:
         pytest.skip("one hardware thread")
     n, stride = 1024, 32768  # 32 MiB
     buf = _rows(n, stride, 4)
-    blocks.SetRouteRates(dict(RATES, host_thread=1e9, host_memory=1.0))
+    blocks.SetRouteRates(dict(RATES, host_thread=1e9, host_memory=1.0, host_cached=1.0))
     try:
-        blocks.ChecksumBatchHost(buf, n, stride, stride, threads=2)
+        blocks.ChecksumBatchHost(buf, n, stride, stride, threads=2)  # 32 MiB: the cache-sized cap
         got = blocks.RouteRates()
-        assert got["observations"] == 1 and got["host_memory"] > 1000.0 and got["host_thread"] == 1e9
+        assert got["observations"] == 1 and got["host_cached"] > 1000.0 and got["host_thread"] == 1e9
+        assert got["host_memory"] == 1.0
     finally:
         blocks.SetRouteRates(None)

@@ -30,10 +30,10 @@ torch = pytest.importorskip("torch")
 STORM_LENS = [72, 28808, 30000, 31808, 32768]
 # rates that make the split the model's clear choice for large calls (a host slower than
 # the link), frozen so that the routed calls below are deterministic
-SLOW_HOST = dict(host_thread=2000.0, host_memory=8000.0, link_pinned=55000.0, link_pageable=50000.0,
-                 link_inplace=50000.0)
-SLOW_LINK = dict(host_thread=40000.0, host_memory=300000.0, link_pinned=100.0, link_pageable=100.0,
-                 link_inplace=100.0)
+SLOW_HOST = dict(host_thread=2000.0, host_memory=8000.0, host_cached=8000.0, link_pinned=55000.0,
+                 link_pageable=50000.0, link_inplace=50000.0)
+SLOW_LINK = dict(host_thread=40000.0, host_memory=300000.0, host_cached=300000.0, link_pinned=100.0,
+                 link_pageable=100.0, link_inplace=100.0)
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -298,7 +298,7 @@ def test_route_devices_and_rates_learned_on_the_gpu():
     try:
         # the device leg is the model's choice (a 1-byte/us host), the link prior far too low
         blocks.SetRouteRates(dict(SLOW_HOST, link_pinned=1000.0, link_inplace=1000.0, host_thread=1.0,
-                                  host_memory=1.0))
+                                  host_memory=1.0, host_cached=1.0))
         got, leg = blocks.ChecksumBatchLeg(reg.a, n, stride, stride, host_threads=1)
         assert leg == _lib.LEG_DEVICE
         r = blocks.RouteRates()
