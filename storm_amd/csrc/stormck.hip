@@ -2558,6 +2558,7 @@ constexpr double kSplitMinClaimBytes = 1 << 20;   // a smaller device claim cost
 constexpr double kSplitDmaBytes = 32 << 20;       // strided claims from this size take the copy engine
 constexpr double kSplitGain = 0.95;               // the split is taken only when predicted 5% faster
 constexpr double kHostOnlyUs = 10.0;              // calls one host thread finishes this fast are not planned
+constexpr double kSplitMinSaveUs = 30.0;          // ... and only when it saves at least this much
 
 // Priors, bytes/us: the rates measured on an MI355X box with its EPYC 9575F host
 // (profiles/r04_batch_e2e/, r04_commit_e2e/).
@@ -2601,7 +2602,9 @@ class RouteModel {
     // that host memory and shared cores put on them (it ran below it).
     void learn_host(uint64_t bytes, unsigned threads, double us) {
         if (bytes < kLearnMinHostBytes || us <= 0) return;
-        const double rate = static_cast<double>(bytes) / us;
+        // the plans add the fork/join of a spread pass on top of bytes / rate: learn the
+        // rate without it
+        const double rate = static_cast<double>(bytes) / std::max(1.0, us - (threads > 1 ? kHostLevelUs : 0.0));
         std::lock_guard<std::mutex> g(mu_);
         if (frozen_) return;
         double& cap = bytes <= kHostCacheBytes ? r_.host_cached : r_.host_memory;
@@ -3224,6 +3227,9 @@ struct LegPlan {
     double best() const { return us[leg == STORMCK_LEG_DEVICE ? 1 : (leg == STORMCK_LEG_SPLIT ? 2 : 0)]; }
 };
 
+// The split is taken only when it is predicted to save both kSplitGain of the best single
+// leg and kSplitMinSaveUs: on small calls the devices' part is a few chunks whose start and
+// finish vary by tens of microseconds (profiles/r05_fourth/), more than it could save.
 void pick_leg(LegPlan* p) {
     double best = p->us[0];
     p->leg = STORMCK_LEG_HOST;
@@ -3231,7 +3237,7 @@ void pick_leg(LegPlan* p) {
         best = p->us[1];
         p->leg = STORMCK_LEG_DEVICE;
     }
-    if (p->us[2] < kSplitGain * best) p->leg = STORMCK_LEG_SPLIT;
+    if (p->us[2] < kSplitGain * best && p->us[2] < best - kSplitMinSaveUs) p->leg = STORMCK_LEG_SPLIT;
 }
 
 // Time of a split that hashes `bytes` on host threads at r_h and devices at r_d together,

@@ -126,6 +126,15 @@ def test_a_slow_link_keeps_everything_on_the_host(rates):
         assert leg == _lib.LEG_HOST, (pinned, us)
 
 
+def test_the_split_must_save_a_margin(rates):
+    """The split is taken only when predicted to save >= 5% of the best single leg and
+    >= 30 us: a 1.5 MB batch whose split would save a few microseconds stays on the host."""
+    rates(device_latency=1.0, host_cached=50000.0, host_thread=50000.0)
+    leg, us = blocks.PlanBatch(48, 32768, 32768, pinned=True)
+    assert math.isfinite(us[2]) and us[2] < 0.95 * us[0] and us[0] - us[2] < 30.0, us
+    assert leg == _lib.LEG_HOST
+
+
 def test_the_start_latency_keeps_short_calls_off_the_split(rates):
     """A split pays the devices' start latency before they return anything: with the pool,
     a c5-size batch (38 MB, ~200 us on the host) does not split when the latency is a large
