@@ -2958,9 +2958,12 @@ void device_part(const SplitArgs& A, SplitQueue& q, double lat_us, DevRun* r) {
     // blocks per chunk: what the staging chunk holds (DMA), or the offsets and lengths its
     // pinned buffer holds, about a chunk's worth of bytes (in place)
     const uint64_t step = B.n == 1 ? std::max<uint64_t>(B.len_of(0), 8) : std::max<uint64_t>(B.stride, 8);
-    const uint64_t max_blocks = A.in_place
+    uint64_t max_blocks = A.in_place
         ? std::max<uint64_t>(1, std::min<uint64_t>(kChunkBytes / 12, static_cast<uint64_t>(kChunkBytes / bpb)))
         : std::max<uint64_t>(1, kChunkBytes / step);
+    // a strided chunk may take the copy engine (issue below): its rows, stride apart, must
+    // fit the staging buffer whatever the blocks' lengths
+    if (!B.offs) max_blocks = std::min<uint64_t>(max_blocks, std::max<uint64_t>(1, kChunkBytes / step));
     double inflight = 0, t0 = 0, t_end = 0;
     double stage_bytes[kStages] = {};
     using ull = unsigned long long;

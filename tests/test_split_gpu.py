@@ -81,6 +81,25 @@ def test_split_fixed_boundaries_storm_lengths():
         reg.close()
 
 
+def test_split_chunks_beyond_one_staging_buffer():
+    """Device shares larger than the 256 MiB staging chunk, with lengths below the stride:
+    every chunk the copy engine takes fits its staging buffer (rows are stride apart)."""
+    n, stride = 12000, 32768  # 393 MB of rows
+    lens = np.full(n, 31808, dtype=np.uint32)
+    lens[::7] = 30000
+    reg = _filled(n, stride, 12)
+    try:
+        want = o.checksum_batch(reg.a, n, stride, lens=lens, threads=8)
+        for d in (n, n - 1, 9000):
+            got, done = blocks.ChecksumBatchSplit(reg.a, n, stride, lens=lens, device_blocks=d)
+            assert done == d and np.array_equal(got, want), d
+        bad = want.copy()
+        bad[[5, n - 5]] ^= 9
+        assert blocks.VerifyChecksumBatchSplit(reg.a, n, stride, bad, lens=lens, device_blocks=n) == (5, 2, n)
+    finally:
+        reg.close()
+
+
 @pytest.mark.parametrize("stride,length", [(32768, 32768), (1024, 1000), (4096, 4096)])
 def test_split_uniform_lengths(stride, length):
     n = 3001
