@@ -2909,6 +2909,7 @@ struct SplitArgs {
     const uint64_t* expected = nullptr;  // verify: compare instead of returning checksums
     Sink* sink = nullptr;                // checksums
     bool in_place = false;               // devices read B.base in place (mapped memory), not by DMA copies
+    double bytes_per_block = 1.0;        // set by split_run
 };
 
 struct DevRun {
@@ -2954,7 +2955,7 @@ void device_part(const SplitArgs& A, SplitQueue& q, double lat_us, DevRun* r) {
             return failed(fail(STORMCK_EHIP, std::string("split: hipHostGetDevicePointer: ") + hipGetErrorString(e)));
         d_base = static_cast<const uint8_t*>(d);
     }
-    const double bpb = std::max(1.0, static_cast<double>(B.bytes(0, B.n)) / static_cast<double>(B.n));
+    const double bpb = A.bytes_per_block;
     // blocks per chunk: what the staging chunk holds (DMA), or the offsets and lengths its
     // pinned buffer holds, about a chunk's worth of bytes (in place)
     const uint64_t step = B.n == 1 ? std::max<uint64_t>(B.len_of(0), 8) : std::max<uint64_t>(B.stride, 8);
@@ -3089,7 +3090,7 @@ bool trace_on() {
 // devs is empty). fixed: STORMCK_SPLIT_BALANCED, or the number of blocks (the last ones)
 // the devices hash. Verify (A.expected): *R gets the lowest mismatching index (n if none)
 // and the count over both sides.
-int split_run(const SplitArgs& A, const std::vector<int>& devs, unsigned pl, uint64_t fixed, SplitResult* R) {
+int split_run(SplitArgs& A, const std::vector<int>& devs, unsigned pl, uint64_t fixed, SplitResult* R) {
     const Blocks& B = A.B;
     const uint64_t n = B.n;
     R->first_bad = n;
@@ -3098,6 +3099,7 @@ int split_run(const SplitArgs& A, const std::vector<int>& devs, unsigned pl, uin
     if (n == 0) return STORMCK_OK;
     const uint64_t bytes = B.bytes(0, n);
     const double bpb = std::max(1.0, static_cast<double>(bytes) / static_cast<double>(n));
+    A.bytes_per_block = bpb;
     const stormck_route_rates rt = RouteModel::get().now();
     ForkJoin& fj = ForkJoin::get();
     pl = std::max(1u, std::min(pl, fj.size()));
@@ -3654,12 +3656,24 @@ int stormck_commit(void* arena, stormck_dirty_block* blocks, uint64_t n, uint64_
     }
     if (mem == Mem::kUnreadable) return not_host_memory(mem);
     const bool registered = mem == Mem::kMapped;
+    // a forest one host thread hashes faster than any device can start returning (storm's
+    // smallest commits: a few blocks) takes the host leg without planning
+    const stormck_route_rates rt = RouteModel::get().now();
+    {
+        uint64_t total = 0;
+        for (uint64_t i = 0; i < n && static_cast<double>(total) / rt.host_thread < kHostOnlyUs; ++i)
+            total += blocks[i].length;
+        if (static_cast<double>(total) / rt.host_thread < kHostOnlyUs) {
+            if (leg_used) *leg_used = STORMCK_LEG_HOST;
+            if (registered) HIP_TRY(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
+            return stormck_commit_host(arena, blocks, n, revision, last_allocated_block, out_checksums, 1);
+        }
+    }
     std::vector<int> devs;
     rc = route_devices(&devs);
     if (rc) return rc;
     CommitShape shape;
     const bool planned = commit_shape(blocks, n, &shape);  // false: malformed (the host leg says why)
-    const stormck_route_rates rt = RouteModel::get().now();
     auto plan_for = [&](unsigned t) {
         return plan_commit(rt, shape, registered, t, static_cast<unsigned>(devs.size()));
     };
