@@ -500,9 +500,14 @@ bool big_w_on() {  // probe knob STORMCK_BIG_W=0: batches from kBigBatch on alwa
     return on;
 }
 
+// remote: the blocks are host memory read in place over PCIe (the split leg). The link
+// carries a kernel's loads as read requests of the loads' size, so the kernels that read
+// 16 bytes per lane in wave-wide runs (LDS-DMA) keep it at its rate, while the register
+// quad kernel's 32-byte reads run it at ~36 GB/s against ~54 (profiles/r05_rates/):
+// gathers past the wide-multi range then take the LDS-DMA var kernel at any size.
 int launch_checksum(const uint8_t* base, uint64_t stride, const uint32_t* lens, uint32_t len, const uint64_t* offs,
                     uint64_t n, uint64_t* out, const uint64_t* expected, unsigned long long* first_bad,
-                    unsigned long long* n_bad, hipStream_t st) {
+                    unsigned long long* n_bad, hipStream_t st, bool remote = false) {
     const bool verify = expected != nullptr;
     // The longest block the dispatch plans for: len for uniform lengths; with per-block
     // lengths (on the device) the caller's upper bound passed in len, 0 = unknown, planned
@@ -615,7 +620,8 @@ int launch_checksum(const uint8_t* base, uint64_t stride, const uint32_t* lens, 
         const char* e = STORMCK_KNOB("STORMCK_VAR_LO");
         return e ? std::strtoull(e, nullptr, 10) : 0;
     }();
-    if (var_on && n >= (var_lo ? var_lo : std::max<uint64_t>(kMidBatch, 44 * cu_count())) && n > 16 * cu_count() &&
+    const uint64_t var_min_n = var_lo ? var_lo : remote ? 0 : std::max<uint64_t>(kMidBatch, 44 * cu_count());
+    if (var_on && n >= var_min_n && n > (remote ? kMultiBpwRing : 16) * cu_count() &&
         (lens || offs) && plan_len > var_min_len() &&
         (offs || ((reinterpret_cast<uintptr_t>(base) & 15) == 0 && (stride & 15) == 0))) {
         // below kBigBatch: 3- or 1-wave workgroups, whichever loads the busiest CU least;
@@ -3035,11 +3041,13 @@ void device_part(const SplitArgs& A, SplitQueue& q, double lat_us, DevRun* r) {
             s.h_result[1] = 0;
             HIP_TRY(hipMemcpyAsync(s.d_result, s.h_result, 16, hipMemcpyHostToDevice, s.stream));
             lrc = launch_checksum(base, stride, dl, plan, offs, cnt, nullptr, s.d_expected,
-                                  reinterpret_cast<ull*>(s.d_result), reinterpret_cast<ull*>(s.d_result + 1), s.stream);
+                                  reinterpret_cast<ull*>(s.d_result), reinterpret_cast<ull*>(s.d_result + 1), s.stream,
+                                  A.in_place && base != s.d_data);
             if (lrc) return lrc;
             HIP_TRY(hipMemcpyAsync(s.h_result, s.d_result, 16, hipMemcpyDeviceToHost, s.stream));
         } else {
-            lrc = launch_checksum(base, stride, dl, plan, offs, cnt, s.d_out, nullptr, nullptr, nullptr, s.stream);
+            lrc = launch_checksum(base, stride, dl, plan, offs, cnt, s.d_out, nullptr, nullptr, nullptr, s.stream,
+                                  A.in_place && base != s.d_data);
             if (lrc) return lrc;
             HIP_TRY(hipMemcpyAsync(s.h_out, s.d_out, cnt * 8, hipMemcpyDeviceToHost, s.stream));
         }
