@@ -125,7 +125,7 @@ def main(tag, arena):
         gather(src, dst, corr)
 
 
-GATHER_KERNEL = "k_xxh64_glds_var<16, 2, false, 8, 8, true, true, true>"
+GATHER_KERNEL = "k_xxh64_glds_var<16, 2, false, 8, 8, true, true, true"  # a prefix: later template arguments vary
 
 
 def last_json(path):
