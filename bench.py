@@ -27,6 +27,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import random
 import sys
 import time
 
@@ -409,7 +410,8 @@ def commit_e2e_workload(a):
     commit (2 leaves + their pointer block), a `-tags test` forest (100 leaves of 536 /
     728 B under fan-out-10 pointer blocks of 256 B, storm_test.go:131-138), and larger
     forests of 16K and 128K leaves. Every leg's checksums must agree. One line per run
-    with a table (median us per commit over --steps reps)."""
+    with a table: median us per commit over --steps rounds, every leg once per round in a
+    fresh seeded order."""
     import ctypes
     import numpy as np
     import torch
@@ -480,7 +482,7 @@ def commit_e2e_workload(a):
         names = ("dev_inplace", "dev_hbm", "host_1", "host_all", "split", "split_1", "routed", "routed_1")
         ts = {leg: [] for leg in names}
         for r in range(2 + (reps if bytes_hashed < (1 << 30) else 3)):  # 2 warm-up rounds, interleaved legs
-            for leg in names:
+            for leg in random.Random(r).sample(names, len(names)):  # a fresh (seeded) order every round
                 dt, out = run(leg)
                 if r >= 2:
                     ts[leg].append(dt)
@@ -541,8 +543,10 @@ def batch_e2e_workload(a):
     batch (1,200 objectlist leaves + a pointer block + the singularity,
     keystore/benchmark_test.go:58-62), the c1 batch (1K x 32 KiB), 3 blocks, a `-tags test`
     batch (100 blocks of 536 / 728 B, storm_test.go:131-138), 16K and 256K blocks of 32 KiB
-    (512 MiB, 8 GiB). Every leg's checksums must agree. One line per batch with the table
-    (median us per call over --steps reps); routed_over_best = routed / the best of
+    (512 MiB, 8 GiB). Every leg's checksums must agree. One line per batch with the table:
+    median us per call over --steps rounds, every leg once per round in a fresh seeded order
+    (no leg always inherits the same predecessor's cache state); routed_over_best = routed /
+    the best of
     host_all, dev, dev_reg, split on the same memory kind (1 thread: host_1, dev, split_1)."""
     import ctypes
     import numpy as np
@@ -635,7 +639,9 @@ def batch_e2e_workload(a):
                  "routed_reg_1"] + (["routed_x2"] if n >= 1024 else [])
         ts = {leg: [] for leg in names}
         for r in range(2 + (reps if hashed < (4 << 30) else 3)):  # 2 warm-up rounds, then timed ones
-            for leg in names:
+            # a fresh leg order every round (seeded): each leg follows different legs, so no
+            # leg inherits one predecessor's cache and device state every time
+            for leg in random.Random(r).sample(names, len(names)):
                 dt, out = run(leg)
                 if r >= 2:
                     ts[leg].append(dt)
