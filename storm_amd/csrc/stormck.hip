@@ -2971,6 +2971,13 @@ void device_part(const SplitArgs& A, SplitQueue& q, double lat_us, DevRun* r) {
     // a strided chunk may take the copy engine (issue below): its rows, stride apart, must
     // fit the staging buffer whatever the blocks' lengths
     if (!B.offs) max_blocks = std::min<uint64_t>(max_blocks, std::max<uint64_t>(1, kChunkBytes / step));
+    // chunks of at most 1/16 of the call (and at least kSplitDmaBytes): each claim is sized
+    // from what the host threads have actually left, so a host faster or slower than its
+    // rate moves the devices' later claims instead of leaving one large chunk in flight
+    // at the end
+    max_blocks = std::min<uint64_t>(
+        max_blocks, std::max<uint64_t>(1, static_cast<uint64_t>(
+                                              std::max(kSplitDmaBytes, bpb * static_cast<double>(B.n) / 16.0) / bpb)));
     double inflight = 0, t0 = 0, t_end = 0;
     double stage_bytes[kStages] = {};
     using ull = unsigned long long;
