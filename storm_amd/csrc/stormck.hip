@@ -19,6 +19,7 @@
 
 #include <fcntl.h>
 #include <pthread.h>
+#include <sched.h>
 #include <sys/uio.h>
 #include <unistd.h>
 
@@ -85,10 +86,29 @@ class ForkJoin {
         while (remaining_.load(std::memory_order_acquire) != 0) std::this_thread::yield();
     }
 
+    // CPUs the process may use at once: its affinity mask, capped by a cgroup v2 CPU quota
+    // (a GPU box grants each GPU's process 16 CPUs of a 256-CPU host by quota)
+    static unsigned usable_cpus() {
+        cpu_set_t set;
+        unsigned cpus = std::max(1u, std::thread::hardware_concurrency());
+        if (sched_getaffinity(0, sizeof set, &set) == 0) cpus = std::max(1, CPU_COUNT(&set));
+        if (FILE* f = std::fopen("/sys/fs/cgroup/cpu.max", "r")) {
+            char quota[32] = {};
+            unsigned long long period = 0;
+            if (std::fscanf(f, "%31s %llu", quota, &period) == 2 && std::strcmp(quota, "max") != 0 && period > 0) {
+                const double q = std::strtod(quota, nullptr) / static_cast<double>(period);
+                cpus = std::min(cpus, std::max(1u, static_cast<unsigned>(q + 0.5)));
+            }
+            std::fclose(f);
+        }
+        return cpus;
+    }
+    unsigned cpus() const { return cpus_; }
+
   private:
     ForkJoin() {
-        const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-        nw_ = std::min(16u, hw) - 1;
+        cpus_ = usable_cpus();
+        nw_ = std::min(16u, cpus_) - 1;
         for (unsigned i = 0; i < nw_; ++i) std::thread([this, i] { loop(i + 1); }).detach();
     }
     void loop(unsigned id) {
@@ -119,7 +139,7 @@ class ForkJoin {
     static inline ForkJoin* instance_ = nullptr;
     static inline std::mutex make_mu_;
     std::atomic<double> busy_until_{0.0};
-    unsigned nw_ = 0;
+    unsigned nw_ = 0, cpus_ = 1;
     std::mutex run_mu_, mu_;
     std::condition_variable cv_;
     std::atomic<uint64_t> gen_{0};
@@ -2671,6 +2691,16 @@ double host_rate(const stormck_route_rates& r, unsigned threads, uint64_t bytes)
     return threads <= 1 ? r.host_thread : std::min(threads * r.host_thread, cap);
 }
 
+// Host threads a split may use beside `nd` device workers: the pool, less one CPU per
+// device where the pool alone would take every CPU the process may use. A device's worker
+// and the HIP runtime threads serving it need a CPU now and then; on a GPU box, whose
+// process gets 16 CPUs by quota, 16 hashing threads beside them starved them, and c5-size
+// splits lost 20-30 % (profiles/r05_seventh/).
+unsigned split_threads(ForkJoin& fj, unsigned nd) {
+    if (nd == 0) return fj.size();
+    return fj.size() + nd > fj.cpus() ? std::max(1u, fj.cpus() > nd ? fj.cpus() - nd : 1u) : fj.size();
+}
+
 // Threads a host pass of `bytes` uses out of `nt` allowed.
 unsigned host_threads_for(uint64_t bytes, unsigned nt) {
     return static_cast<unsigned>(std::min<uint64_t>(std::max(1u, nt), std::max<uint64_t>(1, bytes / kHostMinBytesPerThread)));
@@ -3117,8 +3147,8 @@ int split_run(SplitArgs& A, const std::vector<int>& devs, unsigned pl, uint64_t 
     A.bytes_per_block = bpb;
     const stormck_route_rates rt = RouteModel::get().now();
     ForkJoin& fj = ForkJoin::get();
-    pl = std::max(1u, std::min(pl, fj.size()));
     const unsigned nd = static_cast<unsigned>(devs.size());
+    pl = std::max(1u, std::min(pl, split_threads(fj, nd)));
     const double r_dev = A.in_place ? rt.link_inplace : rt.link_pinned;
     const double r_host = host_rate(rt, pl, bytes);
     SplitQueue q(n, nd ? fixed : 0, bpb, r_host, r_dev, nd);
@@ -3284,8 +3314,11 @@ LegPlan plan_batch(const stormck_route_rates& r, uint64_t n, const BatchShape& s
         const double link = pinned ? r.link_pinned : r.link_pageable;
         const double fill = pinned ? 0.0 : static_cast<double>(std::min<uint64_t>(s.bytes, kChunkBytes)) / kStageCopyBytesPerUs;
         p.us[1] = kDevBatchCallUs + chain + bytes / (ndev * link) + fill;
-        if (pinned && n >= 2)
-            p.us[2] = split_us(bytes, r_h, ndev * r.link_inplace, r.device_latency, level, p.us[0]);
+        if (pinned && n >= 2) {
+            const unsigned ps = std::min(pl, split_threads(ForkJoin::get(), ndev));
+            p.us[2] = split_us(bytes, host_rate(r, ps, s.bytes), ndev * r.link_inplace, r.device_latency,
+                               ps > 1 ? kHostLevelUs : 0.0, p.us[0]);
+        }
     }
     pick_leg(&p);
     return p;
@@ -3347,7 +3380,7 @@ LegPlan plan_commit(const stormck_route_rates& r, const CommitShape& s, bool reg
                                               static_cast<double>(s.bytes[l]) / r.link_inplace);
         if (s.cnt[0] >= 2) {
             const double h0 = host_height_us(r, s, 0, nt);
-            const unsigned pl = host_threads_for(s.bytes[0], nt);
+            const unsigned pl = std::min(host_threads_for(s.bytes[0], nt), split_threads(ForkJoin::get(), ndev));
             const double t0 = split_us(static_cast<double>(s.bytes[0]), host_rate(r, pl, s.bytes[0]), ndev * r.link_inplace,
                                        r.device_latency, pl > 1 ? kHostLevelUs : 0.0, h0);
             p.us[2] = p.us[0] - h0 + t0;
