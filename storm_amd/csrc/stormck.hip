@@ -3220,7 +3220,11 @@ int split_run(SplitArgs& A, const std::vector<int>& devs, unsigned pl, uint64_t 
     R->first_bad = fb;
     R->n_bad = nb;
     RouteModel& m = RouteModel::get();
-    m.learn_host(host_bytes.load(), parts, h_us);
+    // host rates from host legs only: in a split the host threads share host memory with
+    // the devices' reads (and leave them a CPU), so their rate there is not the host leg's
+    // the plans compare against (c5's learned cap fell 25 % under the measured host leg
+    // and the c5 batch split where the host alone was faster, profiles/r05_eighth/)
+    if (posted.empty()) m.learn_host(host_bytes.load(), parts, h_us);
     const double fixed_us = kDevBatchCallUs + static_cast<double>(A.plan_len) / kDevChainBytesPerUs;
     for (const DevRun& r : runs) {
         m.learn_link(A.in_place ? Link::kInplace : Link::kPinned, r.bytes, r.busy_us - fixed_us);
