@@ -3502,6 +3502,15 @@ int commit_heights(uint8_t* arena, stormck_dirty_block* blocks, const CommitPlan
     return STORMCK_OK;
 }
 
+// Work queued on `st` has finished (a query when it is idle, which is the common case for
+// storm's commits, else a synchronise): what host threads read next is what it wrote.
+int stream_drained(hipStream_t st) {
+    if (hipStreamQuery(st) == hipSuccess) return STORMCK_OK;
+    (void)hipGetLastError();
+    HIP_TRY(hipStreamSynchronize(st));
+    return STORMCK_OK;
+}
+
 // Host arguments of the batch entry points, checked the same way for every leg.
 int batch_args(const void* base, uint64_t n, const uint64_t* out_or_expected) {
     if (n == 0) return STORMCK_OK;
@@ -3717,7 +3726,10 @@ int stormck_commit(void* arena, stormck_dirty_block* blocks, uint64_t n, uint64_
             total += blocks[i].length;
         if (static_cast<double>(total) / rt.host_thread < kHostOnlyUs) {
             if (leg_used) *leg_used = STORMCK_LEG_HOST;
-            if (registered) HIP_TRY(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
+            if (registered) {
+                rc = stream_drained(static_cast<hipStream_t>(stream));
+                if (rc) return rc;
+            }
             return stormck_commit_host(arena, blocks, n, revision, last_allocated_block, out_checksums, 1);
         }
     }
@@ -3741,7 +3753,10 @@ int stormck_commit(void* arena, stormck_dirty_block* blocks, uint64_t n, uint64_
     }
     // host threads read the arena now: device work the caller queued on `stream` (e.g. a
     // kernel writing blocks into the registered arena) must have landed first
-    if (registered) HIP_TRY(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
+    if (registered) {
+        rc = stream_drained(static_cast<hipStream_t>(stream));
+        if (rc) return rc;
+    }
     if (p.leg == STORMCK_LEG_SPLIT) {
         CommitPlan P;
         rc = commit_plan(blocks, n, revision, last_allocated_block, &P);
