@@ -1,0 +1,99 @@
+// Probe (GPU box): the fixed cost the routed entry points add to storm's smallest calls,
+// in C, without Python: the primitives a routed call runs before it hashes (pointer
+// classification, the host-readability check, the stream query) and the routed call
+// against its host leg on three 32 KiB blocks, pageable and registered.
+//   hipcc -O2 -std=c++17 -Iinclude tools/route_overhead.cpp -Lstorm_amd/lib -lstormck \
+//       -Wl,-rpath,$PWD/storm_amd/lib -o tools/route_overhead
+#include <hip/hip_runtime.h>
+#include <sys/uio.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#include "stormck.h"
+
+static double now_us() {
+    return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// median over 9 rounds of the mean of `reps` calls, in microseconds
+template <class F>
+static double per_call(F f, int reps = 2000) {
+    std::vector<double> r;
+    for (int k = 0; k < 9; ++k) {
+        const double t0 = now_us();
+        for (int i = 0; i < reps; ++i) f();
+        r.push_back((now_us() - t0) / reps);
+    }
+    std::sort(r.begin(), r.end());
+    return r[4];
+}
+
+int main() {
+    if (stormck_init(0) != STORMCK_OK) {
+        std::fprintf(stderr, "init: %s\n", stormck_last_error());
+        return 1;
+    }
+    const uint64_t blk = 32768, n = 3;
+    void* pg = std::aligned_alloc(4096, 1 << 20);
+    void* rg = std::aligned_alloc(4096, 1 << 20);
+    std::fill_n(static_cast<unsigned char*>(pg), 1 << 20, 7);
+    std::fill_n(static_cast<unsigned char*>(rg), 1 << 20, 7);
+    if (stormck_host_register(rg, 1 << 20) != STORMCK_OK) {
+        std::fprintf(stderr, "register: %s\n", stormck_last_error());
+        return 1;
+    }
+    hipStream_t st;
+    (void)hipStreamCreate(&st);
+    hipPointerAttribute_t a;
+    std::printf("hipPointerGetAttributes registered %.3f us\n", per_call([&] { (void)hipPointerGetAttributes(&a, rg); }));
+    std::printf("hipPointerGetAttributes pageable   %.3f us\n", per_call([&] {
+                    if (hipPointerGetAttributes(&a, pg) != hipSuccess) (void)hipGetLastError();
+                }));
+    std::printf("process_vm_readv 2 bytes           %.3f us\n", per_call([&] {
+                    unsigned char got[2];
+                    iovec l = {got, 2};
+                    iovec r[2] = {{pg, 1}, {static_cast<unsigned char*>(pg) + 3 * blk - 1, 1}};
+                    (void)process_vm_readv(getpid(), &l, 1, r, 2, 0);
+                }));
+    std::printf("hipStreamQuery null stream         %.3f us\n", per_call([&] { (void)hipStreamQuery(nullptr); }));
+    std::printf("hipStreamQuery created stream      %.3f us\n", per_call([&] { (void)hipStreamQuery(st); }));
+
+    uint64_t out[n];
+    uint32_t leg = 0;
+    for (void* base : {pg, rg}) {
+        const char* what = base == pg ? "pageable  " : "registered";
+        const double h = per_call([&] { (void)stormck_checksum_host_leg(base, blk, nullptr, blk, n, out, 1); });
+        const double r = per_call([&] { (void)stormck_checksum_batch(base, blk, nullptr, blk, n, out, 0, &leg); });
+        std::printf("batch %s 3 x 32 KiB: host leg %.3f us  routed %.3f us (leg %u)  +%.3f us\n", what, h, r, leg, r - h);
+    }
+    stormck_dirty_block b[n] = {};
+    for (uint64_t i = 0; i < n; ++i) {
+        b[i].data_offset = i * blk;
+        b[i].origin_pointer = STORMCK_NO_ORIGIN;
+        b[i].parent = STORMCK_NO_PARENT;
+        b[i].address = i + 1;
+        b[i].birth_revision = 5;
+        b[i].length = static_cast<uint32_t>(blk);
+        b[i].type = STORMCK_LEAF_BLOCK;
+    }
+    for (void* base : {pg, rg}) {
+        const char* what = base == pg ? "pageable  " : "registered";
+        uint64_t last = 100;
+        const double h = per_call([&] { (void)stormck_commit_host(base, b, n, 9, &last, out, 1); });
+        const double r = per_call([&] { (void)stormck_commit(base, b, n, 9, &last, out, nullptr, 0, &leg); });
+        const double rs = per_call([&] { (void)stormck_commit(base, b, n, 9, &last, out, st, 0, &leg); });
+        std::printf("commit %s 3 x 32 KiB: host %.3f us  routed %.3f us  routed on a stream %.3f us (leg %u)  +%.3f us\n",
+                    what, h, r, rs, leg, r - h);
+    }
+    (void)hipStreamDestroy(st);
+    stormck_host_unregister(rg);
+    std::free(pg);
+    std::free(rg);
+    stormck_shutdown();
+    return 0;
+}
