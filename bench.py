@@ -553,7 +553,9 @@ def batch_e2e_workload(a):
       routed_reg / routed_reg_1   the routed call on registered memory (it may split),
       routed_x2    two callers at once, each routed on its own half of the batch (wall
                    time of both; ADVICE r04: a caller that finds the pool busy plans on its
-                   own thread).
+                   own thread). Batches of 512 MB and more only: below, starting and joining
+                   two Python threads costs more than the call (c5-size pairs are timed in C
+                   by tools/route_overhead.cpp).
     The routed calls use the rates the library measured so far in this process (every leg
     above updates them): `rates` is the model after the row. Batches: storm's c5 commit
     batch (1,200 objectlist leaves + a pointer block + the singularity,
@@ -670,7 +672,7 @@ def batch_e2e_workload(a):
         row = {"batch": name, "blocks": n, "hashed_bytes": hashed}
         shares = {}
         names = ["dev", "host_1", "host_all", "routed", "routed_1", "dev_reg", "split", "split_1", "routed_reg",
-                 "routed_reg_1"] + (["routed_x2"] if n >= 1024 else [])
+                 "routed_reg_1"] + (["routed_x2"] if hashed >= (512 << 20) else [])
         ts = {leg: [] for leg in names}
         for r in range(2 + (reps if hashed < (4 << 30) else 3)):  # 2 warm-up rounds, then timed ones
             # a fresh leg order every round (seeded): each leg follows different legs, so no

@@ -2583,6 +2583,7 @@ constexpr double kSplitChunkUs = 8.0;             // a chunk issued behind one i
 constexpr double kSplitMinClaimBytes = 1 << 20;   // a smaller device claim costs about what it saves
 constexpr double kSplitDmaBytes = 32 << 20;       // strided claims from this size take the copy engine
 constexpr double kSplitGain = 0.95;               // the split is taken only when predicted 5% faster
+constexpr double kSplitGainCached = 0.8;          // ... 20% for a call of at most kHostCacheBytes
 constexpr double kHostOnlyUs = 10.0;              // calls one host thread finishes this fast are not planned
 constexpr double kSplitMinSaveUs = 30.0;          // ... and only when it saves at least this much
 
@@ -3283,15 +3284,22 @@ struct LegPlan {
 
 // The split is taken only when it is predicted to save both kSplitGain of the best single
 // leg and kSplitMinSaveUs: on small calls the devices' part is a few chunks whose start and
-// finish vary by tens of microseconds (profiles/r05_fourth/), more than it could save.
-void pick_leg(LegPlan* p) {
+// finish vary by tens of microseconds (profiles/r05_fourth/), more than it could save. A
+// call of at most kHostCacheBytes needs kSplitGainCached: its host leg runs twice as fast
+// from warm host caches as from cold ones (c5 on the pool: 77 us called back to back,
+// 135-170 us between other work, profiles/r05_learn/), so its learned rate is a blend and
+// the prediction loose, and the device's part gains nothing from the caches. Measured on six
+// boxes, the split never beat the pool by more than 6% at c5 size, and beat one host
+// thread by 1.6-2x.
+void pick_leg(LegPlan* p, double bytes) {
     double best = p->us[0];
     p->leg = STORMCK_LEG_HOST;
     if (p->us[1] < best) {
         best = p->us[1];
         p->leg = STORMCK_LEG_DEVICE;
     }
-    if (p->us[2] < kSplitGain * best && p->us[2] < best - kSplitMinSaveUs) p->leg = STORMCK_LEG_SPLIT;
+    const double gain = bytes <= static_cast<double>(kHostCacheBytes) ? kSplitGainCached : kSplitGain;
+    if (p->us[2] < gain * best && p->us[2] < best - kSplitMinSaveUs) p->leg = STORMCK_LEG_SPLIT;
 }
 
 // Time of a split that hashes `bytes` on host threads at r_h and devices at r_d together,
@@ -3324,7 +3332,7 @@ LegPlan plan_batch(const stormck_route_rates& r, uint64_t n, const BatchShape& s
                                ps > 1 ? kHostLevelUs : 0.0, p.us[0]);
         }
     }
-    pick_leg(&p);
+    pick_leg(&p, bytes);
     return p;
 }
 
@@ -3390,7 +3398,9 @@ LegPlan plan_commit(const stormck_route_rates& r, const CommitShape& s, bool reg
             p.us[2] = p.us[0] - h0 + t0;
         }
     }
-    pick_leg(&p);
+    double total = 0;
+    for (uint64_t b : s.bytes) total += static_cast<double>(b);
+    pick_leg(&p, total);
     return p;
 }
 

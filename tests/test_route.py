@@ -176,6 +176,24 @@ def test_the_start_latency_keeps_short_calls_off_the_split(rates):
     assert leg == _lib.LEG_SPLIT, us
 
 
+def test_cache_sized_calls_split_only_on_a_wide_margin(rates):
+    """A call of at most 64 MiB (storm's c5 commit batch, 38 MB) splits only when predicted
+    20% faster than the best single leg: its host leg's rate swings 2x with the host's
+    caches. A split predicted 17% faster stays on the pool; with one host thread the split
+    is predicted ~2x faster and is taken; the same margin on a 128 MiB batch splits."""
+    c5 = [31808] * 1200 + [30000, 72]
+    rates(device_latency=40.0)
+    leg, us = blocks.PlanBatch(len(c5), 32768, lens=c5, pinned=True)
+    if _pool() > 1:
+        assert 0.8 <= us[2] / us[0] < 0.95 and us[0] - us[2] >= 30, us
+        assert leg == _lib.LEG_HOST, us
+    leg, us = blocks.PlanBatch(len(c5), 32768, lens=c5, pinned=True, host_threads=1)
+    assert leg == _lib.LEG_SPLIT and us[2] < 0.6 * us[0], us
+    leg, us = blocks.PlanBatch(4096, 32768, 32768, pinned=True)
+    if _pool() > 1:
+        assert us[2] < 0.95 * us[0] and leg == _lib.LEG_SPLIT, us
+
+
 def test_a_fast_host_makes_the_split_a_tie_and_keeps_the_host(rates):
     """When the link adds under 5% to the host's rate the split is not taken (no flapping
     between two legs of about the same time)."""

@@ -1,17 +1,20 @@
 // Probe (GPU box): the fixed cost the routed entry points add to storm's smallest calls,
 // in C, without Python: the primitives a routed call runs before it hashes (pointer
 // classification, the host-readability check, the stream query) and the routed call
-// against its host leg on three 32 KiB blocks, pageable and registered.
+// against its host leg on three 32 KiB blocks, pageable and registered; then two callers
+// at once on the halves of a c5-size batch.
 //   hipcc -O2 -std=c++17 -Iinclude tools/route_overhead.cpp -Lstorm_amd/lib -lstormck \
-//       -Wl,-rpath,$PWD/storm_amd/lib -o tools/route_overhead
+//       -Wl,-rpath,'$ORIGIN/../storm_amd/lib' -pthread -o tools/route_overhead
 #include <hip/hip_runtime.h>
 #include <sys/uio.h>
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
+#include <thread>
 #include <vector>
 
 #include "stormck.h"
@@ -89,6 +92,51 @@ int main() {
         const double rs = per_call([&] { (void)stormck_commit(base, b, n, 9, &last, out, st, 0, &leg); });
         std::printf("commit %s 3 x 32 KiB: host %.3f us  routed %.3f us  routed on a stream %.3f us (leg %u)  +%.3f us\n",
                     what, h, r, rs, leg, r - h);
+    }
+    // two callers at once on the halves of a registered c5-size batch (1,202 x 32 KiB
+    // slots), against one call on the whole: threads started beforehand and released
+    // together, so only the library's handling of the second caller is timed
+    {
+        const uint64_t nb = 1202, half = nb / 2;
+        const uint64_t bytes = nb * blk;
+        void* c5 = std::aligned_alloc(4096, bytes);
+        std::fill_n(static_cast<unsigned char*>(c5), bytes, 5);
+        stormck_host_register(c5, bytes);
+        std::vector<uint64_t> o(nb);
+        const double one = per_call([&] { (void)stormck_checksum_batch(c5, blk, nullptr, 31808, nb, o.data(), 0, &leg); }, 50);
+        std::printf("c5-size batch, one caller: %.1f us (leg %u)\n", one, leg);
+        for (int round = 0; round < 3; ++round) {
+            std::atomic<int> go{0}, ready{0};
+            double t_done[2] = {0, 0};
+            uint32_t legs[2] = {0, 0};
+            auto body = [&](int k) {
+                ready.fetch_add(1);
+                while (go.load(std::memory_order_acquire) == 0) {
+                }
+                const uint64_t lo = k ? half : 0, cnt = k ? nb - half : half;
+                (void)stormck_checksum_batch(static_cast<unsigned char*>(c5) + lo * blk, blk, nullptr, 31808, cnt,
+                                             o.data() + lo, 0, &legs[k]);
+                t_done[k] = now_us();
+            };
+            std::vector<double> walls;
+            for (int rep = 0; rep < 20; ++rep) {
+                ready = 0;
+                go = 0;
+                std::thread a(body, 0), b(body, 1);
+                while (ready.load() < 2) {
+                }
+                const double t0 = now_us();
+                go.store(1, std::memory_order_release);
+                a.join();
+                b.join();
+                walls.push_back(std::max(t_done[0], t_done[1]) - t0);
+            }
+            std::sort(walls.begin(), walls.end());
+            std::printf("c5-size batch, two callers on halves: median %.1f us, min %.1f, max %.1f (legs %u %u)\n",
+                        walls[walls.size() / 2], walls.front(), walls.back(), legs[0], legs[1]);
+        }
+        stormck_host_unregister(c5);
+        std::free(c5);
     }
     (void)hipStreamDestroy(st);
     stormck_host_unregister(rg);
