@@ -2657,11 +2657,16 @@ class RouteModel {
     }
     // A split's device part: its first chunk came back `us` after the call posted it, of
     // which `bytes` over the link at the current rate account for `bytes / rate`.
+    // One observation moves the latency up by at most a quarter of itself (plus 25 us): a
+    // spike (the device's first kernel launches in a process loading their code, tens of
+    // ms) would otherwise price the devices out of every later split, and a device that
+    // never gets a chunk is never measured again to correct it.
     void learn_latency(uint64_t bytes, double rate, double us) {
         if (us <= 0 || rate <= 0) return;
-        const double lat = std::max(1.0, us - static_cast<double>(bytes) / rate);
         std::lock_guard<std::mutex> g(mu_);
         if (frozen_) return;
+        const double lat = std::min(std::max(1.0, us - static_cast<double>(bytes) / rate),
+                                    2.0 * r_.device_latency + 100.0);
         r_.device_latency = ewma(r_.device_latency, lat);
         ++r_.observations;
     }
@@ -2956,6 +2961,7 @@ struct DevRun {
     double busy_us = 0;
     double started = 0, first_issue = 0;  // when the worker began, issued its first chunk (now_us clock)
     double first_done = 0;                // when its first chunk came back (0: none)
+    bool cold = false;                    // the device's staging was set up in this call
     double finished = 0;
     uint64_t first_bytes = 0;             // that chunk's bytes
 };
@@ -2981,6 +2987,7 @@ void device_part(const SplitArgs& A, SplitQueue& q, double lat_us, DevRun* r) {
     int rc = get_ctx(&c);
     if (rc) return failed(rc);
     std::lock_guard<std::mutex> g(c->mu);
+    r->cold = !c->ready;
     rc = ensure_ready(c);
     if (rc) return failed(rc);
     const Blocks& B = A.B;
@@ -3233,7 +3240,7 @@ int split_run(SplitArgs& A, const std::vector<int>& devs, unsigned pl, uint64_t 
         // caller holds its results (the caller's own wake-up included when the device
         // finished last), less its bytes over the link; from parts small enough that the
         // link time is a minor, well-estimated share of that
-        if (r.first_done > 0 && r.bytes <= kLatencyProbeBytes) {
+        if (r.first_done > 0 && r.bytes <= kLatencyProbeBytes && !r.cold) {
             const double back = r.finished > h0 + h_us ? t_back : r.finished;
             m.learn_latency(r.bytes, r_dev, back - t_post);
         }

@@ -327,6 +327,29 @@ def test_route_devices_and_rates_learned_on_the_gpu():
         reg.close()
 
 
+def test_split_latency_learning_is_bounded():
+    """A split's device part measures the devices' start latency, and one observation moves
+    it up by at most a quarter of (itself + 100 us): a one-off spike (the process's first
+    kernel launches loading their code) must not price the device out of every later
+    split, since a device that gets no chunk is never measured again."""
+    n, stride = 512, 32768  # 16 MiB: first chunks within the latency probe's size
+    reg = _filled(n, stride, 11)
+    want = o.checksum_batch(reg.a, n, stride, stride)
+    try:
+        blocks.SetRouteRates(dict(SLOW_HOST, device_latency=10.0))  # learning
+        lat = 10.0
+        for _ in range(3):
+            got, done = blocks.ChecksumBatchSplit(reg.a, n, stride)
+            assert np.array_equal(got, want)
+            assert done > 0
+            r = blocks.RouteRates()
+            assert 1.0 <= r["device_latency"] <= lat + 0.25 * (lat + 100.0) + 1e-6, (lat, r)
+            lat = r["device_latency"]
+    finally:
+        blocks.SetRouteRates(None)
+        reg.close()
+
+
 def test_stream_forget():
     s = torch.cuda.Stream()
     n, stride = 1024, 32768  # a ring-eligible batch (k_xxh64_wide_multi)

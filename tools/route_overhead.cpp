@@ -135,6 +135,55 @@ int main() {
             std::printf("c5-size batch, two callers on halves: median %.1f us, min %.1f, max %.1f (legs %u %u)\n",
                         walls[walls.size() / 2], walls.front(), walls.back(), legs[0], legs[1]);
         }
+        // the same slots as one height of a commit with one host thread: the routed commit
+        // (which picks the split) against the split called directly, alternating
+        std::vector<stormck_dirty_block> fb(nb);
+        for (uint64_t i = 0; i < nb; ++i) {
+            fb[i] = {};
+            fb[i].data_offset = i * blk;
+            fb[i].origin_pointer = STORMCK_NO_ORIGIN;
+            fb[i].parent = STORMCK_NO_PARENT;
+            fb[i].address = i + 1;
+            fb[i].birth_revision = 5;
+            fb[i].length = 31808;
+            fb[i].type = STORMCK_LEAF_BLOCK;
+        }
+        std::vector<double> t_routed, t_split;
+        uint64_t last = 1u << 20, done = 0;
+        auto show = [&](const char* when) {
+            stormck_route_rates rr;
+            stormck_route_get_rates(&rr);
+            uint32_t pleg = 0;
+            double us[3];
+            stormck_route_plan_commit(fb.data(), nb, STORMCK_MEM_PINNED, 1, 1, &pleg, us);
+            std::printf("%s: rates thread %.0f memory %.0f cached %.0f inplace %.0f latency %.1f; plan leg %u: "
+                        "host %.1f device %.1f split %.1f us\n",
+                        when, rr.host_thread, rr.host_memory, rr.host_cached, rr.link_inplace, rr.device_latency,
+                        pleg, us[0], us[1], us[2]);
+        };
+        show("before");
+        for (int rep = 0; rep < 61; ++rep) {
+            double t0 = now_us();
+            (void)stormck_commit(c5, fb.data(), nb, 9, &last, o.data(), nullptr, 1, &leg);
+            const double r = now_us() - t0;
+            t0 = now_us();
+            (void)stormck_commit_split(c5, fb.data(), nb, 9, &last, o.data(), nullptr, 0, 1, STORMCK_SPLIT_BALANCED,
+                                       &done);
+            const double s = now_us() - t0;
+            if (rep) {
+                t_routed.push_back(r);
+                t_split.push_back(s);
+            }
+            if (rep < 3) {
+                std::printf("rep %d: routed %.1f us (leg %u), split %.1f us (device %llu leaves)\n", rep, r, leg, s,
+                            static_cast<unsigned long long>(done));
+                show("after");
+            }
+        }
+        std::sort(t_routed.begin(), t_routed.end());
+        std::sort(t_split.begin(), t_split.end());
+        std::printf("c5-size commit, 1 host thread: routed %.1f us (leg %u)  split %.1f us (device %llu leaves)\n",
+                    t_routed[30], leg, t_split[30], static_cast<unsigned long long>(done));
         stormck_host_unregister(c5);
         std::free(c5);
     }
