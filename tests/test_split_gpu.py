@@ -339,7 +339,7 @@ def test_split_latency_learning_is_bounded():
         blocks.SetRouteRates(dict(SLOW_HOST, device_latency=10.0))  # learning
         lat = 10.0
         for _ in range(3):
-            got, done = blocks.ChecksumBatchSplit(reg.a, n, stride)
+            got, done = blocks.ChecksumBatchSplit(reg.a, n, stride, stride)
             assert np.array_equal(got, want)
             assert done > 0
             r = blocks.RouteRates()
