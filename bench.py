@@ -497,7 +497,11 @@ def commit_e2e_workload(a):
         shares = {}
         names = ("dev_inplace", "dev_hbm", "host_1", "host_all", "split", "split_1", "routed", "routed_1")
         ts = {leg: [] for leg in names}
-        for r in range(2 + (reps if bytes_hashed < (1 << 30) else 3)):  # 2 warm-up rounds, interleaved legs
+        # 2 warm-up rounds, then timed ones, interleaved legs; calls of at most 64 MiB get 3x
+        # the rounds: each leg's median then spans enough predecessor orders that none of
+        # them (a device left idle and clocked down by a long host leg, say) sets it
+        rounds = 3 * reps if bytes_hashed <= (64 << 20) else (reps if bytes_hashed < (1 << 30) else 3)
+        for r in range(2 + rounds):
             for leg in random.Random(r).sample(names, len(names)):  # a fresh (seeded) order every round
                 dt, out = run(leg)
                 if r >= 2:
@@ -674,7 +678,10 @@ def batch_e2e_workload(a):
         names = ["dev", "host_1", "host_all", "routed", "routed_1", "dev_reg", "split", "split_1", "routed_reg",
                  "routed_reg_1"] + (["routed_x2"] if hashed >= (512 << 20) else [])
         ts = {leg: [] for leg in names}
-        for r in range(2 + (reps if hashed < (4 << 30) else 3)):  # 2 warm-up rounds, then timed ones
+        # 2 warm-up rounds, then timed ones (3x the rounds for calls of at most 64 MiB, as in
+        # commit_e2e)
+        rounds = 3 * reps if hashed <= (64 << 20) else (reps if hashed < (4 << 30) else 3)
+        for r in range(2 + rounds):
             # a fresh leg order every round (seeded): each leg follows different legs, so no
             # leg inherits one predecessor's cache and device state every time
             for leg in random.Random(r).sample(names, len(names)):

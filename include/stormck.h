@@ -193,7 +193,10 @@ int stormck_verify_host_leg(const void* base, uint64_t stride, const uint32_t* l
 uint64_t stormck_xxh64(const void* p, uint64_t n_bytes);
 int stormck_checksum(const void* p, uint64_t n_bytes, uint64_t* out);
 int stormck_checksum_gpu(const void* p, uint64_t n_bytes, uint64_t* out);
-/* Page-lock a host range so the host path can DMA from it without staging copies. */
+/* Page-lock and map a host range (for every device) so the device and split legs DMA it or
+ * read it in place, without staging copies. Also sets up the calling thread's current
+ * device's staging for those legs (once per process), so the first routed call that uses
+ * the device does not pay for it. */
 int stormck_host_register(void* p, uint64_t bytes);
 int stormck_host_unregister(void* p);
 /* Device-visible address of host memory registered with stormck_host_register: the

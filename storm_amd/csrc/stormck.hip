@@ -1753,6 +1753,15 @@ int stormck_host_register(void* p, uint64_t bytes) {
     // portable: pinned for every device of the process (stormck_checksum_host_multi DMAs
     // ranges of one registered buffer to several devices)
     HIP_TRY(hipHostRegister(p, bytes, hipHostRegisterMapped | hipHostRegisterPortable));
+    // registered memory is what the device and split legs read: set up the current device's
+    // stages now (pinned and device buffers, ~0.3 s once per process) rather than inside the
+    // first routed call that splits (storm registers cache.data once, at start-up). Best
+    // effort: a failure here is the first device call's to report.
+    DeviceCtx* c = nullptr;
+    if (get_ctx(&c) == STORMCK_OK) {
+        std::lock_guard<std::mutex> g(c->mu);
+        (void)ensure_ready(c);
+    }
     return STORMCK_OK;
 }
 
