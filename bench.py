@@ -551,6 +551,8 @@ def batch_e2e_workload(a):
     then on the same memory registered with stormck_host_register (as the Go binding's
     cache.data):
       dev_reg      the device pipeline, DMA in place,
+      host_1_reg / host_all_reg   the host leg on the registered copy (the legs the routed
+                   and split calls on registered memory are compared with),
       split        stormck_checksum_split, balanced: the pool from the front and the device
                    from the back at once (split_dev_share = the device's blocks / n),
       split_1      the same with one host thread,
@@ -625,8 +627,8 @@ def batch_e2e_workload(a):
             if leg in ("dev", "dev_reg"):
                 def f():
                     return L.stormck_checksum_host(bp, stride, lp, ln, n, op)
-            elif leg in ("host_1", "host_all"):
-                nt = 1 if leg == "host_1" else threads
+            elif leg in ("host_1", "host_all", "host_1_reg", "host_all_reg"):
+                nt = 1 if leg.startswith("host_1") else threads
 
                 def f():
                     return L.stormck_checksum_host_leg(bp, stride, lp, ln, n, op, nt)
@@ -675,7 +677,8 @@ def batch_e2e_workload(a):
 
         row = {"batch": name, "blocks": n, "hashed_bytes": hashed}
         shares = {}
-        names = ["dev", "host_1", "host_all", "routed", "routed_1", "dev_reg", "split", "split_1", "routed_reg",
+        names = ["dev", "host_1", "host_all", "routed", "routed_1", "dev_reg", "host_1_reg", "host_all_reg", "split",
+                 "split_1", "routed_reg",
                  "routed_reg_1"] + (["routed_x2"] if hashed >= (512 << 20) else [])
         ts = {leg: [] for leg in names}
         # 2 warm-up rounds, then timed ones (3x the rounds for calls of at most 64 MiB, as in
@@ -704,9 +707,9 @@ def batch_e2e_workload(a):
             return min(row[k + "_us"] for k in ks)
         row["routed_over_best"] = round(row["routed_us"] / best("host_all", "dev"), 3)
         row["routed_1_over_best"] = round(row["routed_1_us"] / best("host_1", "dev"), 3)
-        row["routed_reg_over_best"] = round(row["routed_reg_us"] / best("host_all", "dev_reg", "split"), 3)
-        row["routed_reg_1_over_best"] = round(row["routed_reg_1_us"] / best("host_1", "dev_reg", "split_1"), 3)
-        row["split_gain"] = round(best("host_all", "dev_reg") / row["split_us"], 3)
+        row["routed_reg_over_best"] = round(row["routed_reg_us"] / best("host_all_reg", "dev_reg", "split"), 3)
+        row["routed_reg_1_over_best"] = round(row["routed_reg_1_us"] / best("host_1_reg", "dev_reg", "split_1"), 3)
+        row["split_gain"] = round(best("host_all_reg", "dev_reg") / row["split_us"], 3)
         row["rates"] = {k: round(v, 1) for k, v in blocks.RouteRates().items()}
         row["agree"] = all(np.array_equal(outs["host_1"], outs[k]) for k in outs)
         rows.append(row)

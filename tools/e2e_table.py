@@ -6,7 +6,8 @@ import json
 import sys
 
 BATCH = [("dev", "device, pageable"), ("dev_reg", "device, registered"), ("host_1", "host, 1 thread"),
-         ("host_all", "host, 16 threads"), ("split", "split"), ("split_1", "split, 1 host thread"),
+         ("host_all", "host, 16 threads"), ("host_1_reg", "host, 1 thread, registered"),
+         ("host_all_reg", "host, 16 threads, registered"), ("split", "split"), ("split_1", "split, 1 host thread"),
          ("routed_reg", "routed (leg)"), ("routed_reg_1", "routed, 1 thread (leg)")]
 COMMIT = [("dev_inplace", "device in place"), ("dev_hbm", "device, HBM arena"), ("host_1", "host, 1 thread"),
           ("host_all", "host, 16 threads"), ("split", "split"), ("split_1", "split, 1 host thread"),
@@ -39,6 +40,9 @@ def table(path):
             first = False
         cells = []
         for k, _ in cols:
+            if k + "_us" not in d:  # sessions before the column existed
+                cells.append("–")
+                continue
             v = fmt(d[k + "_us"])
             if k.startswith("routed"):
                 v += f" ({d.get(k + '_leg')})"
