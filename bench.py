@@ -27,7 +27,6 @@ from __future__ import annotations
 import argparse
 import json
 import os
-import random
 import sys
 import time
 
@@ -388,6 +387,24 @@ def c5_workload(a):
     return rc
 
 
+def balanced_orders(names):
+    """Orders of the legs in which each leg follows every other leg equally often (a Williams
+    design: len(names) orders for an even count, twice that for an odd one, each leg once
+    per order)."""
+    n = len(names)
+    first, lo, hi = [0], 1, n - 1
+    while len(first) < n:
+        first.append(lo)
+        lo += 1
+        if len(first) < n:
+            first.append(hi)
+            hi -= 1
+    rows = [[(x + i) % n for x in first] for i in range(n)]
+    if n % 2:
+        rows += [list(reversed(r)) for r in rows]
+    return [[names[k] for k in r] for r in rows]
+
+
 def commit_e2e_workload(a):
     """f1 end to end from host memory, in the Go binding's configuration: storm's
     cache.data as page-aligned registered host memory (integration/go/cache/
@@ -497,12 +514,14 @@ def commit_e2e_workload(a):
         shares = {}
         names = ("dev_inplace", "dev_hbm", "host_1", "host_all", "split", "split_1", "routed", "routed_1")
         ts = {leg: [] for leg in names}
-        # 2 warm-up rounds, then timed ones, interleaved legs; calls of at most 64 MiB get 3x
-        # the rounds: each leg's median then spans enough predecessor orders that none of
-        # them (a device left idle and clocked down by a long host leg, say) sets it
-        rounds = 3 * reps if bytes_hashed <= (64 << 20) else (reps if bytes_hashed < (1 << 30) else 3)
+        # 2 warm-up rounds, then timed ones, the legs interleaved in balanced orders (each leg
+        # follows every other leg equally often: a leg's time depends on its predecessor,
+        # e.g. a device left idle by a long host leg starts slower); calls of at most 64 MiB
+        # run a whole cycle of the orders
+        rounds = len(names) if bytes_hashed <= (64 << 20) else (reps if bytes_hashed < (1 << 30) else 3)
+        orders = balanced_orders(names)
         for r in range(2 + rounds):
-            for leg in random.Random(r).sample(names, len(names)):  # a fresh (seeded) order every round
+            for leg in orders[r % len(orders)]:
                 dt, out = run(leg)
                 if r >= 2:
                     ts[leg].append(dt)
@@ -681,13 +700,11 @@ def batch_e2e_workload(a):
                  "split_1", "routed_reg",
                  "routed_reg_1"] + (["routed_x2"] if hashed >= (512 << 20) else [])
         ts = {leg: [] for leg in names}
-        # 2 warm-up rounds, then timed ones (3x the rounds for calls of at most 64 MiB, as in
-        # commit_e2e)
-        rounds = 3 * reps if hashed <= (64 << 20) else (reps if hashed < (4 << 30) else 3)
+        # 2 warm-up rounds, then timed ones in balanced orders, as in commit_e2e
+        rounds = len(names) if hashed <= (64 << 20) else (reps if hashed < (4 << 30) else 3)
+        orders = balanced_orders(names)
         for r in range(2 + rounds):
-            # a fresh leg order every round (seeded): each leg follows different legs, so no
-            # leg inherits one predecessor's cache and device state every time
-            for leg in random.Random(r).sample(names, len(names)):
+            for leg in orders[r % len(orders)]:
                 dt, out = run(leg)
                 if r >= 2:
                     ts[leg].append(dt)
