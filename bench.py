@@ -1175,7 +1175,7 @@ def block_checksum_workload(a) -> int:
                                            "profile_frac", "profile_timed_launches", "bench_under_rocprof",
                                            "traffic_over_algorithmic", "placement_spread")}
 
-    # The frac depends on where the arena lands in HBM (0.85-0.89 across fresh processes;
+    # The frac depends on where the arena lands in HBM (0.84-0.89 across fresh processes;
     # neither VMM placement collapses the spread, DESIGN_LOG.md §10.1): report this line's frac
     # beside the committed session's placement spread, the spread widened to include it.
     placement = None
