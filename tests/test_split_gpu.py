@@ -125,6 +125,30 @@ def test_split_short_test_tag_blocks():
         reg.close()
 
 
+@pytest.mark.parametrize("n", [1, 2, 3, 37])
+def test_split_edge_shapes(n):
+    """Ragged edges of a split: 1-3 blocks with every boundary, empty and sub-stripe blocks
+    (0, 1, 7, 31 and 33 bytes beside storm's lengths), a base 8 bytes past a page (rows
+    not 16-byte aligned), the device reading in place. Exact against the oracle."""
+    stride = 4096
+    reg = Registered(n * stride + 4096)
+    try:
+        reg.a[:] = np.random.default_rng(n).integers(0, 256, size=reg.a.size, dtype=np.uint8)
+        view = reg.a[8:8 + n * stride]
+        lens = np.array([[0, 1, 7, 31, 33, 4088, 2048][i % 7] for i in range(n)], dtype=np.uint32)
+        want = o.checksum_batch(view, n, stride, lens=lens)
+        assert int(want[0]) == 0xEF46DB3751D8E999  # XXH64 of no bytes
+        for d in sorted({0, 1, n // 2, n - 1, n}):
+            got, done = blocks.ChecksumBatchSplit(view, n, stride, lens=lens, device_blocks=d)
+            assert done == d and np.array_equal(got, want), (n, d)
+            bad = want.copy()
+            bad[n - 1] ^= 1
+            fb, nb, done = blocks.VerifyChecksumBatchSplit(view, n, stride, bad, lens=lens, device_blocks=d)
+            assert (fb, nb, done) == (n - 1, 1, d), (n, d)
+    finally:
+        reg.close()
+
+
 def test_split_verify_mismatches_on_each_side_of_the_boundary():
     n, stride, d = 3000, 32768, 1000
     edge = n - d  # host: [0, edge), device: [edge, n)
@@ -232,6 +256,21 @@ def test_commit_split_fixed_matches_storm_loop(device_leaves):
         assert done == device_leaves
         assert np.array_equal(cs, ref_cs) and last2 == ref_last and np.array_equal(b, ref_b)
         assert np.array_equal(reg.a, ref_arena)  # every Pointer and type stored into its parent
+    finally:
+        reg.close()
+
+
+@pytest.mark.parametrize("n_leaves,device_leaves", [(1, 0), (1, 1), (2, 1), (2, 2), (1201, 1201)])
+def test_commit_split_tiny_and_two_node_forests(n_leaves, device_leaves):
+    """The smallest forests (one leaf alone; two leaves under a pointer block) with the
+    boundary at each place, and 1,201 leaves (two pointer blocks and their root) all on the
+    device."""
+    b, reg, last, (ref_cs, ref_b, ref_last, ref_arena) = _commit_case(n_leaves, 100 + n_leaves + device_leaves)
+    try:
+        cs, last2, done = sc.commit_split(reg.a, b, 9, last, devices=[0], device_leaves=device_leaves)
+        assert done == device_leaves
+        assert np.array_equal(cs, ref_cs) and last2 == ref_last and np.array_equal(b, ref_b)
+        assert np.array_equal(reg.a, ref_arena)
     finally:
         reg.close()
 
