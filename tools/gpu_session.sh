@@ -13,6 +13,8 @@
 #   bench                  the default bench line (c3, BASELINE metric)
 #   batch_e2e commit_e2e gather c5 commit keytags
 #                          bench.py --workload <step> --steps 7
+#   placement              8 fresh plain c3 processes (bench.py --steps 5 --no-cpu): the spread
+#                          of the line's frac with where each arena lands in HBM
 #   prof                   tools/profile.sh <tag>: fresh plain c3 processes, the bench under
 #                          rocprofv3 --kernel-trace --stats, separate FETCH_SIZE / WRITE_SIZE
 #                          passes and their calibration, the gather workload likewise
@@ -44,6 +46,12 @@ for step in "$@"; do
         batch_e2e|commit_e2e|gather|c5|commit|keytags)
             timeout -k 10 900 python bench.py --workload "$step" --steps 7 > "$out/$step.log" 2>&1; rc=$?
             tail -c 300 "$out/$step.log"; echo ;;
+        placement)
+            rc=0
+            for i in 1 2 3 4 5 6 7 8; do
+                timeout -k 10 300 python bench.py --steps 5 --warmup 1 --no-cpu > "$out/placement_$i.log" 2>&1 || { rc=$?; break; }
+                python tools/placement_summary.py "$out/placement_$i.log" | tee -a "$out/placement.jsonl"
+            done ;;
         prof)
             timeout -k 10 1100 bash tools/profile.sh "$tag" > "$out/prof.log" 2>&1; rc=$?
             tail -3 "$out/prof.log" ;;
