@@ -427,8 +427,9 @@ def commit_e2e_workload(a):
     commit (2 leaves + their pointer block), a `-tags test` forest (100 leaves of 536 /
     728 B under fan-out-10 pointer blocks of 256 B, storm_test.go:131-138), and larger
     forests of 16K and 128K leaves. Every leg's checksums must agree. One line per run
-    with a table: median us per commit over --steps rounds, every leg once per round in a
-    fresh seeded order."""
+    with a table: median us per commit, every leg once per round in balanced orders (each
+    leg follows every other equally often; a whole cycle of orders for forests of at most
+    64 MiB, --steps rounds up to 1 GiB, 3 above), calls under 1 MiB as the mean of 200."""
     import ctypes
     import numpy as np
     import torch
@@ -587,10 +588,11 @@ def batch_e2e_workload(a):
     keystore/benchmark_test.go:58-62), the c1 batch (1K x 32 KiB), 3 blocks, a `-tags test`
     batch (100 blocks of 536 / 728 B, storm_test.go:131-138), 16K and 256K blocks of 32 KiB
     (512 MiB, 8 GiB). Every leg's checksums must agree. One line per batch with the table:
-    median us per call over --steps rounds, every leg once per round in a fresh seeded order
-    (no leg always inherits the same predecessor's cache state); routed_over_best = routed /
-    the best of
-    host_all, dev, dev_reg, split on the same memory kind (1 thread: host_1, dev, split_1)."""
+    median us per call, every leg once per round in balanced orders (each leg follows every
+    other equally often; a whole cycle of orders for batches of at most 64 MiB, --steps
+    rounds up to 4 GiB, 3 above), calls under 1 MiB as the mean of 200; routed_over_best =
+    routed / the best of host_all and dev (pageable memory); routed_reg_over_best = routed_reg
+    / the best of host_all_reg, dev_reg and split (registered; 1 thread: the _1 legs)."""
     import ctypes
     import numpy as np
     import torch
