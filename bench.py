@@ -11,7 +11,7 @@ Workloads:
          shards (strong scaling; 8M per GPU at N = 8), RCCL all-gather of the
          shard roots.
 A shard exceeds one MI355X's 288 GB of HBM, so its blocks stream through a
-resident 4M-block (128 GiB) arena; before each pass the on-device generator
+resident 2M-block (64 GiB) arena; before each pass the on-device generator
 writes that pass's own logical blocks. The regeneration has its
 own HIP events and is taken out of the step time, so `value` covers the hash
 launches, the Merkle tree and the gather. Every block hashed is distinct, and the
@@ -55,7 +55,10 @@ def parse():
     p.add_argument("--blocks", type=int, default=0,
                    help="blocks per GPU per step (weak scaling); default: c3 (16M) at N = 1, c4 (64M total) at N > 1")
     p.add_argument("--total-blocks", type=int, default=0, help="blocks over all GPUs per step (strong scaling)")
-    p.add_argument("--arena", type=int, default=4 << 20, help="resident arena (blocks)")
+    # 2M blocks (64 GiB, 8 passes for c3): every fresh process lands at 0.892-0.893 of peak;
+    # a 4M-block (128 GiB) arena ran 0.849-0.902 by where it landed in HBM, alternating
+    # between processes (profiles/r05_placement/ against r05_arena64/)
+    p.add_argument("--arena", type=int, default=2 << 20, help="resident arena (blocks)")
     p.add_argument("--alloc", default="plain", choices=sorted(ALLOC_MODES),
                    help="arena placement: plain = hipMalloc (stormck_device_alloc); with the probe build "
                         "(STORMCK_LIBRARY=tools/libstormck_probes.so) also vmm = a 1 GiB-aligned "

@@ -10,7 +10,7 @@ From gpurun_out/prof_<tag>/:
   gather_{trace,fetch,write}/...     -> gather_*.csv, gather_traffic.json (the gather
                                         workload: hash kernel + locality-order kernels)
 
-traffic.json (per launch of the dominant kernel, one 4M-block arena pass):
+traffic.json (per launch of the dominant kernel, one 2M-block arena pass):
   hbm_bytes_per_launch = FETCH_SIZE x 1024 x correction + WRITE_SIZE x 1024, where the
   gfx950 FETCH_SIZE correction is calibrated on a read-peak kernel of known byte count
   (MI355X_MICROARCH.md, HBM / rocprofv3 section: FETCH_SIZE counts half of a wide
@@ -183,4 +183,4 @@ def gather(src, dst, corr):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 4 << 20)
+    main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 2 << 20)

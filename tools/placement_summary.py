@@ -25,6 +25,6 @@ if len(sys.argv) > 2:
         if "k_xxh64_glds_skew" in row["Name"] and "true" in row["Name"].split(",")[5]:
             avg = float(row["AverageNs"]) * 1e-6
             out["prof_avg_ms"] = round(avg, 4)
-            out["prof_frac"] = round(4194304 * 32776 / (avg * 1e-3) / 8e12, 4)
+            out["prof_frac"] = round(d["config"]["arena_blocks"] * 32776 / (avg * 1e-3) / 8e12, 4)
             out["prof_calls"] = int(row["Calls"])
 print(json.dumps(out))
