@@ -55,9 +55,9 @@ def parse():
     p.add_argument("--blocks", type=int, default=0,
                    help="blocks per GPU per step (weak scaling); default: c3 (16M) at N = 1, c4 (64M total) at N > 1")
     p.add_argument("--total-blocks", type=int, default=0, help="blocks over all GPUs per step (strong scaling)")
-    # 2M blocks (64 GiB, 8 passes for c3): every fresh process lands at 0.892-0.893 of peak;
-    # a 4M-block (128 GiB) arena ran 0.849-0.902 by where it landed in HBM, alternating
-    # between processes (profiles/r05_placement/ against r05_arena64/)
+    # 2M blocks (64 GiB, 8 passes for c3): 0.868-0.896 of peak over 24 fresh processes,
+    # median 0.893; a 4M-block (128 GiB) arena ran 0.838-0.902, median 0.876, by where it
+    # landed in HBM
     p.add_argument("--arena", type=int, default=2 << 20, help="resident arena (blocks)")
     p.add_argument("--alloc", default="plain", choices=sorted(ALLOC_MODES),
                    help="arena placement: plain = hipMalloc (stormck_device_alloc); with the probe build "
