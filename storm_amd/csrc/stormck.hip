@@ -875,7 +875,13 @@ int launch_checksum(const uint8_t* base, uint64_t stride, const uint32_t* lens, 
         if (wgs > 0x7fffffffULL) return fail(STORMCK_EINVAL, "batch too large for one launch");
         const uint64_t cus = cu_count();
         const uint64_t steps_per_wg = (wgs + cus - 1) / cus * ((len / 32) / kTileStripes);
-        if (cus > 0 && wgs >= cus && steps_per_wg >= kSkewMinSteps) {
+        // probe knob STORMCK_SKEW_MIN_STEPS: the skewed kernel's threshold (A/B of the two
+        // kernels at the c3 arena's 2M-block launches)
+        static const uint64_t skew_min = [] {
+            const char* e = STORMCK_KNOB("STORMCK_SKEW_MIN_STEPS");
+            return e ? std::strtoull(e, nullptr, 10) : kSkewMinSteps;
+        }();
+        if (cus > 0 && wgs >= cus && steps_per_wg >= skew_min) {
             // large batch: persistent workgroups, one per CU, waves' streams 4 KiB apart
 #define STORMCK_SKEW(VER)                                                                                        \
     hipLaunchKernelGGL((k_xxh64_glds_skew<kTileStripes, kAuxNT, VER, kGldsWaves, kSkewTiles>),                 \
