@@ -3,7 +3,7 @@
 c4 is 64M x 32 KiB blocks sharded 8M per GPU over 8 GPUs, with the shard roots
 gathered and combined. Its arithmetic does not depend on which GPU a shard runs on,
 so this test runs the 8 shards one after another on one GPU, exactly as each rank of
-bench.py would: the shard streams through a 4M-block arena (2 passes, the arena
+bench.py would: the shard streams through a 2M-block arena (4 passes, the arena
 regenerated with the pass's own logical blocks), the shard tree is built on the
 device (k_pointer_level*), and the 8 roots are combined on the device
 (k_pointer_node). Checked against tests/golden/c3c4_roots.json, computed with
@@ -44,7 +44,7 @@ def c4_checksums(dev):
     from storm_amd import dist as sdist
     from storm_amd import engine
     fx = load_golden("c3c4_roots.json")
-    n_total, world, arena_n = fx["c4"]["n_total"], 8, 4 << 20
+    n_total, world, arena_n = fx["c4"]["n_total"], 8, 2 << 20  # bench.py --arena default
     arena = torch.empty((arena_n, BLOCK), dtype=torch.uint8, device=dev)
     cs = torch.empty(n_total, dtype=torch.int64, device=dev)
     for r in range(world):
