@@ -149,6 +149,40 @@ def test_split_edge_shapes(n):
         reg.close()
 
 
+@pytest.mark.parametrize("seed", range(16))
+def test_split_fuzz(seed):
+    """Random splits against the oracle: block count, stride, per-block or uniform lengths
+    (storm's and `-tags test` sizes, empty and sub-stripe ones), base offset, host threads,
+    a fixed or balanced device share, and planted mismatches anywhere (verify: the lowest
+    index and the count over both sides)."""
+    rng = np.random.default_rng(1000 + seed)
+    stride = int(rng.choice([1024, 4096, 32768]))
+    n = int(rng.integers(1, 3000 if stride == 32768 else 9000))
+    shift = int(rng.choice([0, 8, 16, 64]))
+    reg = Registered(n * stride + 4096)
+    try:
+        reg.a[:] = rng.integers(0, 256, size=reg.a.size, dtype=np.uint8)
+        view = reg.a[shift:shift + n * stride]
+        pool = [x for x in STORM_LENS + [0, 1, 31, 256, 536, 728] if x <= stride]
+        lens = rng.choice(pool, size=n).astype(np.uint32) if rng.random() < 0.7 else None
+        length = None if lens is not None else int(rng.choice([x for x in pool if x > 0]))
+        want = o.checksum_batch(view, n, stride, length or 0, lens=lens)
+        d = None if rng.random() < 0.4 else int(rng.integers(0, n + 1))
+        threads = int(rng.choice([0, 1, 3]))
+        got, done = blocks.ChecksumBatchSplit(view, n, stride, length, lens=lens, host_threads=threads,
+                                              device_blocks=d)
+        assert np.array_equal(got, want) and (d is None or done == d) and done <= n, (seed, n, d)
+        bad = want.copy()
+        planted = sorted(set(int(i) for i in rng.integers(0, n, size=int(rng.integers(0, 5)))))
+        for i in planted:
+            bad[i] ^= 1 << int(rng.integers(0, 64))
+        fb, nb, done = blocks.VerifyChecksumBatchSplit(view, n, stride, bad, length, lens=lens,
+                                                       host_threads=threads, device_blocks=d)
+        assert (fb, nb) == ((planted[0], len(planted)) if planted else (n, 0)), (seed, planted, fb, nb)
+    finally:
+        reg.close()
+
+
 def test_split_verify_mismatches_on_each_side_of_the_boundary():
     n, stride, d = 3000, 32768, 1000
     edge = n - d  # host: [0, edge), device: [edge, n)
