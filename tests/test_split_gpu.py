@@ -311,6 +311,26 @@ def test_commit_split_tiny_and_two_node_forests(n_leaves, device_leaves):
         reg.close()
 
 
+@pytest.mark.parametrize("seed", range(8))
+def test_commit_split_fuzz(seed):
+    """Random forests through the split commit against storm's loop (the oracle): leaf
+    count, fan-out (deeper trees at small fan-outs), relocations, record order, host
+    threads, and a fixed or balanced leaf share."""
+    rng = np.random.default_rng(2000 + seed)
+    n_leaves = int(rng.integers(1, 5000))
+    fanout = int(rng.choice([10, 100, 1200]))
+    b, reg, last, (ref_cs, ref_b, ref_last, ref_arena) = _commit_case(n_leaves, 3000 + seed, fanout=fanout)
+    try:
+        d = None if rng.random() < 0.4 else int(rng.integers(0, n_leaves + 1))
+        threads = int(rng.choice([0, 1, 3]))
+        cs, last2, done = sc.commit_split(reg.a, b, 9, last, host_threads=threads, device_leaves=d)
+        assert d is None or done == d
+        assert np.array_equal(cs, ref_cs) and last2 == ref_last and np.array_equal(b, ref_b), (seed, n_leaves, d)
+        assert np.array_equal(reg.a, ref_arena)
+    finally:
+        reg.close()
+
+
 def test_routed_commit_takes_the_split_and_matches():
     b, reg, last, (ref_cs, ref_b, ref_last, ref_arena) = _commit_case(6000, 77)
     try:
