@@ -331,6 +331,43 @@ def test_commit_split_fuzz(seed):
         reg.close()
 
 
+@pytest.mark.parametrize("seed", range(8))
+def test_routed_fuzz(seed):
+    """The routed batch, verify and commit on random shapes under rates that force each
+    leg (a slow host: device or split; a slow link: host; the measured priors: any):
+    always exact, whichever leg runs."""
+    rng = np.random.default_rng(4000 + seed)
+    rates = [SLOW_HOST, SLOW_LINK, None][seed % 3]
+    n, stride = int(rng.integers(1, 6000)), 32768
+    lens = rng.choice(STORM_LENS, size=n).astype(np.uint32)
+    reg = _filled(n, stride, 5000 + seed)
+    try:
+        blocks.SetRouteRates(rates, freeze=rates is not None)
+        want = o.checksum_batch(reg.a, n, stride, lens=lens, threads=8)
+        got, leg = blocks.ChecksumBatchLeg(reg.a, n, stride, lens=lens, host_threads=int(rng.choice([0, 1])))
+        assert np.array_equal(got, want) and leg in (_lib.LEG_HOST, _lib.LEG_DEVICE, _lib.LEG_SPLIT)
+        if rates is SLOW_LINK:
+            assert leg == _lib.LEG_HOST
+        bad = want.copy()
+        k = int(rng.integers(0, n))
+        bad[k] ^= 2
+        fb, nb, leg = blocks.VerifyChecksumBatchLeg(reg.a, n, stride, bad, lens=lens)
+        assert (fb, nb) == (k, 1), (seed, k, fb, nb, leg)
+    finally:
+        blocks.SetRouteRates(None)
+        reg.close()
+    b, reg, last, (ref_cs, ref_b, ref_last, ref_arena) = _commit_case(int(rng.integers(1, 4000)), 6000 + seed)
+    try:
+        blocks.SetRouteRates(rates, freeze=rates is not None)
+        cs, last2, leg = sc.commit(reg.a.ctypes.data, b, 9, last, host_threads=int(rng.choice([0, 1])))
+        assert leg in (_lib.LEG_HOST, _lib.LEG_DEVICE, _lib.LEG_SPLIT)
+        assert np.array_equal(cs, ref_cs) and last2 == ref_last and np.array_equal(b, ref_b), (seed, leg)
+        assert np.array_equal(reg.a, ref_arena)
+    finally:
+        blocks.SetRouteRates(None)
+        reg.close()
+
+
 def test_routed_commit_takes_the_split_and_matches():
     b, reg, last, (ref_cs, ref_b, ref_last, ref_arena) = _commit_case(6000, 77)
     try:
