@@ -8,8 +8,10 @@ back (include/stormck.h, "routing of host-memory work"). Bit-exact against the C
 commit loop, cache/cache.go:87-137 + trace.go:274-320):
   * fixed boundaries, from all-host to all-device, on strided, per-block-length and short
     (`-tags test`) batches, with mismatches planted on each side of the boundary;
-  * edge shapes (1-3 blocks, empty and sub-stripe blocks, unaligned rows) and a seeded
-    fuzz over counts, strides, lengths, offsets, threads, shares and planted mismatches;
+  * edge shapes (1-3 blocks, empty and sub-stripe blocks, unaligned rows) and seeded
+    fuzzes: split batches (counts, strides, lengths, offsets, threads, shares, planted
+    mismatches), split commits (forests, fan-outs, shares), routed calls under rates that
+    force each leg;
   * the balanced split and the routed call taking it;
   * the split commit (leaves on both sides, in place) against the oracle's commit, with
     relocations, and the routed commit taking it;
