@@ -21,6 +21,8 @@
 #include <cstddef>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
+#include <new>
 #include <optional>
 #include <stdexcept>
 #include <string>
@@ -108,13 +110,78 @@ inline std::optional<Error> VerifyChecksum(BlockAddress address, const void* p, 
 }
 
 // Batched checksums of n host blocks at base + i*stride (length bytes each, or lens[i]),
-// routed by the library's cost model (stormck_checksum_batch): the device over PCIe or
-// its host leg on host_threads threads (0 = the pool), whichever it predicts is faster.
+// routed by the library's cost model (stormck_checksum_batch): its host leg on
+// host_threads threads (0 = the pool), the device over PCIe, or both at once on disjoint
+// blocks (the split leg, for registered memory), whichever it predicts is fastest.
 inline std::vector<Hash> ChecksumBatch(const void* base, size_t n, size_t stride, uint32_t length,
                                        const uint32_t* lens = nullptr, uint32_t host_threads = 0) {
     std::vector<Hash> out(n);
     if (n) detail::check(stormck_checksum_batch(base, stride, lens, length, n, out.data(), host_threads, nullptr));
     return out;
+}
+
+enum class Leg : uint32_t { None = STORMCK_LEG_NONE, Host = STORMCK_LEG_HOST, Device = STORMCK_LEG_DEVICE,
+                            Split = STORMCK_LEG_SPLIT };
+
+// ChecksumBatch, also reporting the leg the library took.
+inline std::vector<Hash> ChecksumBatchLeg(const void* base, size_t n, size_t stride, uint32_t length, Leg* leg,
+                                          const uint32_t* lens = nullptr, uint32_t host_threads = 0) {
+    std::vector<Hash> out(n);
+    uint32_t used = STORMCK_LEG_NONE;
+    if (n) detail::check(stormck_checksum_batch(base, stride, lens, length, n, out.data(), host_threads, &used));
+    if (leg) *leg = static_cast<Leg>(used);
+    return out;
+}
+
+// The split leg alone (stormck_checksum_split) on pinned or registered memory: the host
+// threads from the front, the route devices from the back. device_blocks:
+// STORMCK_SPLIT_BALANCED (sized from the measured rates) or exactly the last
+// device_blocks blocks on the devices. *device_done: the blocks the devices hashed.
+inline std::vector<Hash> ChecksumBatchSplit(const void* base, size_t n, size_t stride, uint32_t length,
+                                            const uint32_t* lens = nullptr, uint32_t host_threads = 0,
+                                            uint64_t device_blocks = STORMCK_SPLIT_BALANCED,
+                                            uint64_t* device_done = nullptr) {
+    std::vector<Hash> out(n);
+    if (n)
+        detail::check(stormck_checksum_split(base, stride, lens, length, n, out.data(), nullptr, 0, host_threads,
+                                             device_blocks, device_done));
+    return out;
+}
+
+// storm's cache.data registered with the library for its lifetime (the Go binding's
+// NewHostArena): page-locked and mapped, so the device and split legs read it in place.
+class HostArena {
+public:
+    explicit HostArena(size_t bytes) : bytes_(bytes), p_(std::aligned_alloc(4096, (bytes + 4095) / 4096 * 4096)) {
+        if (!p_) throw std::bad_alloc();
+        const int rc = stormck_host_register(p_, bytes_);
+        if (rc != STORMCK_OK) {
+            std::free(p_);
+            throw DeviceError(rc);
+        }
+    }
+    ~HostArena() {
+        (void)stormck_host_unregister(p_);
+        std::free(p_);
+    }
+    HostArena(const HostArena&) = delete;
+    HostArena& operator=(const HostArena&) = delete;
+    uint8_t* data() { return static_cast<uint8_t*>(p_); }
+    size_t size() const { return bytes_; }
+
+private:
+    size_t bytes_;
+    void* p_;
+};
+
+// The routing model's rates (bytes/us) as measured so far, and the devices routed calls use.
+inline stormck_route_rates RouteRates() {
+    stormck_route_rates r{};
+    detail::check(stormck_route_get_rates(&r));
+    return r;
+}
+inline void RouteDevices(const std::vector<int>& devices) {
+    detail::check(stormck_route_devices(devices.empty() ? nullptr : devices.data(), static_cast<int>(devices.size())));
 }
 
 // The device leg alone (stormck_checksum_host: H2D, kernel, D2H pipelined).

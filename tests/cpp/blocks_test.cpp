@@ -1,5 +1,6 @@
 // C++ mirror of storm's blocks tests, run against libstormck (batches and ChecksumGPU on
-// the GPU, single calls on the library's host leg).
+// the GPU, single calls on the library's host leg), plus the routed legs on a registered
+// arena (HostArena, the split leg).
 // Each TEST mirrors a reference test (file:line in its comment). Relations are
 // asserted here; absolute values are printed as one JSON object for
 // tests/test_cpp_mirror.py to compare with tests/golden/layouts.json.
@@ -179,6 +180,41 @@ static void TestBatch() {
     EXPECT(bad.first_bad == 123 && bad.n_bad == 1);
 }
 
+// The routed legs on storm's configuration: cache.data registered (HostArena), the routed
+// batch, the split leg with fixed and balanced shares, verify across the boundary.
+static void TestRoutedLegs() {
+    const size_t n = 2000, stride = 32768;
+    HostArena arena(n * stride);
+    uint64_t x = 0x2545F4914F6CDD1DULL;
+    for (size_t i = 0; i < arena.size(); ++i) {
+        x ^= x << 13; x ^= x >> 7; x ^= x << 17;
+        arena.data()[i] = static_cast<uint8_t>(x);
+    }
+    std::vector<uint32_t> lens(n);
+    const uint32_t storm[] = {72, 28808, 30000, 31808, 32768};
+    for (size_t i = 0; i < n; ++i) lens[i] = storm[(i * 7) % 5];
+    std::vector<Hash> want(n);
+    for (size_t i = 0; i < n; ++i) want[i] = Checksum(arena.data() + i * stride, lens[i]);
+    Leg leg = Leg::None;
+    EXPECT(ChecksumBatchLeg(arena.data(), n, stride, 0, &leg, lens.data()) == want);
+    EXPECT(leg == Leg::Host || leg == Leg::Device || leg == Leg::Split);
+    for (uint64_t d : {uint64_t{0}, uint64_t{1}, uint64_t{n / 2}, uint64_t{n}}) {
+        uint64_t done = ~0ULL;
+        EXPECT(ChecksumBatchSplit(arena.data(), n, stride, 0, lens.data(), 0, d, &done) == want);
+        EXPECT(done == d);
+    }
+    EXPECT(ChecksumBatchSplit(arena.data(), n, stride, 0, lens.data(), 1) == want);  // balanced, one host thread
+    std::vector<Hash> bad = want;
+    bad[n / 2 - 1] ^= 1;
+    bad[n / 2] ^= 1;
+    uint64_t fb = 0, nb = 0, dd = 0;
+    const int rc = stormck_verify_split(arena.data(), stride, lens.data(), 0, n, bad.data(), &fb, &nb, nullptr, 0, 0,
+                                        n / 2, &dd);
+    EXPECT(rc == STORMCK_EMISMATCH && fb == n / 2 - 1 && nb == 2 && dd == n / 2);
+    EXPECT(RouteRates().host_thread > 0);
+    RouteDevices({});
+}
+
 // zero blocks of every type (prod sizes and `test`-tag sizes)
 template <class T>
 static std::string zero_cs() {
@@ -193,6 +229,7 @@ int main() {
     std::string sing = TestSingularity();
     TestKnownAnswers();
     TestBatch();
+    TestRoutedLegs();
     TestNewBlocksProduceConsistentResult();
     std::printf("{\"pointer_block_test_sequence\": %s, \"blob_test_block\": %s, \"singularity\": %s, "
                 "\"zero\": {\"prod\": {\"pointer\": %s, \"objectlist\": %s, \"spacelist\": %s, \"blob\": %s, "
