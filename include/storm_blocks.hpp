@@ -174,6 +174,28 @@ private:
     void* p_;
 };
 
+// Cache.Commit's data phase as the Go binding's CommitBatch runs it (stormck_commit): the
+// dirty forest in `arena` (cache.data; registered: any leg, unregistered: the host leg),
+// children first, relocation, each block's Pointer and type stored into its parent.
+// `dirty` gets the relocated addresses and birth revisions, as storm's blockMetadata.
+struct CommitResult {
+    std::vector<Hash> checksums;  // per dirty block, in the caller's order
+    BlockAddress last_allocated;
+    Leg leg;
+};
+inline CommitResult CommitBatch(void* arena, std::vector<stormck_dirty_block>& dirty, uint64_t revision,
+                                BlockAddress last_allocated, uint32_t host_threads = 0, void* stream = nullptr) {
+    CommitResult r{std::vector<Hash>(dirty.size()), last_allocated, Leg::None};
+    uint64_t la = last_allocated;
+    uint32_t used = STORMCK_LEG_NONE;
+    if (!dirty.empty())
+        detail::check(stormck_commit(arena, dirty.data(), dirty.size(), revision, &la, r.checksums.data(), stream,
+                                     host_threads, &used));
+    r.last_allocated = la;
+    r.leg = static_cast<Leg>(used);
+    return r;
+}
+
 // The routing model's rates (bytes/us) as measured so far, and the devices routed calls use.
 inline stormck_route_rates RouteRates() {
     stormck_route_rates r{};

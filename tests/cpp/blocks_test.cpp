@@ -4,6 +4,7 @@
 // Each TEST mirrors a reference test (file:line in its comment). Relations are
 // asserted here; absolute values are printed as one JSON object for
 // tests/test_cpp_mirror.py to compare with tests/golden/layouts.json.
+#include <cstddef>
 #include <cstdio>
 #include <cstring>
 #include <memory>
@@ -215,6 +216,50 @@ static void TestRoutedLegs() {
     RouteDevices({});
 }
 
+// Cache.Commit's data phase (cache/cache.go:87-137, trace.go:274-320) through CommitBatch:
+// three objectlist leaves under one pointer block in a registered arena. Leaves first,
+// relocated in order, their Pointers and types stored into the pointer block, whose
+// checksum then covers them.
+static void TestCommitBatch() {
+    const size_t slot = 32768;
+    HostArena arena(4 * slot);
+    std::memset(arena.data(), 0, arena.size());
+    for (size_t i = slot; i < arena.size(); ++i) arena.data()[i] = static_cast<uint8_t>(i * 2654435761u >> 13);
+    std::vector<stormck_dirty_block> dirty(4);
+    for (int i = 0; i < 3; ++i) {
+        dirty[i] = {};
+        dirty[i].data_offset = (i + 1) * slot;
+        dirty[i].origin_pointer = i * sizeof(Pointer);
+        dirty[i].origin_type = offsetof(PointerBlock<>, PointedBlockTypes) + i;
+        dirty[i].parent = 3;
+        dirty[i].address = 10 + i;
+        dirty[i].birth_revision = 1;
+        dirty[i].length = sizeof(ObjectListBlock<>);
+        dirty[i].type = LeafBlockType;
+    }
+    dirty[3] = {};
+    dirty[3].data_offset = 0;
+    dirty[3].origin_pointer = STORMCK_NO_ORIGIN;
+    dirty[3].parent = STORMCK_NO_PARENT;
+    dirty[3].address = 50;
+    dirty[3].birth_revision = 1;
+    dirty[3].length = sizeof(PointerBlock<>);
+    dirty[3].type = PointerBlockType;
+    std::vector<Hash> leaves(3);
+    for (int i = 0; i < 3; ++i) leaves[i] = Checksum(arena.data() + (i + 1) * slot, sizeof(ObjectListBlock<>));
+    const CommitResult r = CommitBatch(arena.data(), dirty, 5, 100);
+    EXPECT(r.leg == Leg::Host || r.leg == Leg::Device || r.leg == Leg::Split);
+    EXPECT(r.last_allocated == 104);
+    const auto* pb = reinterpret_cast<const PointerBlock<>*>(arena.data());
+    for (int i = 0; i < 3; ++i) {
+        EXPECT(r.checksums[i] == leaves[i]);
+        EXPECT(dirty[i].address == 101u + i && dirty[i].birth_revision == 6);
+        EXPECT(pb->Pointers[i].Checksum == leaves[i] && pb->Pointers[i].Address == 101u + i &&
+               pb->Pointers[i].BirthRevision == 6 && pb->PointedBlockTypes[i] == LeafBlockType);
+    }
+    EXPECT(dirty[3].address == 104 && r.checksums[3] == BlockChecksum(pb));
+}
+
 // zero blocks of every type (prod sizes and `test`-tag sizes)
 template <class T>
 static std::string zero_cs() {
@@ -230,6 +275,7 @@ int main() {
     TestKnownAnswers();
     TestBatch();
     TestRoutedLegs();
+    TestCommitBatch();
     TestNewBlocksProduceConsistentResult();
     std::printf("{\"pointer_block_test_sequence\": %s, \"blob_test_block\": %s, \"singularity\": %s, "
                 "\"zero\": {\"prod\": {\"pointer\": %s, \"objectlist\": %s, \"spacelist\": %s, \"blob\": %s, "
