@@ -1763,11 +1763,13 @@ int stormck_host_register(void* p, uint64_t bytes) {
     // stages now (pinned and device buffers, ~0.3 s once per process) rather than inside the
     // first routed call that splits (storm registers cache.data once, at start-up). Best
     // effort: a failure here is the first device call's to report.
+    const std::string before = g_last_error;  // a best-effort failure is not this call's error
     DeviceCtx* c = nullptr;
     if (get_ctx(&c) == STORMCK_OK) {
         std::lock_guard<std::mutex> g(c->mu);
         (void)ensure_ready(c);
     }
+    g_last_error = before;
     return STORMCK_OK;
 }
 
