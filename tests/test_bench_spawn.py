@@ -102,3 +102,17 @@ def test_root_fixture_names_the_workloads():
         assert name == f"c4 world {world}"
         assert want[1] == sdist.global_root_addr(bench.C4_BLOCKS) and want[3] == 1
     assert bench.root_fixture(12345, 1, False) == (None, None)
+
+
+@pytest.mark.parametrize("n", [2, 8, 12, 13])
+def test_e2e_leg_orders_are_balanced(n):
+    """The E2E workloads' leg orders (bench.balanced_orders): every leg once per order,
+    and each leg right after every other leg equally often (a leg's time depends on what
+    ran before it: DESIGN.md §4.2)."""
+    from collections import Counter
+    names = [f"leg{i}" for i in range(n)]
+    orders = bench.balanced_orders(names)
+    assert len(orders) == (n if n % 2 == 0 else 2 * n)
+    assert all(sorted(o) == sorted(names) for o in orders)
+    pairs = Counter((o[i - 1], o[i]) for o in orders for i in range(1, n))
+    assert len(pairs) == n * (n - 1) and len(set(pairs.values())) == 1
