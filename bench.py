@@ -43,7 +43,7 @@ C4_BLOCKS = 64 << 20  # BASELINE.json configs[3]
 SYNTH_SEED = 0x53544F524D  # synthetic block generator seed ("STORM")
 # --alloc: (placement mode, physical chunk bytes); modes other than plain need the probe
 # build (STORMCK_LIBRARY=tools/libstormck_probes.so: stormck_device_alloc_placed)
-ALLOC_MODES = {"plain": (0, 0), "vmm": (1, 0), "vmm1g": (1, 1 << 30), "contig": (2, 0)}
+ALLOC_MODES = {"plain": (0, 0), "contig": (2, 0)}
 KERNEL = "k_xxh64_glds_skew<16,nt,8w,4KiB>"  # dominant kernel (storm_amd/csrc/kernels.h), as named in profiles/traffic.json
 
 
@@ -61,9 +61,7 @@ def parse():
     p.add_argument("--arena", type=int, default=2 << 20, help="resident arena (blocks)")
     p.add_argument("--alloc", default="plain", choices=sorted(ALLOC_MODES),
                    help="arena placement: plain = hipMalloc (stormck_device_alloc); with the probe build "
-                        "(STORMCK_LIBRARY=tools/libstormck_probes.so) also vmm = a 1 GiB-aligned "
-                        "VMM reservation backed by one physical allocation; vmm1g = backed by 1 GiB allocations; "
-                        "contig = hipDeviceMallocContiguous")
+                        "(STORMCK_LIBRARY=tools/libstormck_probes.so) also contig = hipDeviceMallocContiguous")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget (rank 0, N=1)")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--settle", type=float, default=1.0,
@@ -89,6 +87,10 @@ def parse():
     p.add_argument("--keys", type=int, default=64 << 20, help="f4: keys per step (a multiple of 1024)")
     p.add_argument("--force-dist", action="store_true",
                    help="take the multi-rank path (process group, root all-gather, combine) even at N=1")
+    p.add_argument("--in-process", action="store_true",
+                   help="c3 / c4 on --gpus N devices from ONE process (storm's case: one Go process), through the "
+                        "C-ABI: per-device arena passes, then stormck_merkle_root_multi (shard trees, in-process "
+                        "RCCL all-gather of the shard roots, combine on every device)")
     p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                    help="nccl = RCCL (production); gloo only to rehearse N>1 with ranks sharing a GPU")
     return p.parse_args()
@@ -482,27 +484,29 @@ def commit_e2e_workload(a):
             la = ctypes.c_uint64(last)
             bp, op, nb = b.ctypes.data, out.ctypes.data, len(b)
             done, used = ctypes.c_uint64(0), ctypes.c_uint32(9)
+            # every pointer argument is converted outside the clock, so the Python columns
+            # differ by the calls' own costs (and ctypes' per-argument cost), not by byref()s
+            pla, pdone, pused = ctypes.byref(la), ctypes.byref(done), ctypes.byref(used)
             if leg in ("dev_inplace", "dev_hbm"):
                 ap = d_host.value if leg == "dev_inplace" else hbm.data_ptr()
 
                 def f():
-                    return L.stormck_commit_device(ap, bp, nb, REV, ctypes.byref(la), op, None)
+                    return L.stormck_commit_device(ap, bp, nb, REV, pla, op, None)
             elif leg in ("host_1", "host_all"):
                 nt = 1 if leg == "host_1" else threads
 
                 def f():
-                    return L.stormck_commit_host(arena_p, bp, nb, REV, ctypes.byref(la), op, nt)
+                    return L.stormck_commit_host(arena_p, bp, nb, REV, pla, op, nt)
             elif leg in ("split", "split_1"):
                 nt = 1 if leg == "split_1" else 0
 
                 def f():
-                    return L.stormck_commit_split(arena_p, bp, nb, REV, ctypes.byref(la), op, None, 0, nt,
-                                                  _lib.SPLIT_BALANCED, ctypes.byref(done))
+                    return L.stormck_commit_split(arena_p, bp, nb, REV, pla, op, None, 0, nt, _lib.SPLIT_BALANCED, pdone)
             else:  # routed: the library's pool (0) or one host thread ("routed_1")
                 nt = 1 if leg == "routed_1" else 0
 
                 def f():
-                    return L.stormck_commit(arena_p, bp, nb, REV, ctypes.byref(la), op, None, nt, ctypes.byref(used))
+                    return L.stormck_commit(arena_p, bp, nb, REV, pla, op, None, nt, pused)
             t0 = time.perf_counter()
             for _ in range(inner):
                 rc = f()
@@ -648,6 +652,7 @@ def batch_e2e_workload(a):
             op = out.ctypes.data
             bp = pg_p if leg in ("dev", "host_1", "host_all", "routed", "routed_1") else reg_p
             done, used = ctypes.c_uint64(0), ctypes.c_uint32(9)
+            pdone, pused = ctypes.byref(done), ctypes.byref(used)  # converted outside the clock
             if leg in ("dev", "dev_reg"):
                 def f():
                     return L.stormck_checksum_host(bp, stride, lp, ln, n, op)
@@ -661,7 +666,7 @@ def batch_e2e_workload(a):
 
                 def f():
                     return L.stormck_checksum_split(bp, stride, lp, ln, n, op, None, 0, nt, _lib.SPLIT_BALANCED,
-                                                    ctypes.byref(done))
+                                                    pdone)
             elif leg == "routed_x2":
                 h = n // 2
                 outs2, rcs = [out[:h], out[h:]], [0, 0]
@@ -686,7 +691,7 @@ def batch_e2e_workload(a):
                 nt = 1 if leg.endswith("_1") else 0
 
                 def f():
-                    return L.stormck_checksum_batch(bp, stride, lp, ln, n, op, nt, ctypes.byref(used))
+                    return L.stormck_checksum_batch(bp, stride, lp, ln, n, op, nt, pused)
             reps_in = 1 if leg == "routed_x2" else inner
             t0 = time.perf_counter()
             for _ in range(reps_in):
@@ -997,6 +1002,62 @@ def spawn_ranks(n: int, argv, entry=None, timeout: float = 0.0) -> int:
     return rc if rc >= 0 else 128 - rc
 
 
+def gather_rank_rows(elapsed: float, wall: float, kms, rank: int, blocks: int, tdev):
+    """All-gather every rank's (elapsed, wall, kernel avg / min / max ms, rank, blocks) over the
+    process group (RCCL on GPUs, gloo in the CPU rehearsal) as a list of rows in rank order."""
+    import torch
+    import torch.distributed as dist
+    kms = sorted(kms)
+    mine = torch.tensor([elapsed, wall, sum(kms) / len(kms), kms[0], kms[-1], float(rank), float(blocks)],
+                        dtype=torch.float64, device=tdev)
+    allr = [torch.empty_like(mine) for _ in range(dist.get_world_size())]
+    dist.all_gather(allr, mine)
+    return [[float(x) for x in r.cpu().tolist()] for r in allr]
+
+
+def summarize_ranks(rows, steps: int):
+    """(the slowest rank's elapsed time, the longest wall time, the per-rank record): the MAX
+    over ranks sets `value`."""
+    slow = max(range(len(rows)), key=lambda r: rows[r][0])
+    ranks = {"slowest_rank": slow,
+             "per_rank": [{"rank": int(r[5]), "blocks": int(r[6]), "ms_per_step": round(r[0] / steps * 1e3, 3),
+                           "kernel_avg_ms": round(r[2], 4), "kernel_min_ms": round(r[3], 4),
+                           "kernel_max_ms": round(r[4], 4)} for r in rows]}
+    return rows[slow][0], max(r[1] for r in rows), ranks
+
+
+C4_WORLD1 = os.path.join(ROOT, "profiles", "c4_world1.json")  # measured c4 N = 1 point (bench.py --in-process)
+
+
+def scaling_reference(world: int, n_total: int, ranks, value: float, scaling: str) -> dict:
+    """Fields of an N > 1 line that say which N = 1 number its scaling reads against (verdict
+    r05 item 3): the driver's N = 1 line is c3 (16M blocks on one GPU), while N > 1 runs c4
+    (64M blocks split over N GPUs, strong scaling), so per-GPU GiB/s is the comparable figure.
+    The strong-scaling N = 1 time of THIS workload is given two ways: estimated from this run
+    (the slowest rank's time per block x all n_total blocks) and, when committed, measured
+    (c4 world 1 in one process on one GPU: profiles/c4_world1.json)."""
+    per = ranks["per_rank"]
+    slow = per[ranks["slowest_rank"]]
+    est_ms = slow["ms_per_step"] / max(slow["blocks"], 1) * n_total
+    ref = {"per_gpu_GiB_s": round(value / world, 2),
+           "scaling_reference": {
+               "read_against": "per_gpu_GiB_s vs the N = 1 line's value (both are GiB/s of distinct 32 KiB blocks "
+                               "per GPU); ms_per_step vs strong_scaling_n1_ms_per_step",
+               "driver_n1_line": "bench.py --gpus 1 = c3: 16M blocks on one GPU (weak); not this workload",
+               "this_workload": f"{scaling} scaling: {n_total} blocks over {world} GPUs",
+               "strong_scaling_n1_ms_per_step_estimate": round(est_ms, 3),
+               "estimate_from": f"rank {slow['rank']}: {slow['ms_per_step']} ms per step for {slow['blocks']} "
+                                f"blocks, x {n_total} blocks"}}
+    if os.path.exists(C4_WORLD1):
+        with open(C4_WORLD1) as f:
+            m = json.load(f)
+        if m.get("total_blocks") == n_total:
+            ref["scaling_reference"]["strong_scaling_n1_ms_per_step"] = m["ms_per_step"]
+            ref["scaling_reference"]["strong_scaling_n1_value_GiB_s"] = m["value"]
+            ref["scaling_reference"]["strong_scaling_n1_source"] = m["source"]
+    return ref
+
+
 def root_fixture(n_total: int, world: int, distributed: bool):
     """The libxxhash root of this workload from tests/golden/c3c4_roots.json
     (oracle/gen_golden.py --c4), as (cs, addr, rev, type), or None if the workload has
@@ -1022,6 +1083,8 @@ def root_fixture(n_total: int, world: int, distributed: bool):
 
 def main():
     a = parse()
+    if a.in_process:
+        sys.exit(block_checksum_inprocess(a))
     if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
         # no launcher: one rank process per GPU, started before this process touches a GPU
         sys.exit(spawn_ranks(a.gpus, sys.argv))
@@ -1151,16 +1214,8 @@ def block_checksum_workload(a) -> int:
     if distributed:
         # every rank's step time and kernel launches; the MAX step time sets `value`
         tdev = dev if a.dist_backend == "nccl" else "cpu"  # gloo all-gathers host tensors
-        mine = torch.tensor([elapsed, wall, avg_ms, kms[0], kms[-1], float(rank)], dtype=torch.float64, device=tdev)
-        allr = [torch.empty_like(mine) for _ in range(world)]
-        dist.all_gather(allr, mine)
-        rows = [[float(x) for x in r.cpu().tolist()] for r in allr]
-        slow = max(range(world), key=lambda r: rows[r][0])
-        elapsed, wall = rows[slow][0], max(r[1] for r in rows)
-        ranks = {"slowest_rank": slow,
-                 "per_rank": [{"rank": int(r[5]), "ms_per_step": round(r[0] / a.steps * 1e3, 3),
-                               "kernel_avg_ms": round(r[2], 4), "kernel_min_ms": round(r[3], 4),
-                               "kernel_max_ms": round(r[4], 4)} for r in rows]}
+        rows = gather_rank_rows(elapsed, wall, kms, rank, n_gpu, tdev)
+        elapsed, wall, ranks = summarize_ranks(rows, a.steps)
     avg_blocks = sum(kblocks) / len(kblocks)
     alg_bytes = avg_blocks * (BLOCK + 8)          # L bytes read + 8 bytes written per block
     achieved = alg_bytes / (avg_ms * 1e-3) / 1e9  # GB/s (decimal, like the spec peak)
@@ -1227,8 +1282,7 @@ def block_checksum_workload(a) -> int:
                        "library": engine.library_record(),
                        "arena": {"va": "0x%x" % arena_ptr, "va_alignment": va_alignment(arena_ptr),
                                  "bytes": arena_n * BLOCK,
-                                 "alloc": {"plain": "hipMalloc", "vmm": "VMM reserve (1 GiB aligned) + one hipMemCreate",
-                                           "vmm1g": "VMM reserve (1 GiB aligned) + 1 GiB hipMemCreate chunks",
+                                 "alloc": {"plain": "hipMalloc",
                                            "contig": "hipExtMallocWithFlags(hipDeviceMallocContiguous)"}[a.alloc]
                                           + (" (stormck_device_alloc)" if a.alloc == "plain" else
                                              " (stormck_device_alloc_placed, probe build)")
@@ -1254,6 +1308,7 @@ def block_checksum_workload(a) -> int:
         if distributed:
             res["config"]["process_group"] = group
             res["ranks"] = ranks
+            res.update(scaling_reference(world, n_total, ranks, value, scaling))
         if world == 1 and not a.no_cpu:
             res["cpu_baseline"] = cpu_baseline(a.cpu_seconds)
         print(json.dumps(res), flush=True)
@@ -1261,6 +1316,153 @@ def block_checksum_workload(a) -> int:
         dist.destroy_process_group()
     torch.cuda.synchronize()
     engine.device_free(arena_ptr)
+    return rc
+
+
+def block_checksum_inprocess(a) -> int:
+    """--in-process: the BASELINE metric on --gpus N devices driven from one process, as storm
+    (one Go process) would through its cgo shim. Each device streams its planned shard
+    (stormck_shard_plan) through its own arena on its own stream, exactly like a rank of the
+    process-per-GPU path; the step's root then comes from ONE C-ABI call,
+    stormck_merkle_root_multi: the shard trees on their devices, an in-process RCCL
+    ncclAllGather of the shard roots, the combining node hashed on every device. The line has
+    the shape of the process-per-GPU line; `ranks` are devices here."""
+    import torch
+
+    from storm_amd import engine, multi
+
+    world = a.gpus
+    n_dev = torch.cuda.device_count()
+    if world > n_dev:
+        raise SystemExit(f"--in-process --gpus {world}: only {n_dev} visible device(s)")
+    if a.blocks:
+        n_total, scaling = a.blocks * world, "weak"
+    else:
+        n_total = a.total_blocks or (C3_BLOCKS if world == 1 else C4_BLOCKS)
+        scaling = "weak" if world == 1 and n_total == C3_BLOCKS else "strong"
+    devices = list(range(world))
+    shards, root_addr = multi.plan(n_total, world, devices)
+    per = []
+    for sh in shards:
+        d = sh.device
+        torch.cuda.set_device(d)
+        engine.init(d)
+        dev = torch.device("cuda", d)
+        arena_n = min(a.arena, max(sh.n, 1))
+        stream = torch.cuda.Stream(device=dev)
+        P = {"dev": dev, "arena": engine.device_alloc(arena_n * BLOCK), "arena_n": arena_n,
+             "cs": torch.empty(max(sh.n, 1), dtype=torch.int64, device=dev), "stream": stream,
+             "passes": (sh.n + arena_n - 1) // arena_n, "fill": [], "hash": []}
+        # the trees run on the shard's stream, after the passes that produced its checksums
+        multi.set_buffers(sh, P["cs"].data_ptr(), stream=stream.cuda_stream)
+        per.append(P)
+    torch.cuda.set_device(0)
+
+    def sync_all():
+        for d in devices:
+            torch.cuda.synchronize(d)
+
+    sync_all()
+
+    def ev_pair():
+        return torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+
+    def step(record: bool):
+        for p in range(max(P["passes"] for P in per)):
+            for sh, P in zip(shards, per):  # pass p on every device before pass p + 1 anywhere
+                first = p * P["arena_n"]
+                if first >= sh.n:
+                    continue
+                cnt = min(P["arena_n"], sh.n - first)
+                st = P["stream"]
+                with torch.cuda.device(P["dev"]):
+                    f, e = (ev_pair(), ev_pair()) if record else (None, None)
+                    if f:
+                        f[0].record(st)
+                    engine.fill_synthetic_device(P["arena"], BLOCK, cnt, sh.leaf_addr_base + first, SYNTH_SEED,
+                                                 st.cuda_stream)
+                    if f:
+                        f[1].record(st)
+                        e[0].record(st)
+                    engine.checksum_device(P["arena"], BLOCK, cnt, P["cs"][first:].data_ptr(), BLOCK, 0,
+                                           st.cuda_stream)
+                    if e:
+                        e[1].record(st)
+                        P["fill"].append(f)
+                        P["hash"].append((e[0], e[1], cnt))
+        return multi.merkle_root_multi(shards, REV, root_addr, FANOUT)  # synchronous
+
+    settle(lambda: step(False), a.settle)
+    for _ in range(a.warmup):
+        step(False)
+    sync_all()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        root, rows = step(True)
+    sync_all()
+    wall = time.perf_counter() - t0
+    # each device's elapsed time is the wall time less its own regeneration; the MAX over
+    # devices (the least regeneration taken out) sets `value`, as the MAX over ranks does
+    dev_rows = []
+    for k, (sh, P) in enumerate(zip(shards, per)):
+        fill_s = sum(f0.elapsed_time(f1) for f0, f1 in P["fill"]) * 1e-3
+        kms = sorted(e0.elapsed_time(e1) for (e0, e1, _) in P["hash"])
+        dev_rows.append([wall - fill_s, wall, sum(kms) / len(kms), kms[0], kms[-1], float(k), float(sh.n)])
+    elapsed, wall, ranks = summarize_ranks(dev_rows, a.steps)
+    for r, sh in zip(ranks["per_rank"], shards):
+        r["device"] = sh.device
+    launches = [(e0.elapsed_time(e1), c) for P in per for (e0, e1, c) in P["hash"]]
+    avg_ms = sum(t for t, _ in launches) / len(launches)
+    avg_blocks = sum(c for _, c in launches) / len(launches)
+    achieved = avg_blocks * (BLOCK + 8) / (avg_ms * 1e-3) / 1e9
+    value = n_total * BLOCK * a.steps / elapsed / 2**30
+
+    fx = golden("c3c4_roots.json")
+    fmt = lambda r: ["0x%016x" % v for v in r[:3]] + [r[3]]  # noqa: E731
+    check, rc = "no fixture for this workload", 0
+    if fx and world == 1 and n_total == fx["c3"]["n"]:
+        ok = fmt(rows[0]) == fx["c3"]["root"]
+        check = "shard root " + ("match (c3" if ok else "MISMATCH vs c3") + ", tests/golden/c3c4_roots.json)"
+        rc = 0 if ok else 3
+    elif fx and n_total == fx["c4"]["n_total"] and str(world) in fx["c4"]["worlds"]:
+        want = fx["c4"]["worlds"][str(world)]
+        ok = fmt(root) == want["global_root"] and [fmt(r) for r in rows] == want["shard_roots"]
+        check = ("match" if ok else "MISMATCH vs") + f" c4 world {world} (global and shard roots, " \
+                                                     "tests/golden/c3c4_roots.json)"
+        rc = 0 if ok else 3
+    cfg = "c3" if (world == 1 and n_total == C3_BLOCKS) else ("c4" if n_total == C4_BLOCKS else "custom")
+    res = {
+        "metric": METRIC, "value": round(value, 2), "unit": "GiB/s", "n_gpus": world, "steps": a.steps,
+        "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True,
+        "scaling": scaling, "vs_baseline": None, "dtype": "u64", "data": "synthetic",
+        "config": {"workload": f"{cfg}: {n_total / 2**20:g}M x 32 KiB blocks over {world} GPU(s) from one process, "
+                               "XXH64 seed 0 (blocks.Checksum) + shard Merkle pointer trees + in-process RCCL "
+                               "all-gather of the shard roots (stormck_merkle_root_multi)",
+                   "total_blocks": n_total, "blocks_per_gpu": [sh.n for sh in shards], "block_bytes": BLOCK,
+                   "arena_blocks": per[0]["arena_n"], "passes_per_step": per[0]["passes"],
+                   "parallelism": f"dp{world} (one process, contiguous block ranges, a device each)",
+                   "library": engine.library_record(),
+                   "process_group": {"mode": "in-process", "world_size": world, "device_count": n_dev,
+                                     "backend": "rccl: ncclCommInitAll + ncclAllGather inside stormck_merkle_root_multi"},
+                   "timed": "K steps between synchronize of every device, minus each device's on-device "
+                            "regeneration (its own HIP events); the slowest device sets the time",
+                   "ms_per_step_with_regeneration": round(wall / a.steps * 1e3, 3)},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None, "kernel": KERNEL,
+                     "avg_launch_ms": round(avg_ms, 4), "launch_ms": {"n": len(launches)},
+                     "algorithmic_bytes_per_launch": int(avg_blocks * (BLOCK + 8))},
+        "root": "0x%016x" % root[0], "root_pointer": fmt(root), "shard_roots": [fmt(r) for r in rows],
+        "root_check": check, "ranks": ranks,
+    }
+    if world > 1:
+        res.update(scaling_reference(world, n_total, ranks, value, scaling))
+    if world == 1 and not a.no_cpu:
+        res["cpu_baseline"] = cpu_baseline(a.cpu_seconds)
+    print(json.dumps(res), flush=True)
+    sync_all()
+    for P in per:
+        with torch.cuda.device(P["dev"]):
+            engine.device_free(P["arena"])
     return rc
 
 

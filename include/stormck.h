@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define STORMCK_ABI_VERSION 5
+#define STORMCK_ABI_VERSION 6
 
 #define STORMCK_OK 0
 #define STORMCK_EINVAL (-1)  /* bad argument (null pointer, n/len/stride out of range, ...) */
@@ -196,7 +196,9 @@ int stormck_checksum_gpu(const void* p, uint64_t n_bytes, uint64_t* out);
 /* Page-lock and map a host range (for every device) so the device and split legs DMA it or
  * read it in place, without staging copies. Also sets up the calling thread's current
  * device's staging for those legs (once per process: 2.25 GiB of HBM and 1 GiB of pinned
- * host memory, ~0.3 s), so the first routed call that uses the device does not pay for it. */
+ * host memory, ~0.3 s), so the first routed call that uses the device does not pay for it.
+ * The library keeps the range in its own list (the routed calls recognise it without a
+ * runtime query): release it with stormck_host_unregister, not hipHostUnregister directly. */
 int stormck_host_register(void* p, uint64_t bytes);
 int stormck_host_unregister(void* p);
 /* Device-visible address of host memory registered with stormck_host_register: the
@@ -235,6 +237,58 @@ int stormck_merkle_root_device(const uint64_t* d_leaf_cs, uint64_t n, uint64_t l
                                uint64_t node_addr_base, uint64_t rev, uint32_t fanout, void* d_workspace,
                                uint64_t workspace_bytes, stormck_pointer* d_root, uint8_t* d_root_type,
                                void* stream);
+
+/* ---- multi-GPU, one process: device-resident shards and their global root (c4) --------
+ * storm is one Go process; on an 8-GPU node it reaches every GPU from it.
+ * A batch of device-resident blocks is sharded into contiguous ranges, each on its own
+ * device. stormck_merkle_root_multi runs each shard's checksums (optional) and its shard
+ * tree (stormck_merkle_root_device) on the shard's device, from one host thread per device,
+ * gathers the shard roots over xGMI with in-process RCCL (ncclCommInitAll over the distinct
+ * devices, one ncclAllGather of their root rows), and hashes the combining pointer block on
+ * EVERY device; the devices must agree. The reference has no multi-device code; the tree
+ * shape is this library's and the node format storm's (blocks/pointer/block.go:10-13).
+ * One shard: */
+typedef struct stormck_shard {
+    const void* d_blocks;    /* block i at d_blocks + i*stride on `device`, `len` bytes; NULL: the
+                              * leaf checksums are already in d_checksums (nothing is hashed) */
+    uint64_t stride;
+    uint64_t n;              /* leaves of the shard */
+    uint64_t* d_checksums;   /* n u64 on `device`: written when d_blocks is set, else read */
+    uint64_t leaf_addr_base; /* Address of leaf i is leaf_addr_base + i (Leaf type, rev) */
+    uint64_t node_addr_base; /* interior nodes: node_addr_base, +1, ... level by level, bottom-up */
+    void* stream;            /* a stream of `device` the shard's work runs on, after what is already
+                              * queued there (e.g. the launches that wrote d_checksums); NULL: the
+                              * library's own stream, which waits for no other stream */
+    int32_t device;          /* HIP device index holding the shard */
+    uint32_t len;            /* bytes hashed per block (when d_blocks is set) */
+} stormck_shard;
+
+/* The build's shard convention (storm_amd/dist.py): n_total leaves in n_shards
+ * contiguous ranges whose sizes differ by at most one; shard s holds leaves [lo_s, hi_s),
+ * addressed lo_s..hi_s-1, its interior nodes from n_total + lo_s (disjoint from every other
+ * shard's and from the leaves for fanout >= 3), and the combining node gets 2 * n_total.
+ * Fills n, leaf_addr_base, node_addr_base and device (shards are dealt to devices[0..n_devices)
+ * in consecutive runs: shard s on devices[s * n_devices / n_shards]) of shards[0..n_shards) and
+ * zeroes the rest; the caller sets d_blocks / stride / len / d_checksums / stream, with shard
+ * s's blocks being logical blocks [lo_s, hi_s) (lo_s = leaf_addr_base). *root_addr (optional)
+ * = 2 * n_total. Needs no device. */
+int stormck_shard_plan(uint64_t n_total, uint32_t n_shards, const int* devices, int n_devices, stormck_shard* shards,
+                       uint64_t* root_addr);
+
+/* The global root of shards[0..n_shards) (1 <= n_shards <= fanout): every shard's tree
+ * (leaves of type Leaf, birth revision rev), then one pointer block holding the shard roots
+ * in shard order, hashed on every device: *root = {its checksum, root_addr, rev}, *root_type =
+ * Pointer. shard_roots / shard_types (optional, n_shards each) = the shard roots (a shard of
+ * n == 0 has a zero root of type Free, of n == 1 its leaf's own Pointer). Synchronous: returns
+ * when every shard's work and the gather have finished; the shards' streams may then be reused.
+ * A device may hold several shards (the gather then carries several rows per device; with one
+ * device the gather is a one-rank RCCL communicator). RCCL (librccl.so.1, from the ROCm
+ * install or already in the process) is loaded at the first call and its communicators are
+ * kept per device set; STORMCK_EHIP names an RCCL that cannot be loaded or fails. Calls are
+ * serialised process-wide (a communicator serves one collective at a time). */
+int stormck_merkle_root_multi(const stormck_shard* shards, uint32_t n_shards, uint64_t rev, uint64_t root_addr,
+                              uint32_t fanout, stormck_pointer* root, uint8_t* root_type, stormck_pointer* shard_roots,
+                              uint8_t* shard_types);
 
 /* ---- f2/f3: batched cold read + verify from a file device -------------------
  * storm's cold fetch reads a block from its Dev and verifies it

@@ -304,3 +304,70 @@ func UnregisterHostMemory(b []byte) error {
 	}
 	return nil
 }
+
+// Shard mirrors stormck_shard (include/stormck.h): one device-resident shard of a batch on an
+// 8-GPU node, driven from storm's one process. Blocks and Checksums are device addresses on
+// Device (e.g. from a HIP allocation the caller owns); they are not Go pointers, so the cgo
+// pointer rules do not apply to them.
+type Shard struct {
+	Blocks       uintptr // block i at Blocks + i*Stride, Len bytes; 0: Checksums already holds the leaf checksums
+	Stride       uint64
+	N            uint64       // leaves of the shard
+	Checksums    uintptr      // N uint64 checksums on Device: written when Blocks is set, read otherwise
+	LeafAddrBase BlockAddress // leaf i is addressed LeafAddrBase + i
+	NodeAddrBase BlockAddress // the shard tree's interior nodes from here, level by level
+	Stream       uintptr      // a HIP stream of Device the shard's work follows (0: the library's own)
+	Device       int32
+	Len          uint32
+}
+
+// compile-time checks that Shard and Pointer have the C layouts (64 and 24 bytes)
+var (
+	_ = [1]struct{}{}[unsafe.Sizeof(Shard{})-64]
+	_ = [1]struct{}{}[unsafe.Sizeof(Pointer{})-24]
+)
+
+// PlanShards deals nTotal leaves into nShards contiguous shards over devices
+// (stormck_shard_plan: consecutive shards per device, leaf and node addresses disjoint,
+// SURVEY.md §8e) and returns them with the combining node's address. The caller fills each
+// shard's Blocks / Stride / Len / Checksums / Stream. Needs no GPU.
+func PlanShards(nTotal uint64, nShards int, devices []int32) ([]Shard, BlockAddress, error) {
+	if nShards <= 0 || len(devices) == 0 {
+		return nil, 0, errors.New("PlanShards: need shards and devices")
+	}
+	shards := make([]Shard, nShards)
+	var rootAddr C.uint64_t
+	rc := C.stormck_shard_plan(C.uint64_t(nTotal), C.uint32_t(nShards), (*C.int)(unsafe.Pointer(&devices[0])),
+		C.int(len(devices)), (*C.stormck_shard)(unsafe.Pointer(&shards[0])), &rootAddr)
+	if rc != C.STORMCK_OK {
+		return nil, 0, stormckError(rc)
+	}
+	return shards, BlockAddress(rootAddr), nil
+}
+
+// MerkleRootDevices computes the global Merkle root of device-resident shards from this one
+// process (stormck_merkle_root_multi): each shard's checksums (when Blocks is set) and its
+// pointer-block tree on its own GPU, the shard roots all-gathered over xGMI by in-process
+// RCCL, and the combining pointer.Block (blocks/pointer/block.go:10-13) hashed on every GPU.
+// It returns the root Pointer (type Pointer) and every shard's root. Synchronous.
+func MerkleRootDevices(shards []Shard, revision uint64, rootAddr BlockAddress) (Pointer, []Pointer, []BlockType, error) {
+	n := len(shards)
+	if n == 0 {
+		return Pointer{}, nil, nil, errors.New("MerkleRootDevices: no shards")
+	}
+	var root Pointer
+	var rootType C.uint8_t
+	shardRoots := make([]Pointer, n)
+	shardTypes := make([]BlockType, n)
+	rc := C.stormck_merkle_root_multi((*C.stormck_shard)(unsafe.Pointer(&shards[0])), C.uint32_t(n),
+		C.uint64_t(revision), C.uint64_t(rootAddr), C.STORMCK_POINTERS_PER_BLOCK,
+		(*C.stormck_pointer)(unsafe.Pointer(&root)), &rootType,
+		(*C.stormck_pointer)(unsafe.Pointer(&shardRoots[0])), (*C.uint8_t)(unsafe.Pointer(&shardTypes[0])))
+	if rc != C.STORMCK_OK {
+		return Pointer{}, nil, nil, stormckError(rc)
+	}
+	if BlockType(rootType) != PointerBlockType {
+		return Pointer{}, nil, nil, errors.Errorf("MerkleRootDevices: root of type %d", rootType)
+	}
+	return root, shardRoots, shardTypes, nil
+}

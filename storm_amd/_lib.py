@@ -26,8 +26,7 @@ EMISMATCH = -5
 # arena placement modes of stormck_device_alloc_placed: the probe build only (measured and
 # rejected in round 4; the product allocates with hipMalloc, stormck_device_alloc)
 ALLOC_PLAIN = 0
-ALLOC_VMM = 1
-ALLOC_CONTIGUOUS = 2
+ALLOC_CONTIGUOUS = 2  # (mode 1, a VMM reservation, was deleted in round 6)
 # STORMCK_LEG_* (stormck_commit, stormck_checksum_batch, the route plan)
 LEG_NONE, LEG_HOST, LEG_DEVICE, LEG_SPLIT = 0, 1, 2, 3
 LEG_NAMES = {LEG_NONE: "none", LEG_HOST: "host", LEG_DEVICE: "device", LEG_SPLIT: "split"}
@@ -65,6 +64,14 @@ class PointerStruct(ctypes.Structure):
     """stormck_pointer == blocks.Pointer (/root/reference/blocks/types.go:35-39)."""
 
     _fields_ = [("Checksum", c_uint64), ("Address", c_uint64), ("BirthRevision", c_uint64)]
+
+
+class ShardStruct(ctypes.Structure):
+    """stormck_shard: one device-resident shard of stormck_merkle_root_multi."""
+
+    _fields_ = [("d_blocks", c_void_p), ("stride", c_uint64), ("n", c_uint64), ("d_checksums", c_void_p),
+                ("leaf_addr_base", c_uint64), ("node_addr_base", c_uint64), ("stream", c_void_p),
+                ("device", ctypes.c_int32), ("len", c_uint32)]
 
 
 # name -> (restype, argtypes); mirrors include/stormck.h one to one.
@@ -109,6 +116,10 @@ SIGNATURES = {
     "stormck_merkle_workspace_bytes": (c_uint64, [c_uint64, c_uint32]),
     "stormck_merkle_root_device": (
         c_int, [c_void_p, c_uint64, c_uint64, c_uint64, c_uint64, c_uint32, c_void_p, c_uint64, c_void_p, c_void_p, c_void_p]),
+    "stormck_shard_plan": (c_int, [c_uint64, c_uint32, c_void_p, c_int, POINTER(ShardStruct), POINTER(c_uint64)]),
+    "stormck_merkle_root_multi": (
+        c_int, [POINTER(ShardStruct), c_uint32, c_uint64, c_uint64, c_uint32, POINTER(PointerStruct),
+                POINTER(c_uint8), POINTER(PointerStruct), POINTER(c_uint8)]),
     "stormck_read_verify_fd": (
         c_int, [c_int, c_void_p, c_void_p, c_uint64, c_uint64, c_void_p, c_uint64, c_void_p, c_uint32, c_void_p, c_void_p]),
     "stormck_key_tags_device": (c_int, [c_void_p, c_uint64, c_void_p, c_void_p, c_uint32, c_uint64, c_void_p, c_void_p]),

@@ -35,7 +35,7 @@ def _newer(target: str, sources) -> bool:
 
 
 # the sources libstormck.so is compiled from (its build id hashes them)
-SOURCES = [os.path.join(CSRC, f) for f in ("stormck.hip", "kernels.h", "xxh64_dev.h", "xxh64_host.h")] + \
+SOURCES = [os.path.join(CSRC, f) for f in ("stormck.hip", "kernels.h", "multi_root.h", "xxh64_dev.h", "xxh64_host.h")] + \
     [os.path.join(ROOT, "include", "stormck.h")]
 
 

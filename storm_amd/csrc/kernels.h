@@ -2157,6 +2157,20 @@ __global__ void k_set_root(const uint64_t* __restrict__ cs, uint64_t addr, uint6
     }
 }
 
+// Multi-GPU combine (stormck_merkle_root_multi): after the gather, shard s's root row
+// {cs, addr, rev, type} is table row map[s]; the combining node's entries are those rows in
+// shard order (what k_pointer_node hashes).
+__global__ void k_gather_root_rows(const uint64_t* __restrict__ table, const uint32_t* __restrict__ map,
+                                   uint32_t count, uint64_t* __restrict__ entries, uint8_t* __restrict__ types) {
+    for (uint32_t s = threadIdx.x; s < count; s += blockDim.x) {
+        const uint64_t* row = table + 4ull * map[s];
+        entries[3ull * s] = row[0];
+        entries[3ull * s + 1] = row[1];
+        entries[3ull * s + 2] = row[2];
+        types[s] = static_cast<uint8_t>(row[3]);
+    }
+}
+
 // ---------------------------------------------------------------------------
 // f1: one level of a level-synchronous commit. blocks[lo, lo + cnt) are this level's
 // dirty records in commit order (the host lays them out so; they may sit in pinned

@@ -15,8 +15,10 @@
 #include <system_error>
 #include <functional>
 #include <thread>
+#include <type_traits>
 #include <vector>
 
+#include <dlfcn.h>
 #include <fcntl.h>
 #include <pthread.h>
 #include <sched.h>
@@ -24,6 +26,8 @@
 #include <unistd.h>
 
 #include <cerrno>
+
+#include <rccl/rccl.h>  // types and declarations only: RCCL is loaded at run time (multi_root.h)
 
 #include "../../include/stormck.h"
 #include "kernels.h"
@@ -86,21 +90,55 @@ class ForkJoin {
         while (remaining_.load(std::memory_order_acquire) != 0) std::this_thread::yield();
     }
 
-    // CPUs the process may use at once: its affinity mask, capped by a cgroup v2 CPU quota
-    // (a GPU box grants each GPU's process 16 CPUs of a 256-CPU host by quota)
+    // CPUs the process may use at once: its affinity mask, capped by the smallest CPU quota
+    // on its cgroup's path (a GPU box grants each GPU's process 16 CPUs of a 256-CPU host by
+    // quota). cgroup v2: cpu.max from the process's own cgroup (/proc/self/cgroup "0::/path",
+    // e.g. a systemd slice on a bare host) up to the root of the mount, as a container sees
+    // it; cgroup v1: cpu.cfs_quota_us / cpu.cfs_period_us of the cpu controller's mount.
     static unsigned usable_cpus() {
         cpu_set_t set;
         unsigned cpus = std::max(1u, std::thread::hardware_concurrency());
         if (sched_getaffinity(0, sizeof set, &set) == 0) cpus = std::max(1, CPU_COUNT(&set));
-        if (FILE* f = std::fopen("/sys/fs/cgroup/cpu.max", "r")) {
-            char quota[32] = {};
-            unsigned long long period = 0;
-            if (std::fscanf(f, "%31s %llu", quota, &period) == 2 && std::strcmp(quota, "max") != 0 && period > 0) {
-                const double q = std::strtod(quota, nullptr) / static_cast<double>(period);
-                cpus = std::min(cpus, std::max(1u, static_cast<unsigned>(q + 0.5)));
-            }
+        double quota = 0;  // smallest quota found, in CPUs (0: none)
+        auto take = [&](double q) {
+            if (q > 0 && (quota == 0 || q < quota)) quota = q;
+        };
+        std::string rel;  // the process's cgroup v2 path
+        if (FILE* f = std::fopen("/proc/self/cgroup", "r")) {
+            char line[4096];
+            while (std::fgets(line, sizeof line, f))
+                if (std::strncmp(line, "0::", 3) == 0) {
+                    rel = line + 3;
+                    while (!rel.empty() && (rel.back() == '\n' || rel.back() == '/')) rel.pop_back();
+                }
             std::fclose(f);
         }
+        for (std::string dir = rel;; dir = dir.substr(0, dir.rfind('/'))) {
+            if (FILE* f = std::fopen(("/sys/fs/cgroup" + dir + "/cpu.max").c_str(), "r")) {
+                char q[32] = {};
+                unsigned long long period = 0;
+                if (std::fscanf(f, "%31s %llu", q, &period) == 2 && std::strcmp(q, "max") != 0 && period > 0)
+                    take(std::strtod(q, nullptr) / static_cast<double>(period));
+                std::fclose(f);
+            }
+            if (dir.empty() || dir.find('/') == std::string::npos) break;
+        }
+        for (const char* d : {"/sys/fs/cgroup/cpu,cpuacct", "/sys/fs/cgroup/cpu"}) {
+            long long q = -1, period = 0;
+            if (FILE* f = std::fopen((std::string(d) + "/cpu.cfs_quota_us").c_str(), "r")) {
+                if (std::fscanf(f, "%lld", &q) != 1) q = -1;
+                std::fclose(f);
+            }
+            if (FILE* f = std::fopen((std::string(d) + "/cpu.cfs_period_us").c_str(), "r")) {
+                if (std::fscanf(f, "%lld", &period) != 1) period = 0;
+                std::fclose(f);
+            }
+            if (q > 0 && period > 0) {
+                take(static_cast<double>(q) / static_cast<double>(period));
+                break;
+            }
+        }
+        if (quota > 0) cpus = std::min(cpus, std::max(1u, static_cast<unsigned>(quota + 0.5)));
         return cpus;
     }
     unsigned cpus() const { return cpus_; }
@@ -1099,7 +1137,10 @@ void release_ctx(DeviceCtx* c) {
 }
 
 // Whether this process can read the first and the last byte of [p, p + bytes) (e.g. not a
-// device address the CPU mapping leaves inaccessible), without faulting: one
+// device address the CPU mapping leaves inaccessible), without faulting. Only the two
+// endpoints are checked: a range with an unmapped page in its middle passes, and the host
+// threads then fault on it as a plain memcpy would (include/stormck.h asks for readable
+// ranges; this check only turns device memory passed by mistake into EINVAL). One
 // process_vm_readv of the two bytes from this process itself (EFAULT when either is not
 // readable), or, where that syscall is not permitted, a write of each byte into a pipe.
 bool host_readable(const void* p, uint64_t bytes) {
@@ -1134,19 +1175,32 @@ enum class Mem {
     kDevice,      // HBM: the _device entry points
     kUnreadable,  // unknown to HIP and not readable by the host
 };
-#ifdef STORMCK_PROBES
-bool in_vmm_arena(const void* p);
-#endif
+// Host ranges registered through stormck_host_register (storm registers cache.data once, at
+// start-up): classify() answers kMapped for them from this list rather than asking the HIP
+// runtime, which takes its memory-object lock (storm's smallest commits pay every fixed cost of
+// the routed call; verdict r05 item 4). Ranges leave the list in stormck_host_unregister.
+std::mutex g_reg_mu;
+std::vector<std::pair<uintptr_t, uintptr_t>> g_reg;  // [lo, hi)
+std::atomic<size_t> g_reg_n{0};
+
+bool in_registered(const void* p, uint64_t bytes) {
+    if (g_reg_n.load(std::memory_order_acquire) == 0) return false;
+    const uintptr_t x = reinterpret_cast<uintptr_t>(p);
+    std::lock_guard<std::mutex> g(g_reg_mu);
+    for (const auto& r : g_reg)
+        if (x >= r.first && x < r.second && bytes <= r.second - x) return true;
+    return false;
+}
 
 Mem classify(const void* p, uint64_t bytes) {
-#ifdef STORMCK_PROBES
-    if (in_vmm_arena(p)) return Mem::kDevice;
-#endif
+    if (in_registered(p, std::max<uint64_t>(bytes, 1))) return Mem::kMapped;
     hipPointerAttribute_t a;
     if (hipPointerGetAttributes(&a, p) == hipSuccess) {
         if (a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeArray) return Mem::kDevice;
-        if (a.type == hipMemoryTypeHost || a.type == hipMemoryTypeManaged)
-            return a.devicePointer ? Mem::kMapped : Mem::kPinned;
+        // managed memory is DMA-able but has no hipHostGetDevicePointer mapping, which the
+        // in-place (kMapped) kernels need: it takes the copy engine
+        if (a.type == hipMemoryTypeManaged) return Mem::kPinned;
+        if (a.type == hipMemoryTypeHost) return a.devicePointer ? Mem::kMapped : Mem::kPinned;
     } else {
         (void)hipGetLastError();
     }
@@ -1386,28 +1440,7 @@ int host_pipeline_multi(const void* base, uint64_t stride, const uint32_t* lens,
     return STORMCK_OK;
 }
 
-#ifdef STORMCK_PROBES
-// Probe build only: arenas from stormck_device_alloc_placed(VMM) (DESIGN_LOG.md, "Arena
-// placement": no better than hipMalloc, and 2 MiB chunks once read wrong before access was
-// set per chunk), with their physical chunks so stormck_device_free can release them.
-constexpr uint64_t kVmmAlign = 1ULL << 30;
-struct VmmArena {
-    uint64_t size = 0, chunk = 0;
-    std::vector<hipMemGenericAllocationHandle_t> handles;
-};
-std::mutex g_arena_mu;
-std::vector<std::pair<void*, VmmArena>> g_vmm;
-
-bool in_vmm_arena(const void* p) {
-    const uintptr_t x = reinterpret_cast<uintptr_t>(p);
-    std::lock_guard<std::mutex> g(g_arena_mu);
-    for (const auto& e : g_vmm) {
-        const uintptr_t b = reinterpret_cast<uintptr_t>(e.first);
-        if (x >= b && x < b + e.second.size) return true;
-    }
-    return false;
-}
-#endif
+#include "multi_root.h"
 
 }  // namespace
 
@@ -1478,79 +1511,21 @@ int stormck_device_alloc(uint64_t bytes, void** d_ptr) {
 
 #ifdef STORMCK_PROBES
 // Probe build only (not in include/stormck.h): the arena placement modes measured and
-// rejected in round 4 (mode 0 hipMalloc, 1 VMM reservation + hipMemCreate chunks,
-// 2 hipDeviceMallocContiguous).
+// rejected in round 4 (mode 0 hipMalloc, 2 hipDeviceMallocContiguous). Mode 1, a VMM
+// reservation backed by hipMemCreate chunks, was deleted in round 6: no better placement,
+// and twice it read wrong blocks.
 int stormck_device_alloc_placed(uint64_t bytes, uint32_t mode, uint64_t chunk_bytes, void** d_ptr,
                                 uint64_t* mapped_chunk) {
+    (void)chunk_bytes;
     if (!d_ptr) return fail(STORMCK_EINVAL, "d_ptr is null");
     *d_ptr = nullptr;
     if (mapped_chunk) *mapped_chunk = 0;
     if (bytes == 0) return fail(STORMCK_EINVAL, "bytes is 0");
-    if (mode > 2) return fail(STORMCK_EINVAL, "unknown allocation mode");
+    if (mode != 0 && mode != 2) return fail(STORMCK_EINVAL, "unknown allocation mode (0 hipMalloc, 2 contiguous)");
     int rc = device_check();
     if (rc) return rc;
-    if (mode == 0) {
-        HIP_TRY(hipMalloc(d_ptr, bytes));
-        return STORMCK_OK;
-    }
-    if (mode == 2) {
-        HIP_TRY(hipExtMallocWithFlags(d_ptr, bytes, hipDeviceMallocContiguous));
-        return STORMCK_OK;
-    }
-    // STORMCK_ALLOC_VMM: a 1 GiB-aligned reservation backed by physical chunks
-    int dev = 0;
-    HIP_TRY(hipGetDevice(&dev));
-    hipMemAllocationProp prop;
-    std::memset(&prop, 0, sizeof prop);
-    prop.type = hipMemAllocationTypePinned;
-    prop.location.type = hipMemLocationTypeDevice;
-    prop.location.id = dev;
-    size_t gmin = 0, grec = 0;
-    HIP_TRY(hipMemGetAllocationGranularity(&gmin, &prop, hipMemAllocationGranularityMinimum));
-    HIP_TRY(hipMemGetAllocationGranularity(&grec, &prop, hipMemAllocationGranularityRecommended));
-    const uint64_t gran = std::max<uint64_t>({gmin, grec, 1});
-    auto round_up = [](uint64_t v, uint64_t m) { return (v + m - 1) / m * m; };
-    const uint64_t chunk = round_up(chunk_bytes ? chunk_bytes : bytes, gran);
-    const uint64_t size = round_up(bytes, chunk);
-    VmmArena a;
-    a.size = size;
-    void* va = nullptr;
-    HIP_TRY(hipMemAddressReserve(&va, size, kVmmAlign, nullptr, 0));
-    auto undo = [&] {
-        for (size_t k = 0; k < a.handles.size(); ++k) {
-            (void)hipMemUnmap(static_cast<uint8_t*>(va) + k * chunk, chunk);
-            (void)hipMemRelease(a.handles[k]);
-        }
-        (void)hipMemAddressFree(va, size);
-        (void)hipGetLastError();
-    };
-    hipMemAccessDesc acc;
-    std::memset(&acc, 0, sizeof acc);
-    acc.location = prop.location;
-    acc.flags = hipMemAccessFlagsProtReadWrite;
-    for (uint64_t off = 0; off < size; off += chunk) {
-        hipMemGenericAllocationHandle_t h;
-        hipError_t e = hipMemCreate(&h, chunk, &prop, 0);
-        if (e == hipSuccess) {
-            e = hipMemMap(static_cast<uint8_t*>(va) + off, chunk, 0, h, 0);
-            if (e != hipSuccess) (void)hipMemRelease(h);
-            else a.handles.push_back(h);
-        }
-        // access per mapped chunk (one call over the whole reservation is not relied on)
-        if (e == hipSuccess) e = hipMemSetAccess(static_cast<uint8_t*>(va) + off, chunk, &acc, 1);
-        if (e != hipSuccess) {
-            undo();
-            return fail(e == hipErrorOutOfMemory ? STORMCK_ENOMEM : STORMCK_EHIP,
-                        std::string("VMM arena: ") + hipGetErrorString(e));
-        }
-    }
-    a.chunk = chunk;
-    {
-        std::lock_guard<std::mutex> g(g_arena_mu);
-        g_vmm.emplace_back(va, std::move(a));
-    }
-    *d_ptr = va;
-    if (mapped_chunk) *mapped_chunk = chunk;
+    if (mode == 0) HIP_TRY(hipMalloc(d_ptr, bytes));
+    else HIP_TRY(hipExtMallocWithFlags(d_ptr, bytes, hipDeviceMallocContiguous));
     return STORMCK_OK;
 }
 #endif
@@ -1559,34 +1534,8 @@ int stormck_device_free(void* d_ptr) {
     if (!d_ptr) return STORMCK_OK;
     int rc = device_check();
     if (rc) return rc;
-#ifndef STORMCK_PROBES
     HIP_TRY(hipFree(d_ptr));
     return STORMCK_OK;
-#else
-    VmmArena a;
-    bool vmm = false;
-    {
-        std::lock_guard<std::mutex> g(g_arena_mu);
-        for (size_t k = 0; k < g_vmm.size(); ++k)
-            if (g_vmm[k].first == d_ptr) {
-                a = std::move(g_vmm[k].second);
-                g_vmm.erase(g_vmm.begin() + static_cast<long>(k));
-                vmm = true;
-                break;
-            }
-    }
-    if (!vmm) {
-        HIP_TRY(hipFree(d_ptr));
-        return STORMCK_OK;
-    }
-    HIP_TRY(hipDeviceSynchronize());  // hipFree's implicit wait: no kernel may still read the arena
-    for (size_t k = 0; k < a.handles.size(); ++k) {
-        HIP_TRY(hipMemUnmap(static_cast<uint8_t*>(d_ptr) + k * a.chunk, a.chunk));
-        HIP_TRY(hipMemRelease(a.handles[k]));
-    }
-    HIP_TRY(hipMemAddressFree(d_ptr, a.size));
-    return STORMCK_OK;
-#endif
 }
 
 int stormck_stream_forget(void* stream) {
@@ -1618,6 +1567,7 @@ int stormck_stream_forget(void* stream) {
 }
 
 void stormck_shutdown(void) {
+    multi_release();
     std::lock_guard<std::mutex> g(g_ctx_mu);
     for (auto& c : g_ctx) {
         if (c) {
@@ -1759,6 +1709,11 @@ int stormck_host_register(void* p, uint64_t bytes) {
     // portable: pinned for every device of the process (stormck_checksum_host_multi DMAs
     // ranges of one registered buffer to several devices)
     HIP_TRY(hipHostRegister(p, bytes, hipHostRegisterMapped | hipHostRegisterPortable));
+    {
+        std::lock_guard<std::mutex> g(g_reg_mu);
+        g_reg.emplace_back(reinterpret_cast<uintptr_t>(p), reinterpret_cast<uintptr_t>(p) + bytes);
+        g_reg_n.store(g_reg.size(), std::memory_order_release);
+    }
     // registered memory is what the device and split legs read: set up the current device's
     // stages now (pinned and device buffers, ~0.3 s once per process) rather than inside the
     // first routed call that splits (storm registers cache.data once, at start-up). Best
@@ -1784,6 +1739,15 @@ int stormck_host_device_pointer(void* p, void** d_p) {
 int stormck_host_unregister(void* p) {
     int rc = device_check();
     if (rc) return rc;
+    {
+        std::lock_guard<std::mutex> g(g_reg_mu);
+        for (size_t k = 0; k < g_reg.size(); ++k)
+            if (g_reg[k].first == reinterpret_cast<uintptr_t>(p)) {
+                g_reg.erase(g_reg.begin() + static_cast<long>(k));
+                break;
+            }
+        g_reg_n.store(g_reg.size(), std::memory_order_release);
+    }
     HIP_TRY(hipHostUnregister(p));
     return STORMCK_OK;
 }
@@ -1937,6 +1901,17 @@ int stormck_merkle_root_device(const uint64_t* d_leaf_cs, uint64_t n, uint64_t l
     hipLaunchKernelGGL(k_set_root, dim3(1), dim3(64), 0, st, cur, addr_base, rev, type, root, d_root_type);
     HIP_TRY(hipGetLastError());
     return STORMCK_OK;
+}
+
+int stormck_shard_plan(uint64_t n_total, uint32_t n_shards, const int* devices, int n_devices, stormck_shard* shards,
+                       uint64_t* root_addr) {
+    return shard_plan(n_total, n_shards, devices, n_devices, shards, root_addr);
+}
+
+int stormck_merkle_root_multi(const stormck_shard* shards, uint32_t n_shards, uint64_t rev, uint64_t root_addr,
+                              uint32_t fanout, stormck_pointer* root, uint8_t* root_type, stormck_pointer* shard_roots,
+                              uint8_t* shard_types) {
+    return merkle_root_multi(shards, n_shards, rev, root_addr, fanout, root, root_type, shard_roots, shard_types);
 }
 
 int stormck_read_verify_fd(int fd, const uint64_t* addresses, const uint32_t* lens, uint64_t n, uint64_t block_size,
@@ -2785,8 +2760,10 @@ unsigned routed_threads(uint32_t host_threads, TimeWith&& time_with) {
 }
 
 // One persistent host thread per device drives that device's part of a split (a thread per
-// call would cost ~30 us to start). A call owns a worker from post() to wait(); a balanced
-// split whose worker another call owns runs without that device.
+// call would cost ~30 us to start). A call owns a worker from acquire() to wait(); a balanced
+// split whose worker another call owns runs without that device. Calls acquire the workers
+// they wait for in ascending device order (split_run), so two fixed-mode calls over the same
+// devices listed in different orders cannot each hold one and wait for the other.
 class DevWorker {
   public:
     static DevWorker* of(int dev) {
@@ -2801,19 +2778,22 @@ class DevWorker {
         if (!table_[dev]) table_[dev] = new DevWorker(dev);  // never destroyed: its thread may be parked at exit
         return table_[dev];
     }
-    bool post(std::function<void()> fn, bool wait_if_busy) {
+    // Take the worker for one call: wait for it, or give up at once if another call owns it.
+    bool acquire(bool wait_if_busy) {
         if (wait_if_busy) {
             own_.lock();
-        } else if (!own_.try_lock()) {
-            return false;
+            return true;
         }
+        return own_.try_lock();
+    }
+    // Run fn on the acquired worker; wait() joins it and releases the worker.
+    void start(std::function<void()> fn) {
         {
             std::lock_guard<std::mutex> g(mu_);
             job_ = std::move(fn);
             pending_ = true;
         }
         cv_.notify_all();
-        return true;
     }
     void wait() {
         {
@@ -2943,7 +2923,7 @@ class SplitQueue {
             if (hi_ <= lo_) return false;
             const uint64_t avail = hi_ - lo_;
             const double R = static_cast<double>(avail) * bpb_;
-            const double r_o = r_host_ + (ndev_ - 1) * r_dev_;
+            const double r_o = r_host_ + (std::max(ndev_, 1u) - 1) * r_dev_;
             const double want = r_o <= 0 ? R : (R / r_o - lat_us - inflight / r_dev_) / (1.0 / r_dev_ + 1.0 / r_o);
             if (want < kSplitMinClaimBytes) return false;
             cnt = std::min<uint64_t>({static_cast<uint64_t>(want / bpb_), max_blocks, avail});
@@ -3176,28 +3156,41 @@ int split_run(SplitArgs& A, const std::vector<int>& devs, unsigned pl, uint64_t 
     pl = std::max(1u, std::min(pl, split_threads(fj, nd)));
     const double r_dev = A.in_place ? rt.link_inplace : rt.link_pinned;
     const double r_host = host_rate(rt, pl, bytes);
-    SplitQueue q(n, nd ? fixed : 0, bpb, r_host, r_dev, nd);
     const double lat = rt.device_latency;
     const double t_post = now_us();
 
+    // the workers this call gets, taken in ascending device order whatever the caller's order
+    // (fixed mode waits for each, so one global order rules out a deadlock between two calls);
+    // balanced: a worker that another call owns is left out (the host takes its share)
     std::vector<DevRun> runs(nd);
-    std::vector<DevWorker*> posted;
-    for (unsigned k = 0; k < nd; ++k) {
+    std::vector<unsigned> order(nd);
+    for (unsigned k = 0; k < nd; ++k) order[k] = k;
+    std::sort(order.begin(), order.end(), [&](unsigned a, unsigned b) { return devs[a] < devs[b]; });
+    std::vector<std::pair<unsigned, DevWorker*>> got;
+    for (unsigned k : order) {
         DevWorker* w = DevWorker::of(devs[k]);
         if (!w) {
             runs[k].rc = STORMCK_EINVAL;
             runs[k].err = "device index beyond 64";
             continue;
         }
+        if (w->acquire(fixed != STORMCK_SPLIT_BALANCED)) got.emplace_back(k, w);
+    }
+    // the queue's balance counts the devices that take part, not the ones listed
+    const unsigned nposted = static_cast<unsigned>(got.size());
+    SplitQueue q(n, nposted ? fixed : 0, bpb, r_host, r_dev, nposted);
+    std::vector<DevWorker*> posted;
+    for (auto& [k, w] : got) {
         DevRun* out = &runs[k];
-        // balanced: a worker that another call owns is left out (the host takes its share)
-        if (w->post([&A, &q, lat, out] { device_part(A, q, lat, out); }, fixed != STORMCK_SPLIT_BALANCED))
-            posted.push_back(w);
+        w->start([&A, &q, lat, out] { device_part(A, q, lat, out); });
+        posted.push_back(w);
     }
 
     // the host part: pieces from the front, small enough near the meeting point to balance
-    const uint64_t want = nd ? static_cast<uint64_t>(static_cast<double>(bytes) / (64.0 * pl) / bpb) : n / (uint64_t{pl} * 8);
-    const uint64_t piece = (std::max<uint64_t>(nd ? 8 : 4, nd ? std::min<uint64_t>(want, 1024) : want) + 3) / 4 * 4;
+    const uint64_t want = nposted ? static_cast<uint64_t>(static_cast<double>(bytes) / (64.0 * pl) / bpb)
+                                  : n / (uint64_t{pl} * 8);
+    const uint64_t piece =
+        (std::max<uint64_t>(nposted ? 8 : 4, nposted ? std::min<uint64_t>(want, 1024) : want) + 3) / 4 * 4;
     std::atomic<uint64_t> host_blocks{0}, host_bytes{0}, bad_n{0}, bad_first{n};
     auto work = [&](unsigned) {
         uint64_t my_n = 0, my_first = n, my_blocks = 0, my_bytes = 0, a = 0, b = 0;
@@ -3224,7 +3217,7 @@ int split_run(SplitArgs& A, const std::vector<int>& devs, unsigned pl, uint64_t 
     };
     const unsigned parts = static_cast<unsigned>(std::min<uint64_t>(pl, (n + piece - 1) / piece));
     const double h0 = now_us();
-    fj.run(parts, work, static_cast<double>(bytes) / (r_host + nd * r_dev));
+    fj.run(parts, work, static_cast<double>(bytes) / (r_host + nposted * r_dev));
     const double h_us = now_us() - h0;
     for (DevWorker* w : posted) w->wait();
     const double t_back = now_us();  // the caller has every device's results
@@ -3338,6 +3331,18 @@ double split_us(double bytes, double r_h, double r_d, double lat, double overhea
 // chunk's staging copy, which nothing overlaps); the split (pinned memory only: from
 // pageable memory the devices need host threads to copy, which hash faster than they copy),
 // the devices reading in place after their start latency.
+// A call one host thread finishes faster than any device can start returning (kHostOnlyUs: a
+// device's start latency is tens of microseconds) is not planned: the routed call takes the
+// host leg on its own thread at once, paying no planning, no device list and no pool
+// (storm's smallest commits, every revision: the singularity, cache/cache.go:64-85).
+bool host_only(const stormck_route_rates& r, double bytes) { return bytes / r.host_thread < kHostOnlyUs; }
+
+LegPlan host_only_plan(const stormck_route_rates& r, double bytes) {
+    LegPlan p;
+    p.us[0] = bytes / r.host_thread;
+    return p;
+}
+
 LegPlan plan_batch(const stormck_route_rates& r, uint64_t n, const BatchShape& s, bool pinned, bool staged_ok,
                    unsigned nt, unsigned ndev) {
     LegPlan p;
@@ -3625,10 +3630,10 @@ int batch_routed(const void* base, uint64_t stride, const uint32_t* lens, uint32
     }
     const Mem mem = classify(base, (n - 1) * stride + (lens ? lens[n - 1] : len));
     if (mem == Mem::kDevice || mem == Mem::kUnreadable) return not_host_memory(mem);
-    // A batch that one host thread hashes faster than any device can start returning
-    // (its start latency, tens of microseconds) takes the host leg without planning.
+    // a batch that one host thread hashes faster than any device can start returning takes
+    // the host leg without planning (host_only)
     const stormck_route_rates rt = RouteModel::get().now();
-    if (static_cast<double>(s.bytes) / rt.host_thread < kHostOnlyUs) {
+    if (host_only(rt, static_cast<double>(s.bytes))) {
         if (leg_used) *leg_used = STORMCK_LEG_HOST;
         return batch_host_leg(base, stride, lens, len, n, out, expected, first_bad, n_bad, 1, true);
     }
@@ -3752,13 +3757,12 @@ int stormck_commit(void* arena, stormck_dirty_block* blocks, uint64_t n, uint64_
     if (mem == Mem::kUnreadable) return not_host_memory(mem);
     const bool registered = mem == Mem::kMapped;
     // a forest one host thread hashes faster than any device can start returning (storm's
-    // smallest commits: a few blocks) takes the host leg without planning
+    // smallest commits: a few blocks) takes the host leg without planning (host_only)
     const stormck_route_rates rt = RouteModel::get().now();
     {
         uint64_t total = 0;
-        for (uint64_t i = 0; i < n && static_cast<double>(total) / rt.host_thread < kHostOnlyUs; ++i)
-            total += blocks[i].length;
-        if (static_cast<double>(total) / rt.host_thread < kHostOnlyUs) {
+        for (uint64_t i = 0; i < n && host_only(rt, static_cast<double>(total)); ++i) total += blocks[i].length;
+        if (host_only(rt, static_cast<double>(total))) {
             if (leg_used) *leg_used = STORMCK_LEG_HOST;
             if (registered) {
                 rc = stream_drained(static_cast<hipStream_t>(stream));
@@ -3894,8 +3898,10 @@ int stormck_route_plan_batch(uint64_t stride, const uint32_t* lens, uint32_t len
     if (!batch_shape(stride, lens, len, n, &s)) return fail(STORMCK_EINVAL, "stride smaller than a block length (blocks overlap)");
     const unsigned nt = host_threads ? std::min<unsigned>(host_threads, ForkJoin::get().size()) : ForkJoin::get().size();
     const uint64_t step = n == 1 ? std::max<uint64_t>(s.longest, 8) : std::max<uint64_t>(stride, 8);
-    const LegPlan p = plan_batch(RouteModel::get().now(), n, s, memory == STORMCK_MEM_PINNED, step <= kChunkBytes, nt,
-                                 n_devices);
+    const stormck_route_rates rt = RouteModel::get().now();
+    const LegPlan p = host_only(rt, static_cast<double>(s.bytes))
+                          ? host_only_plan(rt, static_cast<double>(s.bytes))
+                          : plan_batch(rt, n, s, memory == STORMCK_MEM_PINNED, step <= kChunkBytes, nt, n_devices);
     *leg = n ? p.leg : STORMCK_LEG_NONE;
     if (predicted_us) std::memcpy(predicted_us, p.us, sizeof p.us);
     return STORMCK_OK;
@@ -3909,7 +3915,11 @@ int stormck_route_plan_commit(const stormck_dirty_block* blocks, uint64_t n, uin
     CommitShape shape;
     if (!commit_shape(blocks, n, &shape)) return fail(STORMCK_EINVAL, "malformed forest (parent range or cycle)");
     const unsigned nt = host_threads ? std::min<unsigned>(host_threads, ForkJoin::get().size()) : ForkJoin::get().size();
-    const LegPlan p = plan_commit(RouteModel::get().now(), shape, memory == STORMCK_MEM_PINNED, nt, n_devices);
+    const stormck_route_rates rt = RouteModel::get().now();
+    double total = 0;
+    for (uint64_t b : shape.bytes) total += static_cast<double>(b);
+    const LegPlan p = host_only(rt, total) ? host_only_plan(rt, total)
+                                           : plan_commit(rt, shape, memory == STORMCK_MEM_PINNED, nt, n_devices);
     *leg = n ? p.leg : STORMCK_LEG_NONE;
     if (predicted_us) std::memcpy(predicted_us, p.us, sizeof p.us);
     return STORMCK_OK;

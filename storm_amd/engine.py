@@ -152,9 +152,9 @@ def device_alloc(nbytes: int) -> int:
 
 def device_alloc_placed(nbytes: int, mode: int, chunk_bytes: int = 0) -> Tuple[int, int]:
     """Probe build only (STORMCK_LIBRARY=tools/libstormck_probes.so): a block arena in
-    placement `mode` (_lib.ALLOC_PLAIN / ALLOC_VMM / ALLOC_CONTIGUOUS), the modes measured
-    and rejected in round 4; returns (device pointer, physical chunk bytes of a VMM arena,
-    else 0). The product library allocates with hipMalloc only (device_alloc)."""
+    placement `mode` (_lib.ALLOC_PLAIN / ALLOC_CONTIGUOUS), the modes measured and rejected
+    in round 4; returns (device pointer, 0). The product library allocates with hipMalloc
+    only (device_alloc). The VMM mode was deleted in round 6."""
     import ctypes
     if not hasattr(lib, "stormck_device_alloc_placed"):
         if mode == _lib.ALLOC_PLAIN:

@@ -38,9 +38,20 @@ def _rank_worker():
             rows = [tuple(int(v) for v in row) for row in table.numpy().view(np.uint64)]
             return o.combine_roots(rows, rev_, addr, fanout)
 
+        t0 = time.perf_counter()
         groot, _ = sdist.global_root(local, rev, n_total, combine)
+        # the N > 1 line's rank summary and scaling fields, through bench.py's own helpers
+        # (per-rank stats all-gathered over gloo here, RCCL on GPUs); the "kernel" times are
+        # this rank's shard-root time
+        el = time.perf_counter() - t0 + 1e-3 * (rank + 1)
+        rows = bench.gather_rank_rows(el, el + 1e-3, [el * 1e3, el * 5e2], rank, hi - lo, "cpu")
+        line = None
+        if rank == 0:
+            elapsed, wall, ranks = bench.summarize_ranks(rows, 1)
+            value = n_total * bench.BLOCK / elapsed / 2**30
+            line = {"value": value, "ranks": ranks, **bench.scaling_reference(world, n_total, ranks, value, "strong")}
         with open(os.path.join(os.environ["SPAWN_TEST_OUT"], f"rank{rank}.json"), "w") as f:
-            json.dump({"rank": rank, "world": world, "root": [int(v) for v in groot]}, f)
+            json.dump({"rank": rank, "world": world, "root": [int(v) for v in groot], "line": line}, f)
     finally:
         dist.destroy_process_group()
 
@@ -72,6 +83,19 @@ def test_spawned_ranks_agree_on_the_combine_fixture(tmp_path, monkeypatch):
         with open(tmp_path / f"rank{r}.json") as f:
             got = json.load(f)
         assert got["world"] == world and got["root"] == want
+        if r == 0:
+            line = got["line"]
+    # the N > 1 line says which N = 1 number it reads against (verdict r05 item 3)
+    n_total = g["n_total"]
+    per = line["ranks"]["per_rank"]
+    assert [p["rank"] for p in per] == list(range(world))
+    assert sum(p["blocks"] for p in per) == n_total
+    slow = per[line["ranks"]["slowest_rank"]]
+    assert slow["ms_per_step"] == max(p["ms_per_step"] for p in per)
+    assert line["per_gpu_GiB_s"] == round(line["value"] / world, 2)
+    ref = line["scaling_reference"]
+    assert "per_gpu_GiB_s" in ref["read_against"] and "c3" in ref["driver_n1_line"]
+    assert ref["strong_scaling_n1_ms_per_step_estimate"] == round(slow["ms_per_step"] / slow["blocks"] * n_total, 3)
 
 
 @pytest.mark.timeout(120)

@@ -96,3 +96,21 @@ def test_c3_root_of_the_first_16m_blocks(dev, c4_checksums):
     root = engine.merkle_root_tensor(c4_checksums[:fx["n"]], fx["leaf_addr_base"], fx["node_addr_base"], REV, FANOUT)
     torch.cuda.synchronize()
     assert _row(root) == fx["root"]
+
+
+@pytest.mark.parametrize("world", [1, 2, 4, 8])
+def test_c4_roots_through_the_c_abi_multi_entry(dev, c4_checksums, world):
+    """The one-process multi-GPU entry (stormck_merkle_root_multi, what storm's cgo shim
+    calls) with device list [0]: the planned shards' trees over slices of the 64M checksums,
+    the RCCL gather (a one-rank communicator here) and the device combine reproduce the c4
+    world-N shard roots and global root (world 1: the strong-scaling N = 1 point)."""
+    from storm_amd import multi
+    fx = load_golden("c3c4_roots.json")["c4"]
+    want = fx["worlds"][str(world)]
+    shards, root_addr = multi.plan(fx["n_total"], world, [0])
+    for sh in shards:
+        multi.set_buffers(sh, c4_checksums[sh.leaf_addr_base:].data_ptr())
+    root, rows = multi.merkle_root_multi(shards, REV, root_addr, FANOUT)
+    fmt = lambda r: ["0x%016x" % v for v in r[:3]] + [r[3]]  # noqa: E731
+    assert [fmt(r) for r in rows] == want["shard_roots"]
+    assert fmt(root) == want["global_root"]

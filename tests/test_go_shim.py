@@ -262,3 +262,34 @@ def test_batches_take_the_routed_batch():
     assert "C.stormck_checksum_host(bytesPtr(data)" in _go_func(text, "ChecksumBatchGPU")
     assert "C.stormck_checksum_host_multi(" in _go_func(text, "ChecksumBatchDevices")
     assert re.search(r"var BatchHostThreads uint32", text)
+
+
+def test_go_shard_has_the_c_layout_and_the_multi_entries_bind_it():
+    """The one-process multi-GPU entries (stormck_shard_plan / stormck_merkle_root_multi):
+    the Go Shard mirrors stormck_shard field by field (sizes and order; 64 bytes), and the
+    shim's PlanShards / MerkleRootDevices pass the shard slice, the root and the shard roots
+    through the C types."""
+    text = open(SHIM).read()
+    body = re.search(r"type Shard struct \{(.*?)\n\}", text, flags=re.S).group(1)
+    go_sizes = {"uintptr": 8, "uint64": 8, "BlockAddress": 8, "int32": 4, "uint32": 4}
+    go = []
+    for line in body.strip().splitlines():
+        line = line.split("//")[0].strip()
+        if line:
+            name, typ = line.split()[:2]
+            go.append((name, go_sizes[typ]))
+    hdr = _strip_c_comments(open(HEADER).read())
+    cbody = re.search(r"typedef struct stormck_shard \{(.*?)\}", hdr, flags=re.S).group(1)
+    c = []
+    for decl in cbody.split(";"):
+        decl = decl.strip()
+        if decl:
+            name = decl.replace("*", " ").split()[-1]
+            c.append((name, 8 if "*" in decl else dict(_C_SIZES, int32_t=4)[decl.split()[0]]))
+    assert [s for _, s in go] == [s for _, s in c] and sum(s for _, s in c) == 64
+    assert [n.lower() for n, _ in go] == [re.sub(r"^d_", "", n).replace("_", "") for n, _ in c]
+    plan = _go_func(text, "PlanShards")
+    assert "C.stormck_shard_plan(" in plan and "(*C.stormck_shard)(unsafe.Pointer(&shards[0]))" in plan
+    root = _go_func(text, "MerkleRootDevices")
+    assert "C.stormck_merkle_root_multi((*C.stormck_shard)(unsafe.Pointer(&shards[0]))" in root
+    assert "C.STORMCK_POINTERS_PER_BLOCK" in root and "(*C.stormck_pointer)(unsafe.Pointer(&root))" in root

@@ -968,24 +968,17 @@ torch.cuda.init()
 engine.init(0)
 n, stride = 12288, 32768
 want = o.checksum_batch(o.fill_synthetic(n, stride, 7), n, stride, stride, threads=8)
-for mode, chunk in ((1, 0), (1, 1 << 21), (2, 0), (0, 0)):
-    ptr, mapped = engine.device_alloc_placed(n * stride, mode, chunk)
+for mode in (2, 0):
+    ptr, mapped = engine.device_alloc_placed(n * stride, mode)
     try:
-        assert ptr % 4096 == 0
-        if mode == 1:
-            assert mapped >= (chunk or n * stride) and mapped % 4096 == 0
-        else:
-            assert mapped == 0
+        assert ptr % 4096 == 0 and mapped == 0
         engine.fill_synthetic_device(ptr, stride, n, 7, o.SYNTH_SEED)
         out = torch.empty(n, dtype=torch.int64, device="cuda")
         engine.checksum_device(ptr, stride, n, out.data_ptr(), stride)
         torch.cuda.synchronize()
         got = out.cpu().numpy().view(np.uint64)
         bad = np.nonzero(got != want)[0]
-        if mode == 1 and bad.size:  # the rejected VMM variant's known defect: reported
-            print("vmm_bad chunk=%d blocks=%d first=%d last=%d" % (chunk, bad.size, bad[0], bad[-1]))
-        else:
-            assert bad.size == 0, (mode, chunk, bad.size, bad[:8])
+        assert bad.size == 0, (mode, bad.size, bad[:8])
         # the routed entries know the arena for device memory: the batch refuses it, the
         # commit takes the device leg (host threads never dereference it)
         cs = np.zeros(4, dtype=np.uint64)
@@ -998,8 +991,7 @@ for mode, chunk in ((1, 0), (1, 1 << 21), (2, 0), (0, 0)):
         got, last_got, leg = sc.commit(ptr, b, 1, last)
         assert leg == _lib.LEG_DEVICE and last_got == last_ref, mode
         assert np.array_equal(b, b_ref)
-        if not (mode == 1 and bad.size):
-            assert np.array_equal(got, cs_ref), mode
+        assert np.array_equal(got, cs_ref), mode
     finally:
         engine.device_free(ptr)
 print("placement modes ok")
@@ -1008,14 +1000,12 @@ print("placement modes ok")
 
 def test_arena_placement_modes_probe_build(dev):
     """The arena placement modes measured and rejected in round 4 (stormck_device_alloc_placed:
-    plain hipMalloc, a VMM reservation with one or several physical allocations, a contiguous
-    allocation; DESIGN_LOG.md) live in the probe build only. Through it, in a child process:
-    a 384 MiB arena in the plain and contiguous modes hashes like the oracle through the
-    LDS-DMA kernel and frees cleanly; a VMM arena's chunk is reported; and the routed entry
-    points recognise every mode's arena as device memory (the batch refuses it, the commit
-    takes the device leg and matches the oracle) rather than handing it to host threads.
-    A VMM arena that hashes wrong blocks (the round-4 defect, seen again on one box in
-    round 5) marks the test xfail with the blocks named."""
+    plain hipMalloc and a contiguous allocation; DESIGN_LOG.md) live in the probe build only.
+    Through it, in a child process: a 384 MiB arena in either mode hashes like the oracle
+    through the LDS-DMA kernel and frees cleanly, and the routed entry points recognise the
+    arena as device memory (the batch refuses it, the commit takes the device leg and
+    matches the oracle) rather than handing it to host threads. Any wrong checksum fails.
+    (The VMM mode was deleted in round 6: it twice read wrong blocks and served no purpose.)"""
     import subprocess
     import sys
     from storm_amd import build as sb
@@ -1024,10 +1014,4 @@ def test_arena_placement_modes_probe_build(dev):
     r = subprocess.run([sys.executable, "-c", PLACEMENT_CHILD, ROOT], cwd=ROOT, capture_output=True, text=True,
                        env=env, timeout=300)
     assert r.returncode == 0 and "placement modes ok" in r.stdout, r.stdout + r.stderr
-    vmm_bad = [ln for ln in r.stdout.splitlines() if ln.startswith("vmm_bad")]
-    if vmm_bad:
-        # plain and contiguous arenas were exact, and every mode routed as device memory;
-        # the VMM arena read wrong blocks, the defect that took it out of the product in
-        # round 5 (it passes on most boxes). Not a product path.
-        pytest.xfail("VMM arena (probe build only) read wrong blocks: " + "; ".join(vmm_bad))
 

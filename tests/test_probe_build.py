@@ -61,9 +61,10 @@ def test_probe_build_is_the_larger_one():
 
 
 def test_product_library_has_one_allocation_mode():
-    """The arena placement modes (VMM reservations, contiguous allocations) were measured no
-    better than hipMalloc in round 4 and live in the probe build only: the product neither
-    exports stormck_device_alloc_placed nor imports the HIP VMM API."""
+    """The arena placement modes (contiguous allocations; VMM reservations until round 6) were
+    measured no better than hipMalloc in round 4 and live in the probe build only: the product
+    neither exports stormck_device_alloc_placed nor imports the HIP VMM API, and the probe
+    build no longer carries the VMM mode, which twice read wrong blocks."""
     import ctypes
     from storm_amd import build as sb
     lib = ctypes.CDLL(_product())
@@ -72,4 +73,6 @@ def test_product_library_has_one_allocation_mode():
     for sym in (b"hipMemCreate", b"hipMemAddressReserve", b"hipMemMap", b"hipExtMallocWithFlags"):
         assert sym not in data, sym
     probes = open(sb.PROBES_LIB, "rb").read()
-    assert b"hipMemCreate" in probes and b"stormck_device_alloc_placed" in probes
+    assert b"stormck_device_alloc_placed" in probes and b"hipExtMallocWithFlags" in probes
+    for sym in (b"hipMemCreate", b"hipMemAddressReserve", b"hipMemMap"):
+        assert sym not in probes, sym

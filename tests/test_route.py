@@ -272,3 +272,30 @@ def test_pool_pass_below_the_threads_rate_measures_the_pool_cap():
         assert got["host_memory"] == 1.0
     finally:
         blocks.SetRouteRates(None)
+
+
+def test_tiny_calls_are_not_planned(rates):
+    """A call one host thread finishes in under 10 us (kHostOnlyUs) takes the host leg on the
+    caller's thread without planning (storm commits at least the singularity every revision,
+    /root/reference/cache/cache.go:64-85): the plan entries report exactly that decision, the
+    host time bytes / host_thread and no device or split time. Slow the host thread down and
+    the same calls are planned again."""
+    three = _forest(2, 31808)                       # 2 objectlist leaves + their pointer block
+    tag = sc.pointer_forest(100, np.array([536, 728] * 50, dtype=np.uint32), 10, slot=32768, revision=1)[0]
+    for forest in (three, tag):
+        total = float(forest["length"].sum())
+        assert total / RATES["host_thread"] < 10.0
+        leg, us = sc.plan_commit(forest, registered=True)
+        assert leg == _lib.LEG_HOST and us[0] == pytest.approx(total / RATES["host_thread"]), us
+        assert math.isinf(us[1]) and math.isinf(us[2])
+        leg, us = blocks.PlanBatch(len(forest), 32768, lens=list(forest["length"]), pinned=True)
+        assert leg == _lib.LEG_HOST and us[0] == pytest.approx(total / RATES["host_thread"]) and math.isinf(us[1])
+        rates(host_thread=total / 50.0)             # 50 us on one thread: planned
+        leg, us = sc.plan_commit(forest, registered=True)
+        assert math.isfinite(us[1]), us
+        leg, us = blocks.PlanBatch(len(forest), 32768, lens=list(forest["length"]), pinned=True)
+        assert math.isfinite(us[1]), us
+        rates(host_thread=total / 10.0)             # exactly 10 us: planned (the bound is strict)
+        leg, us = sc.plan_commit(forest, registered=True)
+        assert math.isfinite(us[1]), us
+        rates()

@@ -12,7 +12,7 @@ import pytest
 from tests.conftest import ROOT
 
 SAN = os.path.join(ROOT, "tests", "sanitize")
-SOURCES = [os.path.join(ROOT, "storm_amd", "csrc", f) for f in ("stormck.hip", "kernels.h", "xxh64_dev.h", "xxh64_host.h")]
+SOURCES = [os.path.join(ROOT, "storm_amd", "csrc", f) for f in ("stormck.hip", "kernels.h", "multi_root.h", "xxh64_dev.h", "xxh64_host.h")]
 SOURCES += [os.path.join(SAN, "host_paths.cpp"), os.path.join(SAN, "build.sh"), os.path.join(ROOT, "include", "stormck.h"),
             os.path.join(ROOT, "oracle", "xxh64_oracle.c")]
 ENV = {"asan": {"ASAN_OPTIONS": "detect_leaks=1:halt_on_error=1:abort_on_error=0",

@@ -13,6 +13,9 @@
 #   bench                  the default bench line (c3, BASELINE metric)
 #   batch_e2e commit_e2e gather c5 commit keytags
 #                          bench.py --workload <step> --steps 7
+#   inproc                 bench.py --in-process at N = 1 on c4 (all 64M blocks, one device):
+#                          the strong-scaling N = 1 point, through stormck_merkle_root_multi
+#   overhead               tools/route_overhead: the routed calls' fixed cost in C
 #   placement              8 fresh plain c3 processes (bench.py --steps 5 --no-cpu): the spread
 #                          of the line's frac with where each arena lands in HBM
 #   prof                   tools/profile.sh <tag>: fresh plain c3 processes, the bench under
@@ -46,6 +49,13 @@ for step in "$@"; do
         batch_e2e|commit_e2e|gather|c5|commit|keytags)
             timeout -k 10 900 python bench.py --workload "$step" --steps 7 > "$out/$step.log" 2>&1; rc=$?
             tail -c 300 "$out/$step.log"; echo ;;
+        inproc)
+            timeout -k 10 600 python bench.py --in-process --gpus 1 --total-blocks 67108864 --steps 3 --warmup 1 \
+                --no-cpu > "$out/inproc.log" 2>&1; rc=$?
+            tail -c 400 "$out/inproc.log"; echo ;;
+        overhead)
+            timeout -k 10 300 ./tools/route_overhead > "$out/route_overhead.log" 2>&1; rc=$?
+            grep -E "commit|batch" "$out/route_overhead.log" | head -6 ;;
         placement)
             rc=0
             for i in 1 2 3 4 5 6 7 8; do
