@@ -392,6 +392,24 @@ def c5_workload(a):
     return rc
 
 
+def calltimer():
+    """tools/libcalltimer.so (storm_amd/build.py build_calltimer): the E2E tables time calls
+    of under 1 MiB in a C loop, so a leg's column is what the call costs and not what
+    Python's ctypes adds per argument (cgo, storm's binding, costs the same per call
+    whatever the argument count). None if not built (then Python's loop is used)."""
+    import ctypes
+    from storm_amd import build as sb
+    if not os.path.exists(sb.CALLTIMER):
+        return None
+    lib = ctypes.CDLL(sb.CALLTIMER)
+    P, U64, U32, I = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int
+    lib.calltimer_commit.restype = ctypes.c_double
+    lib.calltimer_commit.argtypes = [I, P, P, U64, U64, U64, P, U32, I, P, P, P, P]
+    lib.calltimer_batch.restype = ctypes.c_double
+    lib.calltimer_batch.argtypes = [I, P, U64, P, U32, U64, P, U32, I, P, P, P]
+    return lib
+
+
 def balanced_orders(names):
     """Orders of the legs in which each leg follows every other leg equally often (a Williams
     design: len(names) orders for an even count, twice that for an odd one, each leg once
@@ -457,6 +475,7 @@ def commit_e2e_workload(a):
     threads = host_cpu_info()["usable_cpus"]
     reps = max(3, a.steps)
     rows = []
+    ct = calltimer()
     for name, nl, lens, fan in shapes:
         b0, size, last = sc.pointer_forest(nl, lens, fan, slot=BLOCK, revision=REV)
         pages = (size + 4095) // 4096 * 4096
@@ -484,6 +503,19 @@ def commit_e2e_workload(a):
             la = ctypes.c_uint64(last)
             bp, op, nb = b.ctypes.data, out.ctypes.data, len(b)
             done, used = ctypes.c_uint64(0), ctypes.c_uint32(9)
+            if inner > 1 and ct is not None:  # a few microseconds: the C loop
+                code = {"dev_inplace": 0, "dev_hbm": 0, "host_1": 1, "host_all": 1, "split": 2, "split_1": 2}.get(leg, 3)
+                ap = d_host.value if leg == "dev_inplace" else (hbm.data_ptr() if leg == "dev_hbm" else arena_p)
+                nt = threads if leg == "host_all" else (1 if leg.endswith("_1") else 0)
+                rc_ = ctypes.c_int(0)
+                dt = ct.calltimer_commit(code, ap, bp, nb, REV, last, op, nt, inner, ctypes.byref(rc_),
+                                         ctypes.byref(used), ctypes.byref(done), ctypes.byref(la)) * 1e-6
+                _lib.check(rc_.value)
+                if leg in ("split", "split_1"):
+                    shares.setdefault(leg, []).append(done.value / nl)
+                elif leg.startswith("routed"):
+                    outs[leg + "_leg"] = int(used.value)
+                return dt, out
             # every pointer argument is converted outside the clock, so the Python columns
             # differ by the calls' own costs (and ctypes' per-argument cost), not by byref()s
             pla, pdone, pused = ctypes.byref(la), ctypes.byref(done), ctypes.byref(used)
@@ -518,7 +550,8 @@ def commit_e2e_workload(a):
                 outs[leg + "_leg"] = int(used.value)
             return dt, out
 
-        row = {"forest": name, "blocks": int(len(b0)), "leaves": nl, "hashed_bytes": bytes_hashed}
+        row = {"forest": name, "blocks": int(len(b0)), "leaves": nl, "hashed_bytes": bytes_hashed,
+               "timed_in": "C loop (tools/libcalltimer.so)" if inner > 1 and ct is not None else "Python"}
         shares = {}
         names = ("dev_inplace", "dev_hbm", "host_1", "host_all", "split", "split_1", "routed", "routed_1")
         ts = {leg: [] for leg in names}
@@ -536,7 +569,7 @@ def commit_e2e_workload(a):
                 outs[leg] = out
         for leg in names:
             med = sorted(ts[leg])[len(ts[leg]) // 2]
-            row[leg + "_us"] = round(med * 1e6, 1)
+            row[leg + "_us"] = round(med * 1e6, 3 if med < 1e-4 else 1)  # ns for calls of a few us
             row[leg + "_GiBps"] = round(bytes_hashed / med / 2**30, 2)
         for k in ("routed_leg", "routed_1_leg"):
             row[k] = _lib.LEG_NAMES.get(outs.get(k), outs.get(k))
@@ -624,6 +657,7 @@ def batch_e2e_workload(a):
     threads = host_cpu_info()["usable_cpus"]
     reps = max(3, a.steps)
     rows = []
+    ct = calltimer()
     for name, n, lens in shapes:
         stride = BLOCK
         # the same blocks twice: pageable (the pageable legs) and registered (the rest), so
@@ -653,6 +687,18 @@ def batch_e2e_workload(a):
             bp = pg_p if leg in ("dev", "host_1", "host_all", "routed", "routed_1") else reg_p
             done, used = ctypes.c_uint64(0), ctypes.c_uint32(9)
             pdone, pused = ctypes.byref(done), ctypes.byref(used)  # converted outside the clock
+            if inner > 1 and ct is not None and leg != "routed_x2":  # a few microseconds: the C loop
+                code = 0 if leg.startswith("dev") else 1 if leg.startswith("host") else 2 if leg.startswith("split") else 3
+                nt = threads if leg.startswith("host_all") else (1 if leg.endswith("_1") or leg.startswith("host_1") else 0)
+                rc_ = ctypes.c_int(0)
+                dt = ct.calltimer_batch(code, bp, stride, lp, ln, n, op, nt, inner, ctypes.byref(rc_), pused,
+                                        pdone) * 1e-6
+                _lib.check(rc_.value)
+                if leg in ("split", "split_1"):
+                    shares.setdefault(leg, []).append(done.value / n)
+                elif leg.startswith("routed"):
+                    legs[leg] = _lib.LEG_NAMES.get(int(used.value), int(used.value))
+                return dt, out
             if leg in ("dev", "dev_reg"):
                 def f():
                     return L.stormck_checksum_host(bp, stride, lp, ln, n, op)
@@ -704,7 +750,8 @@ def batch_e2e_workload(a):
                 legs[leg] = _lib.LEG_NAMES.get(int(used.value), int(used.value))
             return dt, out
 
-        row = {"batch": name, "blocks": n, "hashed_bytes": hashed}
+        row = {"batch": name, "blocks": n, "hashed_bytes": hashed,
+               "timed_in": "C loop (tools/libcalltimer.so)" if inner > 1 and ct is not None else "Python"}
         shares = {}
         names = ["dev", "host_1", "host_all", "routed", "routed_1", "dev_reg", "host_1_reg", "host_all_reg", "split",
                  "split_1", "routed_reg",
@@ -721,7 +768,7 @@ def batch_e2e_workload(a):
                 outs[leg] = out
         for leg in names:
             med = sorted(ts[leg])[len(ts[leg]) // 2]
-            row[leg + "_us"] = round(med * 1e6, 1)
+            row[leg + "_us"] = round(med * 1e6, 3 if med < 1e-4 else 1)  # ns for calls of a few us
             row[leg + "_GiBps"] = round(hashed / med / 2**30, 2)
         _lib.check(L.stormck_host_unregister(reg.ctypes.data))
         for k in ("routed", "routed_1", "routed_reg", "routed_reg_1"):

@@ -27,6 +27,7 @@
 #include <stdexcept>
 #include <string>
 #include <type_traits>
+#include <utility>
 #include <vector>
 
 #include "stormck.h"
@@ -204,6 +205,37 @@ inline stormck_route_rates RouteRates() {
 }
 inline void RouteDevices(const std::vector<int>& devices) {
     detail::check(stormck_route_devices(devices.empty() ? nullptr : devices.data(), static_cast<int>(devices.size())));
+}
+
+// One process, several GPUs (stormck_shard_plan / stormck_merkle_root_multi): n_total leaves
+// dealt into n_shards contiguous shards over `devices`; the caller fills each shard's device
+// buffers (d_blocks / stride / len / d_checksums / stream). Returns the shards and the
+// combining node's address.
+inline std::pair<std::vector<stormck_shard>, BlockAddress> PlanShards(uint64_t n_total, uint32_t n_shards,
+                                                                      const std::vector<int>& devices) {
+    std::vector<stormck_shard> shards(n_shards);
+    uint64_t root_addr = 0;
+    detail::check(stormck_shard_plan(n_total, n_shards, devices.data(), static_cast<int>(devices.size()),
+                                     shards.data(), &root_addr));
+    return {shards, root_addr};
+}
+
+// Every shard's checksums (when d_blocks is set) and tree on its device, the shard roots
+// gathered over xGMI by in-process RCCL, the combining pointer block hashed on every device.
+struct MultiRoot {
+    Pointer root;  // {checksum, root_addr, revision}, of type Pointer
+    std::vector<Pointer> shard_roots;
+    std::vector<BlockType> shard_types;
+};
+inline MultiRoot MerkleRootDevices(const std::vector<stormck_shard>& shards, uint64_t revision, BlockAddress root_addr,
+                                   uint32_t fanout = STORMCK_POINTERS_PER_BLOCK) {
+    MultiRoot r{{}, std::vector<Pointer>(shards.size()), std::vector<BlockType>(shards.size())};
+    uint8_t type = 0;
+    detail::check(stormck_merkle_root_multi(shards.data(), static_cast<uint32_t>(shards.size()), revision, root_addr,
+                                            fanout, reinterpret_cast<stormck_pointer*>(&r.root), &type,
+                                            reinterpret_cast<stormck_pointer*>(r.shard_roots.data()),
+                                            reinterpret_cast<uint8_t*>(r.shard_types.data())));
+    return r;
 }
 
 // The device leg alone (stormck_checksum_host: H2D, kernel, D2H pipelined).

@@ -381,8 +381,12 @@ int stormck_commit_host(void* arena, stormck_dirty_block* blocks, uint64_t n, ui
  * device leg in place over the link, the host leg on host_threads threads (0 = the pool),
  * or the split (stormck_commit_split: the leaves on both at once). An unregistered host
  * arena is out of the devices' reach and takes the host leg. Before a host or split leg
- * reads a registered arena, `stream` is synchronised (device writes queued on it land
- * first). *leg_used (optional) = STORMCK_LEG_HOST / _DEVICE / _SPLIT. Needs a gfx950 device
+ * reads a registered arena, a non-NULL `stream` is synchronised (device writes the caller
+ * queued on it land first). With `stream` NULL those legs wait for nothing: storm writes
+ * cache.data on the host only (the Go binding passes nil), and the query would be most of
+ * the routed call's cost on its smallest commits; a caller whose null-stream work writes the
+ * arena synchronises it first (the device leg itself launches on the null stream then).
+ * *leg_used (optional) = STORMCK_LEG_HOST / _DEVICE / _SPLIT. Needs a gfx950 device
  * like every batched entry point (STORMCK_ENODEV without one). */
 #define STORMCK_LEG_NONE 0u
 #define STORMCK_LEG_HOST 1u

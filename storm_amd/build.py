@@ -101,6 +101,20 @@ def build_oracle(force: bool = False) -> str:
     return out
 
 
+CALLTIMER = os.path.join(ROOT, "tools", "libcalltimer.so")  # bench.py's C timing loop for us-scale calls
+
+
+def build_calltimer(force: bool = False) -> str:
+    """tools/libcalltimer.so: storm-sized calls timed in a C loop (tools/calltimer.cpp;
+    measurement only, links the product library)."""
+    src = os.path.join(ROOT, "tools", "calltimer.cpp")
+    if force or not _newer(CALLTIMER, [src, LIB]):
+        subprocess.run(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-I", os.path.join(ROOT, "include"), src,
+                        "-L", LIB_DIR, "-lstormck", "-Wl,-rpath,$ORIGIN/../storm_amd/lib", "-o", CALLTIMER],
+                       check=True)
+    return CALLTIMER
+
+
 PROBES = ("probe", "probe_keys", "probe_small", "alloc_probe", "phase_probe", "span_probe", "clock_probe")  # tools/<name>.hip: design probes
 SANITIZE = os.path.join(ROOT, "tests", "sanitize")
 READPEAK = os.path.join(ROOT, "tools", "libreadpeak.so")  # bench.py's measured read peak (not product)
@@ -133,6 +147,13 @@ def build_probe(force: bool = False) -> str:
     if force or not _newer(out, [src, LIB]):
         subprocess.run(["g++", "-O2", "-std=c++17", "-I", os.path.join(ROOT, "include"), src, "-L", LIB_DIR,
                         "-lstormck", "-Wl,-rpath,$ORIGIN/../storm_amd/lib", "-o", out], check=True)
+    built.append(out)
+    # tools/route_overhead.cpp: the routed calls' fixed cost in C (links the library)
+    out = os.path.join(ROOT, "tools", "route_overhead")
+    src = os.path.join(ROOT, "tools", "route_overhead.cpp")
+    if force or not _newer(out, [src, LIB]):
+        subprocess.run([hipcc(), "-O2", "-std=c++17", "-I", os.path.join(ROOT, "include"), src, "-L", LIB_DIR,
+                        "-lstormck", "-Wl,-rpath,$ORIGIN/../storm_amd/lib", "-pthread", "-o", out], check=True)
     built.append(out)
     return " ".join(built)
 

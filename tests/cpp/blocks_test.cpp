@@ -268,6 +268,39 @@ static std::string zero_cs() {
     return hex(BlockChecksum(b.get()));
 }
 
+// The one-process multi-GPU root through the mirror: 4 shards of 5,000 synthetic 4 KiB blocks
+// (logical blocks 0..19,999, stormck_fill_synthetic_device) on device 0, hashed, treed,
+// gathered through a one-rank RCCL communicator and combined; tests/test_cpp_mirror.py checks
+// the roots against the oracle.
+static std::string TestMerkleRootDevices() {
+    const uint64_t n_total = 20000, stride = 4096;
+    auto [shards, root_addr] = PlanShards(n_total, 4, {0});
+    EXPECT(root_addr == 2 * n_total && shards.size() == 4);
+    void* blocks = nullptr;
+    void* cs = nullptr;
+    detail::check(stormck_device_alloc(n_total * stride, &blocks));
+    detail::check(stormck_device_alloc(n_total * 8, &cs));
+    detail::check(stormck_fill_synthetic_device(blocks, stride, n_total, 0, 0x53544F524DULL, nullptr));
+    detail::check(stormck_device_status(nullptr));  // the fill (null stream) has landed
+    for (stormck_shard& sh : shards) {
+        sh.d_blocks = static_cast<uint8_t*>(blocks) + sh.leaf_addr_base * stride;
+        sh.stride = stride;
+        sh.len = static_cast<uint32_t>(stride);
+        sh.d_checksums = static_cast<uint64_t*>(cs) + sh.leaf_addr_base;
+    }
+    const MultiRoot r = MerkleRootDevices(shards, 1, root_addr);
+    EXPECT(r.root.Address == root_addr && r.root.BirthRevision == 1);
+    std::string out = "{\"root\": " + hex(r.root.Checksum) + ", \"shard_roots\": [";
+    for (size_t k = 0; k < r.shard_roots.size(); ++k) {
+        EXPECT(r.shard_types[k] == LeafBlockType || r.shard_types[k] == PointerBlockType);
+        out += (k ? ", [" : "[") + hex(r.shard_roots[k].Checksum) + ", " + std::to_string(r.shard_roots[k].Address) +
+               ", " + std::to_string(static_cast<int>(r.shard_types[k])) + "]";
+    }
+    detail::check(stormck_device_free(blocks));
+    detail::check(stormck_device_free(cs));
+    return out + "]}";
+}
+
 int main() {
     std::string ptr = TestPointerChecksum();
     std::string blob = TestMappingBlobToSlice();
@@ -277,11 +310,12 @@ int main() {
     TestRoutedLegs();
     TestCommitBatch();
     TestNewBlocksProduceConsistentResult();
-    std::printf("{\"pointer_block_test_sequence\": %s, \"blob_test_block\": %s, \"singularity\": %s, "
+    std::string multi = TestMerkleRootDevices();
+    std::printf("{\"multi\": %s, \"pointer_block_test_sequence\": %s, \"blob_test_block\": %s, \"singularity\": %s, "
                 "\"zero\": {\"prod\": {\"pointer\": %s, \"objectlist\": %s, \"spacelist\": %s, \"blob\": %s, "
                 "\"singularity\": %s}, \"test\": {\"pointer\": %s, \"objectlist\": %s, \"spacelist\": %s}}, "
                 "\"failures\": %d}\n",
-                ptr.c_str(), blob.c_str(), sing.c_str(), zero_cs<PointerBlock<>>().c_str(),
+                multi.c_str(), ptr.c_str(), blob.c_str(), sing.c_str(), zero_cs<PointerBlock<>>().c_str(),
                 zero_cs<ObjectListBlock<>>().c_str(), zero_cs<SpaceListBlock<>>().c_str(), zero_cs<BlobBlock>().c_str(),
                 zero_cs<SingularityBlock>().c_str(), zero_cs<PointerBlock<10>>().c_str(),
                 zero_cs<ObjectListBlock<10>>().c_str(), zero_cs<SpaceListBlock<10>>().c_str(), g_fail);

@@ -44,3 +44,13 @@ def test_cpp_mirror_runs_reference_tests():
     for tag, names in got["zero"].items():
         for name, v in names.items():
             assert hx(v) == hx(g["zero_block_checksums"][tag][name]), (tag, name)
+    # the one-process multi-GPU root (PlanShards / MerkleRootDevices) against the oracle
+    import numpy as np
+    from oracle import oracle as o
+    from storm_amd import dist as sdist
+    n_total, stride, world = 20000, 4096, 4
+    cs = o.checksum_batch(o.fill_synthetic(n_total, stride, 0), n_total, stride, stride, threads=8)
+    rows = [o.merkle_root(cs[lo:hi], lo, sdist.shard_node_addr_base(n_total, lo), 1)
+            for lo, hi in sdist.plan(n_total, world)]
+    assert [[hx(r[0]), r[1], r[2]] for r in got["multi"]["shard_roots"]] == [[r[0], r[1], r[3]] for r in rows]
+    assert hx(got["multi"]["root"]) == o.combine_roots(rows, 1, sdist.global_root_addr(n_total))[0]

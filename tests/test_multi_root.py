@@ -190,7 +190,8 @@ def _device_shards(n_total, world, devices, stride, length, first=0, streams=Fal
     (3, 40_000, 1024, 1024, 1200, False),
     (8, 25_000, 2048, 2048, 10, True),
     (8, 5, 512, 500, 10, False),      # shards of 0 and 1 leaves: Free and Leaf roots
-    (16, 12_345, 768, 728, 10, False),  # `-tags test` block sizes, more shards than the c4 world
+    (10, 12_345, 768, 728, 10, False),  # `-tags test` block sizes and fan-out: as many shards as it holds
+    (16, 12_345, 768, 728, 1200, True),  # more shards than the c4 world
 ])
 def test_one_device_holds_every_shard(dev, world, n_total, stride, length, fanout, streams):
     """Device list [0]: the library hashes each shard's blocks, builds each shard tree,
@@ -232,10 +233,22 @@ def test_precomputed_leaf_checksums(dev):
 
 
 @pytest.mark.gpu
+def test_more_shards_than_the_combining_node_holds(dev):
+    """The combining node is one pointer block: at most `fanout` shard roots."""
+    from storm_amd import _lib, multi
+    shards, ra = multi.plan(100, 11, [0])
+    with pytest.raises(_lib.StormckError, match="1..fanout"):
+        multi.merkle_root_multi(shards, REV, ra, 10)
+
+
+@pytest.mark.gpu
 def test_bad_shard_device_is_named(dev):
     from storm_amd import _lib, multi
     shards, ra = multi.plan(100, 2, [0])
-    shards[1].device = 4096
+    keep = torch.empty(100, dtype=torch.int64, device=dev)
+    for sh in shards:
+        multi.set_buffers(sh, keep[sh.leaf_addr_base:].data_ptr())
+    shards[1].device = 4096  # every shard is checked before any device work
     with pytest.raises(_lib.StormckError, match=r"shards\[1\].device = 4096"):
         multi.merkle_root_multi(shards, REV, ra)
     shards, ra = multi.plan(100, 2, [0])  # n > 0 without checksums

@@ -14,6 +14,7 @@
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <thread>
 #include <vector>
 
@@ -36,7 +37,8 @@ static double per_call(F f, int reps = 2000) {
     return r[4];
 }
 
-int main() {
+int main(int argc, char** argv) {
+    const bool only_c5 = argc > 1 && std::strcmp(argv[1], "c5") == 0;  // the c5-size A/B alone (traceable)
     if (stormck_init(0) != STORMCK_OK) {
         std::fprintf(stderr, "init: %s\n", stormck_last_error());
         return 1;
@@ -53,6 +55,8 @@ int main() {
     hipStream_t st;
     (void)hipStreamCreate(&st);
     hipPointerAttribute_t a;
+    uint32_t leg = 0;
+    if (!only_c5) {
     std::printf("hipPointerGetAttributes registered %.3f us\n", per_call([&] { (void)hipPointerGetAttributes(&a, rg); }));
     std::printf("hipPointerGetAttributes pageable   %.3f us\n", per_call([&] {
                     if (hipPointerGetAttributes(&a, pg) != hipSuccess) (void)hipGetLastError();
@@ -67,7 +71,6 @@ int main() {
     std::printf("hipStreamQuery created stream      %.3f us\n", per_call([&] { (void)hipStreamQuery(st); }));
 
     uint64_t out[n];
-    uint32_t leg = 0;
     for (void* base : {pg, rg}) {
         const char* what = base == pg ? "pageable  " : "registered";
         const double h = per_call([&] { (void)stormck_checksum_host_leg(base, blk, nullptr, blk, n, out, 1); });
@@ -93,6 +96,7 @@ int main() {
         std::printf("commit %s 3 x 32 KiB: host %.3f us  routed %.3f us  routed on a stream %.3f us (leg %u)  +%.3f us\n",
                     what, h, r, rs, leg, r - h);
     }
+    }  // !only_c5
     // two callers at once on the halves of a registered c5-size batch (1,202 x 32 KiB
     // slots), against one call on the whole: threads started beforehand and released
     // together, so only the library's handling of the second caller is timed
@@ -105,6 +109,66 @@ int main() {
         std::vector<uint64_t> o(nb);
         const double one = per_call([&] { (void)stormck_checksum_batch(c5, blk, nullptr, 31808, nb, o.data(), 0, &leg); }, 50);
         std::printf("c5-size batch, one caller: %.1f us (leg %u)\n", one, leg);
+        // the routed batch against the host leg it takes, alternating call by call (registered
+        // and pageable copies of the same slots): what routing costs at storm's commit size
+        {
+            void* c5p = std::aligned_alloc(4096, bytes);
+            std::memcpy(c5p, c5, bytes);
+            for (void* base : {c5, c5p}) {
+                std::vector<double> th, tr;
+                int seen[4] = {0, 0, 0, 0};  // legs the routed calls took
+                for (int rep = 0; rep < 201; ++rep) {
+                    double h = 0, r = 0;
+                    for (int k = 0; k < 2; ++k) {  // which goes first alternates: each follows the other
+                        const double t0 = now_us();
+                        if ((k ^ rep) & 1) {
+                            (void)stormck_checksum_batch(base, blk, nullptr, 31808, nb, o.data(), 0, &leg);
+                            r = now_us() - t0;
+                            ++seen[leg & 3];
+                        } else {
+                            (void)stormck_checksum_host_leg(base, blk, nullptr, 31808, nb, o.data(), 0);
+                            h = now_us() - t0;
+                        }
+                    }
+                    if (rep) {
+                        th.push_back(h);
+                        tr.push_back(r);
+                    }
+                }
+                std::sort(th.begin(), th.end());
+                std::sort(tr.begin(), tr.end());
+                std::printf("c5-size batch %s, alternating: host leg (pool) %.1f us  routed %.1f us  x%.3f  "
+                            "(routed legs: host %d, device %d, split %d)\n",
+                            base == c5 ? "registered" : "pageable  ", th[100], tr[100], tr[100] / th[100], seen[1],
+                            seen[2], seen[3]);
+            }
+            std::free(c5p);
+        }
+        // the same on the registered slots, five forms in rotation (each follows every other):
+        // which part of the routed call costs what at this size
+        {
+            const char* names[5] = {"host_leg(0)", "batch(0)", "host_leg(16)", "batch(16)", "batch(1)"};
+            std::vector<double> t[5];
+            for (int rep = 0; rep < 101; ++rep)
+                for (int j = 0; j < 5; ++j) {
+                    const int k = (j + rep) % 5;
+                    const double t0 = now_us();
+                    switch (k) {
+                        case 0: (void)stormck_checksum_host_leg(c5, blk, nullptr, 31808, nb, o.data(), 0); break;
+                        case 1: (void)stormck_checksum_batch(c5, blk, nullptr, 31808, nb, o.data(), 0, &leg); break;
+                        case 2: (void)stormck_checksum_host_leg(c5, blk, nullptr, 31808, nb, o.data(), 16); break;
+                        case 3: (void)stormck_checksum_batch(c5, blk, nullptr, 31808, nb, o.data(), 16, &leg); break;
+                        default: (void)stormck_checksum_batch(c5, blk, nullptr, 31808, nb, o.data(), 1, &leg); break;
+                    }
+                    if (rep) t[k].push_back(now_us() - t0);
+                }
+            std::printf("c5-size batch registered, rotating medians:");
+            for (int k = 0; k < 5; ++k) {
+                std::sort(t[k].begin(), t[k].end());
+                std::printf(" %s %.1f", names[k], t[k][t[k].size() / 2]);
+            }
+            std::printf(" us\n");
+        }
         for (int round = 0; round < 3; ++round) {
             std::atomic<int> go{0}, ready{0};
             double t_done[2] = {0, 0};
