@@ -457,7 +457,8 @@ uint32_t pipe_staging() {
 // 16 blocks per workgroup (one full chain wave) through 4-slot rings of 2 KiB chunks with
 // double-buffered stagers, for batches of 9..16 blocks per CU: measured no faster than
 // the register-quad kernel (2,049 / 3,072 / 4,096 blocks of 31,808 B: 33.2 / 35.3 / 38.1
-// against 34.7 / 35.0 / 35.1 us, profiles/r03c/), so off; probe knob STORMCK_WIDE16=1.
+// against 34.7 / 35.0 / 35.1 us in a round-3 probe; two 8-block rings per CU lost the same
+// way, profiles/r03_multi16/), so off; probe knob STORMCK_WIDE16=1.
 bool wide16_on() {
     static const bool on = [] {
         const char* e = STORMCK_KNOB("STORMCK_WIDE16");

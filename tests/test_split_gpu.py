@@ -494,3 +494,60 @@ def test_stream_forget():
     engine.stream_forget(s.cuda_stream)  # a stream with no slot: nothing to do
     torch.cuda.synchronize()
     assert int(out[0]) & ((1 << 64) - 1) == o.xxh64(bytes(stride))
+
+
+def test_routed_batch_on_managed_memory():
+    """hipMallocManaged memory has no hipHostGetDevicePointer mapping, so it is
+    classified as DMA-able host memory (the copy engine), not as registered memory the
+    kernels read in place. The routed batch forced onto the split (a slow host, frozen) and
+    the split leg with a fixed share hash it exactly."""
+    hip = ctypes.CDLL("libamdhip64.so.7")  # the runtime torch and the library share
+    n, stride = 2048, 32768
+    p = ctypes.c_void_p()
+    if hip.hipMallocManaged(ctypes.byref(p), ctypes.c_size_t(n * stride), ctypes.c_uint(1)) != 0 or not p.value:
+        pytest.skip("hipMallocManaged not available on this device")
+    try:
+        a = np.ctypeslib.as_array((ctypes.c_uint8 * (n * stride)).from_address(p.value))
+        a[:] = np.random.default_rng(77).integers(0, 256, size=n * stride, dtype=np.uint8)
+        want = o.checksum_batch(a, n, stride, stride, threads=8)
+        blocks.SetRouteRates(SLOW_HOST, freeze=True)
+        got, leg = blocks.ChecksumBatchLeg(a, n, stride, stride)
+        assert leg in (_lib.LEG_SPLIT, _lib.LEG_DEVICE) and np.array_equal(got, want), leg
+        got, done = blocks.ChecksumBatchSplit(a, n, stride, stride, devices=[0], device_blocks=n // 2)
+        assert done == n // 2 and np.array_equal(got, want)
+    finally:
+        blocks.SetRouteRates(None)
+        hip.hipFree(p)
+
+
+def test_fixed_splits_over_reversed_device_lists_finish():
+    """two fixed-mode splits at once over the same two devices listed in
+    opposite orders take the device workers in one global order, so neither waits for a
+    worker the other holds. Skipped on a one-GPU box (a device listed twice is listed once)."""
+    if torch.cuda.device_count() < 2:
+        pytest.skip("one visible device")
+    n, stride = 4096, 32768
+    regs = [_filled(n, stride, 90 + k) for k in range(2)]
+    try:
+        wants = [o.checksum_batch(r.a, n, stride, stride, threads=8) for r in regs]
+        errors = []
+
+        def call(k):
+            try:
+                for _ in range(10):
+                    got, done = blocks.ChecksumBatchSplit(regs[k].a, n, stride, stride, devices=[k, 1 - k],
+                                                          device_blocks=n - 100)
+                    assert done == n - 100 and np.array_equal(got, wants[k])
+            except Exception as e:  # reported below
+                errors.append(e)
+
+        ts = [threading.Thread(target=call, args=(k,), daemon=True) for k in range(2)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join(60)
+        assert not any(t.is_alive() for t in ts), "fixed splits over reversed device lists did not finish"
+        assert not errors, errors
+    finally:
+        for r in regs:
+            r.close()
