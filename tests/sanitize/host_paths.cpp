@@ -16,7 +16,8 @@
 //     (pageable and registered sources, parallel staging copies, both stages), the
 //     batched verify and the file read-verify reader threads, and four host threads
 //     calling the library at once; the split leg (host threads and the device worker
-//     on one call, fixed and balanced, checksum, verify and commit) from two callers.
+//     on one call, fixed and balanced, checksum, verify and commit) from two callers; the
+//     one-process multi-GPU root (stormck_merkle_root_multi, in-process RCCL) from two.
 // Exit status 0 = every check passed and the sanitizer reported nothing (sanitizer
 // reports abort the process: halt_on_error / -fno-sanitize-recover).
 #include <fcntl.h>
@@ -39,6 +40,12 @@
 
 extern "C" {
 uint64_t oracle_xxh64(const void* data, size_t n);
+void oracle_fill_synthetic(void* dst, size_t stride, size_t n, uint64_t first, uint64_t seed);
+size_t oracle_pointer_block_size(uint32_t fanout);
+void oracle_pack_pointer_block(uint8_t* dst, uint32_t fanout, const uint64_t* cs, const uint64_t* addr,
+                               const uint64_t* rev, const uint8_t* types, uint32_t m);
+size_t oracle_merkle_root(const uint64_t* leaf_cs, size_t n, uint64_t leaf_addr_base, uint64_t node_addr_base,
+                          uint64_t rev, uint32_t fanout, uint64_t root[3], uint8_t* root_type);
 int oracle_commit(uint8_t* arena, stormck_dirty_block* blocks, size_t n, uint64_t revision, uint64_t* last_allocated,
                   uint64_t* out_cs);
 }
@@ -92,6 +99,15 @@ static void argument_errors() {
     CHECK(stormck_key_tags_device(nullptr, 48, nullptr, nullptr, 48, 10, &out, nullptr) == STORMCK_EINVAL);
     CHECK(stormck_checksum_host(nullptr, 32, nullptr, 32, 4, &out) == STORMCK_EINVAL);
     CHECK(stormck_checksum_host_multi(small, 32, nullptr, 32, 2, &out, nullptr, 0) == STORMCK_EINVAL);
+    stormck_shard sh[2] = {};
+    stormck_pointer pr{};
+    uint8_t pt = 0;
+    const int dev0 = 0;
+    CHECK(stormck_shard_plan(10, 0, &dev0, 1, sh, nullptr) == STORMCK_EINVAL);
+    CHECK(stormck_shard_plan(10, 2, nullptr, 0, sh, nullptr) == STORMCK_EINVAL);
+    CHECK(stormck_merkle_root_multi(sh, 2, 1, 20, 1200, nullptr, &pt, nullptr, nullptr) == STORMCK_EINVAL);
+    CHECK(stormck_merkle_root_multi(sh, 0, 1, 20, 1200, &pr, &pt, nullptr, nullptr) == STORMCK_EINVAL);
+    CHECK(stormck_merkle_root_multi(sh, 2, 1, 20, 1, &pr, &pt, nullptr, nullptr) == STORMCK_EINVAL);
     const uint64_t addr_big[1] = {1ULL << 60}, addr0[1] = {0};
     const uint32_t len100[1] = {100};
     const uint64_t exp0[1] = {0};
@@ -496,6 +512,74 @@ static void concurrent_callers() {
     close(devnull);
 }
 
+// The one-process multi-GPU root (stormck_merkle_root_multi) on device 0, from two callers
+// at once (the library serialises the calls): five planned shards whose blocks the library
+// hashes, their trees, the one-rank RCCL gather and the combine, against the oracle's shard
+// trees and combining node.
+static void multi_root_paths() {
+    constexpr uint64_t n_total = 5003, stride = 4096, kShards = 5;
+    constexpr uint64_t seed = 0x53544F524DULL;
+    const int dev0 = 0;
+    std::vector<stormck_shard> plan(kShards);
+    uint64_t root_addr = 0;
+    CHECK(stormck_shard_plan(n_total, kShards, &dev0, 1, plan.data(), &root_addr) == STORMCK_OK &&
+          root_addr == 2 * n_total);
+    std::vector<uint8_t> host(n_total * stride);
+    oracle_fill_synthetic(host.data(), stride, n_total, 0, seed);
+    std::vector<uint64_t> cs(n_total);
+    for (uint64_t i = 0; i < n_total; ++i) cs[i] = oracle_xxh64(host.data() + i * stride, stride);
+    uint64_t rc[kShards], ra[kShards], rr[kShards];
+    uint8_t rt[kShards];
+    for (uint64_t s = 0; s < kShards; ++s) {
+        uint64_t root[3];
+        oracle_merkle_root(cs.data() + plan[s].leaf_addr_base, plan[s].n, plan[s].leaf_addr_base, plan[s].node_addr_base,
+                           1, STORMCK_POINTERS_PER_BLOCK, root, &rt[s]);
+        rc[s] = root[0];
+        ra[s] = root[1];
+        rr[s] = root[2];
+    }
+    std::vector<uint8_t> node(oracle_pointer_block_size(STORMCK_POINTERS_PER_BLOCK));
+    oracle_pack_pointer_block(node.data(), STORMCK_POINTERS_PER_BLOCK, rc, ra, rr, rt, kShards);
+    const uint64_t want = oracle_xxh64(node.data(), node.size());
+    void* d_blocks = nullptr;
+    CHECK(stormck_device_alloc(n_total * stride, &d_blocks) == STORMCK_OK);
+    CHECK(stormck_fill_synthetic_device(d_blocks, stride, n_total, 0, seed, nullptr) == STORMCK_OK);
+    CHECK(stormck_device_status(nullptr) == STORMCK_OK);
+    auto run = [&](int t) {
+        CHECK(stormck_init(0) == STORMCK_OK);
+        void* d_cs = nullptr;
+        CHECK(stormck_device_alloc(n_total * 8, &d_cs) == STORMCK_OK);
+        std::vector<stormck_shard> shards = plan;
+        for (stormck_shard& sh : shards) {
+            sh.d_blocks = static_cast<uint8_t*>(d_blocks) + sh.leaf_addr_base * stride;
+            sh.stride = stride;
+            sh.len = static_cast<uint32_t>(stride - 8 * t);  // the callers hash different lengths
+            sh.d_checksums = static_cast<uint64_t*>(d_cs) + sh.leaf_addr_base;
+        }
+        for (int it = 0; it < 3; ++it) {
+            stormck_pointer root{};
+            uint8_t type = 0;
+            std::vector<stormck_pointer> srows(kShards);
+            std::vector<uint8_t> stypes(kShards);
+            CHECK(stormck_merkle_root_multi(shards.data(), kShards, 1, root_addr, STORMCK_POINTERS_PER_BLOCK, &root, &type,
+                                            srows.data(), stypes.data()) == STORMCK_OK);
+            if (t == 0) {
+                CHECK(root.checksum == want && root.address == root_addr && root.birth_revision == 1 &&
+                      type == STORMCK_POINTER_BLOCK);
+                for (uint64_t s = 0; s < kShards; ++s)
+                    CHECK(srows[s].checksum == rc[s] && srows[s].address == ra[s] && stypes[s] == rt[s]);
+            } else {
+                CHECK(root.address == root_addr && type == STORMCK_POINTER_BLOCK && root.checksum != want);
+            }
+        }
+        CHECK(stormck_device_free(d_cs) == STORMCK_OK);
+    };
+    std::vector<std::thread> th;
+    for (int t = 0; t < 2; ++t) th.emplace_back(run, t);
+    for (auto& x : th) x.join();
+    CHECK(stormck_device_free(d_blocks) == STORMCK_OK);
+}
+
 int main() {
     std::setvbuf(stdout, nullptr, _IONBF, 0);  // progress lines reach a log file at once
     single_calls();
@@ -515,6 +599,8 @@ int main() {
     if (device) std::printf("concurrent callers: done\n");
     if (device) split_paths();
     if (device) std::printf("split leg: done\n");
+    if (device) multi_root_paths();
+    if (device) std::printf("multi-GPU root: done\n");
     stormck_shutdown();
     std::printf("%s: %d failure(s)\n", g_fail.load() ? "FAILED" : "ok", g_fail.load());
     return g_fail ? 1 : 0;
