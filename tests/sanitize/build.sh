@@ -21,12 +21,12 @@ for f in "${host[@]}"; do san+=(-Xarch_host "$f"); done
 HIPCC=${HIPCC:-/opt/rocm/bin/hipcc}
 CLANG=${CLANG:-/opt/rocm/llvm/bin/clang}
 # the library (device code for gfx950 untouched, host pass instrumented)
-"$HIPCC" --offload-arch=gfx950 -O1 -g -std=c++17 -fPIC "${san[@]}" -c -o "$out/stormck_$kind.o" \
+"$HIPCC" --offload-arch=gfx950 -O1 -gline-tables-only -std=c++17 -fPIC "${san[@]}" -c -o "$out/stormck_$kind.o" \
     "$R/storm_amd/csrc/stormck.hip"
 # the driver and the oracle (host only)
-"$CLANG" -x c++ -std=c++17 -O1 -g "${host[@]}" -D__HIP_PLATFORM_AMD__ -I /opt/rocm/include -I "$R/include" \
+"$CLANG" -x c++ -std=c++17 -O1 -gline-tables-only "${host[@]}" -D__HIP_PLATFORM_AMD__ -I /opt/rocm/include -I "$R/include" \
     -c -o "$out/host_paths_$kind.o" "$R/tests/sanitize/host_paths.cpp"
-"$CLANG" -x c -O1 -g "${host[@]}" -c -o "$out/oracle_$kind.o" "$R/oracle/xxh64_oracle.c"
+"$CLANG" -x c -O1 -gline-tables-only "${host[@]}" -c -o "$out/oracle_$kind.o" "$R/oracle/xxh64_oracle.c"
 "$HIPCC" --hip-link --offload-arch=gfx950 "${san[@]}" -o "$out/host_paths_$kind" \
     "$out/stormck_$kind.o" "$out/host_paths_$kind.o" "$out/oracle_$kind.o" -lpthread
 echo "$out/host_paths_$kind"
