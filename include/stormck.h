@@ -258,7 +258,8 @@ typedef struct stormck_shard {
     uint64_t node_addr_base; /* interior nodes: node_addr_base, +1, ... level by level, bottom-up */
     void* stream;            /* a stream of `device` the shard's work runs on, after what is already
                               * queued there (e.g. the launches that wrote d_checksums); NULL: the
-                              * library's own stream, which waits for no other stream */
+                              * library's own stream, which waits for no other stream. A stream of
+                              * another device is STORMCK_EINVAL */
     int32_t device;          /* HIP device index holding the shard */
     uint32_t len;            /* bytes hashed per block (when d_blocks is set) */
 } stormck_shard;

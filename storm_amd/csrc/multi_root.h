@@ -199,6 +199,13 @@ int merkle_root_multi(const stormck_shard* shards, uint32_t S, uint64_t rev, uin
         if (sh.n > 0 && !sh.d_checksums) return fail(STORMCK_EINVAL, who + ".d_checksums is null");
         if (sh.d_blocks && sh.n > 1 && sh.stride < sh.len)
             return fail(STORMCK_EINVAL, who + ": stride smaller than len (blocks overlap)");
+        if (sh.stream) {  // work enqueued on another device's stream would run there
+            hipDevice_t sd = -1;
+            HIP_TRY(hipStreamGetDevice(static_cast<hipStream_t>(sh.stream), &sd));
+            if (sd != sh.device)
+                return fail(STORMCK_EINVAL, who + ".stream belongs to device " + std::to_string(sd) + ", not " +
+                                                std::to_string(sh.device));
+        }
         const auto it = std::find(devs.begin(), devs.end(), sh.device);
         slot[s] = static_cast<uint32_t>(it - devs.begin());
         if (it == devs.end()) {
