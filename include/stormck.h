@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define STORMCK_ABI_VERSION 6
+#define STORMCK_ABI_VERSION 7
 
 #define STORMCK_OK 0
 #define STORMCK_EINVAL (-1)  /* bad argument (null pointer, n/len/stride out of range, ...) */
@@ -290,6 +290,16 @@ int stormck_shard_plan(uint64_t n_total, uint32_t n_shards, const int* devices, 
 int stormck_merkle_root_multi(const stormck_shard* shards, uint32_t n_shards, uint64_t rev, uint64_t root_addr,
                               uint32_t fanout, stormck_pointer* root, uint8_t* root_type, stormck_pointer* shard_roots,
                               uint8_t* shard_types);
+
+/* The gather layout stormck_merkle_root_multi uses for shards[0..n_shards), without a device
+ * (planning only; device indices are not checked against the visible devices):
+ * devices[0..*n_devices) = the shards' distinct devices in order of first appearance (the
+ * communicator's ranks), *rows = R, the most shards on one device (each device sends R root
+ * rows of 32 bytes; rows it does not fill stay zero), table_row[s] = the row of the gathered
+ * D x R table holding shard s's root (device slot * R + the shard's place among that device's
+ * shards). devices needs room for 64 entries. */
+int stormck_multi_layout(const stormck_shard* shards, uint32_t n_shards, int32_t* devices, uint32_t* n_devices,
+                         uint32_t* rows, uint32_t* table_row);
 
 /* ---- f2/f3: batched cold read + verify from a file device -------------------
  * storm's cold fetch reads a block from its Dev and verifies it

@@ -12,6 +12,6 @@ from them, and per-shard roots gathered over RCCL. Submodules:
 * ``build``    — in-tree hipcc build of libstormck.so
 """
 
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 __all__ = ["ABI_VERSION"]

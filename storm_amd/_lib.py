@@ -120,6 +120,8 @@ SIGNATURES = {
     "stormck_merkle_root_multi": (
         c_int, [POINTER(ShardStruct), c_uint32, c_uint64, c_uint64, c_uint32, POINTER(PointerStruct),
                 POINTER(c_uint8), POINTER(PointerStruct), POINTER(c_uint8)]),
+    "stormck_multi_layout": (
+        c_int, [POINTER(ShardStruct), c_uint32, c_void_p, POINTER(c_uint32), POINTER(c_uint32), c_void_p]),
     "stormck_read_verify_fd": (
         c_int, [c_int, c_void_p, c_void_p, c_uint64, c_uint64, c_void_p, c_uint64, c_void_p, c_uint32, c_void_p, c_void_p]),
     "stormck_key_tags_device": (c_int, [c_void_p, c_uint64, c_void_p, c_void_p, c_uint32, c_uint64, c_void_p, c_void_p]),

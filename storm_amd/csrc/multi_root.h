@@ -178,6 +178,39 @@ int shard_plan(uint64_t n_total, uint32_t n_shards, const int* devices, int n_de
     return STORMCK_OK;
 }
 
+// The gather layout of shards[0..S): the distinct devices in order of first appearance (the
+// communicator's ranks), shard s -> (device slot, its row among that device's shards), R =
+// the most shards on one device, and map[s] = slot * R + row, shard s's row of the gathered
+// D x R table. Needs no device (stormck_multi_layout exposes it to the CPU tests).
+struct MultiLayout {
+    std::vector<int> devs;
+    std::vector<uint32_t> slot, row, per_dev, map;
+    uint64_t R = 0;
+};
+
+int multi_layout(const stormck_shard* shards, uint32_t S, MultiLayout* L) {
+    L->devs.clear();
+    L->per_dev.clear();
+    L->slot.assign(S, 0);
+    L->row.assign(S, 0);
+    L->map.assign(S, 0);
+    for (uint32_t s = 0; s < S; ++s) {
+        const int dev = shards[s].device;
+        if (dev < 0) return fail(STORMCK_EINVAL, "shards[" + std::to_string(s) + "].device is negative");
+        const auto it = std::find(L->devs.begin(), L->devs.end(), dev);
+        L->slot[s] = static_cast<uint32_t>(it - L->devs.begin());
+        if (it == L->devs.end()) {
+            if (L->devs.size() == 64) return fail(STORMCK_EINVAL, "more than 64 devices");
+            L->devs.push_back(dev);
+            L->per_dev.push_back(0);
+        }
+        L->row[s] = L->per_dev[L->slot[s]]++;
+    }
+    L->R = S ? *std::max_element(L->per_dev.begin(), L->per_dev.end()) : 0;
+    for (uint32_t s = 0; s < S; ++s) L->map[s] = static_cast<uint32_t>(L->slot[s] * L->R + L->row[s]);
+    return STORMCK_OK;
+}
+
 int merkle_root_multi(const stormck_shard* shards, uint32_t S, uint64_t rev, uint64_t root_addr, uint32_t fanout,
                       stormck_pointer* root, uint8_t* root_type, stormck_pointer* shard_roots, uint8_t* shard_types) {
     if (!root || !root_type) return fail(STORMCK_EINVAL, "null root pointer");
@@ -187,10 +220,6 @@ int merkle_root_multi(const stormck_shard* shards, uint32_t S, uint64_t rev, uin
     if (rc) return rc;
     int count = 0;
     HIP_TRY(hipGetDeviceCount(&count));
-    // distinct devices in order of first appearance; shard s -> (device slot, row on it)
-    std::vector<int> devs;
-    std::vector<uint32_t> slot(S), row(S);
-    std::vector<uint32_t> per_dev;
     for (uint32_t s = 0; s < S; ++s) {
         const stormck_shard& sh = shards[s];
         const std::string who = "shards[" + std::to_string(s) + "]";
@@ -206,23 +235,20 @@ int merkle_root_multi(const stormck_shard* shards, uint32_t S, uint64_t rev, uin
                 return fail(STORMCK_EINVAL, who + ".stream belongs to device " + std::to_string(sd) + ", not " +
                                                 std::to_string(sh.device));
         }
-        const auto it = std::find(devs.begin(), devs.end(), sh.device);
-        slot[s] = static_cast<uint32_t>(it - devs.begin());
-        if (it == devs.end()) {
-            if (devs.size() == 64) return fail(STORMCK_EINVAL, "more than 64 devices");
-            hipDeviceProp_t prop;
-            HIP_TRY(hipGetDeviceProperties(&prop, sh.device));
-            if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
-                return fail(STORMCK_ENODEV, who + ".device is not gfx950: " + prop.gcnArchName);
-            devs.push_back(sh.device);
-            per_dev.push_back(0);
-        }
-        row[s] = per_dev[slot[s]]++;
     }
+    MultiLayout lay;
+    rc = multi_layout(shards, S, &lay);
+    if (rc) return rc;
+    for (const int dev : lay.devs) {
+        hipDeviceProp_t prop;
+        HIP_TRY(hipGetDeviceProperties(&prop, dev));
+        if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+            return fail(STORMCK_ENODEV, "device " + std::to_string(dev) + " is not gfx950: " + prop.gcnArchName);
+    }
+    const std::vector<int>& devs = lay.devs;
+    const std::vector<uint32_t>&slot = lay.slot, &row = lay.row, &map = lay.map;
     const uint64_t D = devs.size();
-    const uint64_t R = *std::max_element(per_dev.begin(), per_dev.end());
-    std::vector<uint32_t> map(S);  // shard s -> row of the gathered table
-    for (uint32_t s = 0; s < S; ++s) map[s] = static_cast<uint32_t>(slot[s] * R + row[s]);
+    const uint64_t R = lay.R;
     // device buffer layout, in u64 words: send [R*4] | recv [D*R*4] | map [S u32] | entries [S*3]
     // | types [S bytes] | node checksum [1] | root row [4] | the device's shard trees
     const uint64_t o_send = 0, o_recv = R * 4, o_map = o_recv + D * R * 4, o_ent = o_map + (S + 1) / 2,

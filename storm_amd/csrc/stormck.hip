@@ -1928,6 +1928,20 @@ int stormck_merkle_root_multi(const stormck_shard* shards, uint32_t n_shards, ui
     return merkle_root_multi(shards, n_shards, rev, root_addr, fanout, root, root_type, shard_roots, shard_types);
 }
 
+int stormck_multi_layout(const stormck_shard* shards, uint32_t n_shards, int32_t* devices, uint32_t* n_devices,
+                         uint32_t* rows, uint32_t* table_row) {
+    if (!shards || n_shards == 0) return fail(STORMCK_EINVAL, "shards: at least one");
+    if (!devices || !n_devices || !rows || !table_row) return fail(STORMCK_EINVAL, "null argument");
+    MultiLayout lay;
+    const int rc = multi_layout(shards, n_shards, &lay);
+    if (rc) return rc;
+    for (size_t d = 0; d < lay.devs.size(); ++d) devices[d] = lay.devs[d];
+    *n_devices = static_cast<uint32_t>(lay.devs.size());
+    *rows = static_cast<uint32_t>(lay.R);
+    for (uint32_t s = 0; s < n_shards; ++s) table_row[s] = lay.map[s];
+    return STORMCK_OK;
+}
+
 int stormck_read_verify_fd(int fd, const uint64_t* addresses, const uint32_t* lens, uint64_t n, uint64_t block_size,
                            void* dst, uint64_t dst_stride, const uint64_t* expected, uint32_t flags,
                            uint64_t* first_bad, uint64_t* n_bad) {

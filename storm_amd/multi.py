@@ -30,6 +30,18 @@ def plan(n_total: int, n_shards: int, devices: Sequence[int]) -> Tuple[List[Shar
     return list(arr), int(root_addr.value)
 
 
+def layout(shards: Sequence[ShardStruct]) -> Tuple[List[int], int, List[int]]:
+    """stormck_multi_layout: (the shards' distinct devices in order of first appearance, R =
+    the most shards on one device, each shard's row of the gathered D x R table). Needs no
+    device: the gather layout stormck_merkle_root_multi uses, for the CPU tests."""
+    n = len(shards)
+    arr = (ShardStruct * n)(*shards)
+    devs, tr = (ctypes.c_int32 * 64)(), (ctypes.c_uint32 * max(n, 1))()
+    nd, rows = ctypes.c_uint32(0), ctypes.c_uint32(0)
+    check(lib.stormck_multi_layout(arr, n, devs, ctypes.byref(nd), ctypes.byref(rows), tr))
+    return [int(devs[i]) for i in range(nd.value)], int(rows.value), [int(tr[i]) for i in range(n)]
+
+
 def _row(p: PointerStruct, t: int) -> Tuple[int, int, int, int]:
     return int(p.Checksum), int(p.Address), int(p.BirthRevision), int(t)
 
@@ -66,4 +78,4 @@ def set_buffers(sh: ShardStruct, d_checksums: int, d_blocks: int = 0, stride: in
     return sh
 
 
-__all__ = ["plan", "merkle_root_multi", "shard", "set_buffers", "_lib"]
+__all__ = ["plan", "layout", "merkle_root_multi", "shard", "set_buffers", "_lib"]

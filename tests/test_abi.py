@@ -40,7 +40,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version():
     from storm_amd import _lib, ABI_VERSION
-    assert _lib.lib.stormck_abi_version() == ABI_VERSION == 6
+    assert _lib.lib.stormck_abi_version() == ABI_VERSION == 7
 
 
 def test_library_build_id_is_the_tree_sources_hash():

@@ -124,6 +124,76 @@ def test_argument_errors():
         assert _lib.last_error(), name
 
 
+def _layout_model(devices_of_shards):
+    """What the gather must hold: ranks = distinct devices by first appearance, R = most shards
+    on one device, shard s in row (rank * R + its place among its device's shards)."""
+    devs, place, seen = [], [], {}
+    for d in devices_of_shards:
+        if d not in seen:
+            seen[d] = 0
+            devs.append(d)
+        place.append(seen[d])
+        seen[d] += 1
+    R = max(seen.values())
+    return devs, R, [devs.index(d) * R + p for d, p in zip(devices_of_shards, place)]
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_gather_layout_for_many_devices(seed):
+    """stormck_multi_layout (the layout stormck_merkle_root_multi gathers with) for 1-8
+    devices and up to 64 shards dealt in runs or interleaved: the C layout equals the model,
+    and a CPU rehearsal of the D-rank all-gather (each device's R send rows, zero where it has
+    fewer shards, concatenated in rank order) hands the combining node every shard's root in
+    shard order, so the global root is the oracle's for any dealing. The one step this does
+    not run is RCCL itself; one-GPU runs cover it at D = 1 (test_one_device_holds_every_shard)."""
+    from oracle import oracle as o
+    from storm_amd import multi
+    rng = np.random.default_rng(seed)
+    n_dev = int(rng.integers(1, 9))
+    pool = [int(d) for d in rng.choice(16, size=n_dev, replace=False)]
+    n_shards = int(rng.integers(1, 65))
+    n_total = int(rng.integers(n_shards, 40 * n_shards))
+    shards, root_addr = multi.plan(n_total, n_shards, pool)
+    if seed % 2:  # interleaved dealing instead of the planner's runs
+        for sh in shards:
+            sh.device = int(rng.choice(pool))
+    on = [sh.device for sh in shards]
+    devs, R, rows = multi.layout(shards)
+    assert (devs, R, rows) == _layout_model(on)
+    assert len(set(rows)) == n_shards and max(rows) < len(devs) * R
+    # rehearse the exchange with the oracle's shard roots
+    cs = o.checksum_batch(o.fill_synthetic(n_total, 64, 0), n_total, 64, 64, threads=4)
+    roots = [o.merkle_root(cs[sh.leaf_addr_base:sh.leaf_addr_base + sh.n], sh.leaf_addr_base, sh.node_addr_base,
+                           REV, 10) for sh in shards]
+    send = {d: [(0, 0, 0, 0)] * R for d in devs}
+    seen = {d: 0 for d in devs}
+    for sh, r in zip(shards, roots):
+        send[sh.device][seen[sh.device]] = r
+        seen[sh.device] += 1
+    table = [row for d in devs for row in send[d]]  # ncclAllGather: rank order
+    gathered = [table[rows[s]] for s in range(n_shards)]
+    assert gathered == roots
+    assert o.combine_roots(gathered, REV, root_addr, 1200) == o.combine_roots(roots, REV, root_addr, 1200)
+
+
+def test_gather_layout_errors():
+    from storm_amd import _lib, multi
+    from storm_amd._lib import ShardStruct
+    L = _lib.lib
+    sh = (ShardStruct * 2)()
+    d, nd, r, tr = (ctypes.c_int32 * 64)(), ctypes.c_uint32(), ctypes.c_uint32(), (ctypes.c_uint32 * 2)()
+    assert L.stormck_multi_layout(None, 2, d, ctypes.byref(nd), ctypes.byref(r), tr) == _lib.EINVAL
+    assert L.stormck_multi_layout(sh, 0, d, ctypes.byref(nd), ctypes.byref(r), tr) == _lib.EINVAL
+    assert L.stormck_multi_layout(sh, 2, None, ctypes.byref(nd), ctypes.byref(r), tr) == _lib.EINVAL
+    sh[1].device = -1
+    assert L.stormck_multi_layout(sh, 2, d, ctypes.byref(nd), ctypes.byref(r), tr) == _lib.EINVAL
+    assert "negative" in _lib.last_error()
+    many = [multi.shard(k, 1, 8, k, 1000 + k) for k in range(65)]
+    with pytest.raises(_lib.StormckError, match="64 devices"):
+        multi.layout(many)
+    assert multi.layout(many[:64])[:2] == (list(range(64)), 1)
+
+
 def _has_gpu():
     from storm_amd import _lib
     return _lib.device_count() > 0
