@@ -238,6 +238,25 @@ inline MultiRoot MerkleRootDevices(const std::vector<stormck_shard>& shards, uin
     return r;
 }
 
+// The layout MerkleRootDevices gathers with (stormck_multi_layout; needs no GPU): the shards'
+// distinct devices in order of first appearance (the RCCL ranks), the root rows each device
+// sends, and each shard's row of the gathered table.
+struct GatherLayout {
+    std::vector<int32_t> devices;
+    uint32_t rows = 0;
+    std::vector<uint32_t> table_row;
+};
+inline GatherLayout MultiLayout(const std::vector<stormck_shard>& shards) {
+    GatherLayout g;
+    g.devices.resize(64);
+    g.table_row.resize(shards.size());
+    uint32_t nd = 0;
+    detail::check(stormck_multi_layout(shards.data(), static_cast<uint32_t>(shards.size()), g.devices.data(), &nd,
+                                       &g.rows, g.table_row.data()));
+    g.devices.resize(nd);
+    return g;
+}
+
 // The device leg alone (stormck_checksum_host: H2D, kernel, D2H pipelined).
 inline std::vector<Hash> ChecksumBatchGPU(const void* base, size_t n, size_t stride, uint32_t length,
                                           const uint32_t* lens = nullptr) {

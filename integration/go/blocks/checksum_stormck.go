@@ -371,3 +371,23 @@ func MerkleRootDevices(shards []Shard, revision uint64, rootAddr BlockAddress) (
 	}
 	return root, shardRoots, shardTypes, nil
 }
+
+// GatherLayout returns the layout MerkleRootDevices gathers the shard roots with
+// (stormck_multi_layout): the shards' distinct devices in order of first appearance (the
+// RCCL ranks), the root rows each device sends, and each shard's row of the gathered table.
+// Needs no GPU.
+func GatherLayout(shards []Shard) ([]int32, int, []uint32, error) {
+	n := len(shards)
+	if n == 0 {
+		return nil, 0, nil, errors.New("GatherLayout: no shards")
+	}
+	devices := make([]int32, 64)
+	tableRow := make([]uint32, n)
+	var nDev, rows C.uint32_t
+	rc := C.stormck_multi_layout((*C.stormck_shard)(unsafe.Pointer(&shards[0])), C.uint32_t(n),
+		(*C.int32_t)(unsafe.Pointer(&devices[0])), &nDev, &rows, (*C.uint32_t)(unsafe.Pointer(&tableRow[0])))
+	if rc != C.STORMCK_OK {
+		return nil, 0, nil, stormckError(rc)
+	}
+	return devices[:nDev], int(rows), tableRow, nil
+}

@@ -276,6 +276,17 @@ static std::string TestMerkleRootDevices() {
     const uint64_t n_total = 20000, stride = 4096;
     auto [shards, root_addr] = PlanShards(n_total, 4, {0});
     EXPECT(root_addr == 2 * n_total && shards.size() == 4);
+    // the gather layout: one device sends all four rows; interleaved over three devices, ranks
+    // by first appearance and R = 2 rows each
+    const GatherLayout one = MultiLayout(shards);
+    EXPECT(one.devices == std::vector<int32_t>{0} && one.rows == 4 &&
+           one.table_row == std::vector<uint32_t>({0, 1, 2, 3}));
+    std::vector<stormck_shard> mixed = shards;
+    const int32_t on[4] = {3, 1, 3, 2};
+    for (int k = 0; k < 4; ++k) mixed[k].device = on[k];
+    const GatherLayout three = MultiLayout(mixed);
+    EXPECT(three.devices == std::vector<int32_t>({3, 1, 2}) && three.rows == 2 &&
+           three.table_row == std::vector<uint32_t>({0, 2, 1, 4}));
     void* blocks = nullptr;
     void* cs = nullptr;
     detail::check(stormck_device_alloc(n_total * stride, &blocks));
